@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Benchmark: reach·timesteps/s of the Muskingum routing hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): the full-Texas-scale synthetic network (190k reaches,
+~300 outlets, deepest flow path ~1500 reaches), deterministic run, 24 h at dt = 300 s
+(T = 288 steps), hourly lateral-inflow forcing (25 rows).  One bench "step" = one whole 24-h
+horizon routed by `mc_run` (forcing interpolation + network routing for all 288 timesteps),
+inputs and outputs resident in HBM.
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): the deterministic run does not shard
+ -- every rank routes its own independent replica (different forcing seed), no
+data-path collective; value = reach·timesteps of all ranks / max-over-ranks time ("weak").
+
+Prints ONE JSON line on rank 0 with `roofline` (HIP-event timed wavefront launches against the
+HBM roofline, algorithmic 72 B per reach·timestep) and `cpu_baseline` (the serial
+C transliteration of the reference loop, oracle/, timed on this host; rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tx-fast-hydrology_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+BYTES_PER_UNIT = 72.0        # 7 f64 reads + 2 f64 writes per reach·timestep
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=190_000)
+    ap.add_argument("--basins", type=int, default=300)
+    ap.add_argument("--depth", type=int, default=1500)
+    ap.add_argument("--T", type=int, default=288)
+    ap.add_argument("--dt", type=float, default=300.0)
+    ap.add_argument("--slots", type=int, default=0)
+    ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--timing-runs", type=int, default=3)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+
+    from oracle import oracle as orc  # noqa: F401  (cpu_baseline leg only)
+    from tx_fast_hydrology_amd import engine, synthetic
+
+    # ---- workload -------------------------------------------------------------------------
+    t_setup = time.time()
+    end = synthetic.river_network(args.n, args.basins, args.depth, np.random.default_rng(0))
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=0)
+    start = np.arange(n, dtype=np.int64)
+    indeg = np.bincount(end, minlength=n) - (end == start)
+    heads = start[indeg == 0]
+    dt = args.dt
+    alpha = (dt - 2 * K * X) / (2 * K * (1 - X) + dt)          # muskingum.py:332-347
+    beta = (dt + 2 * K * X) / (2 * K * (1 - X) + dt)
+    chi = (2 * K * (1 - X) - dt) / (2 * K * (1 - X) + dt)
+    gamma = dt / (K * (1 - X) + dt / 2)
+    i0 = np.zeros(n)
+    np.add.at(i0, end, o0)                                      # muskingum.py:416-417
+    rows = int(np.ceil(args.T * dt / 3600.0)) + 1
+    xp_ns, fp = synthetic.forcing(n, rows=rows, seed=1 + rank)
+    xp = xp_ns.astype(float)
+    x = xp[0] + dt * 1e9 * np.arange(1, args.T + 1)
+
+    net = engine.RoutingNet(end, indeg, heads, slots=args.slots, tile=args.tile)
+    net.set_coeffs(alpha, beta, chi, gamma)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fp)
+    info = net.info
+    setup_s = time.time() - t_setup
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- warmup + timed region -------------------------------------------------------------
+    for _ in range(args.warmup):
+        net.run(x)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        net.run(x)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    units = float(n) * args.T * args.steps * world
+    value = units / elapsed
+
+    # ---- roofline of the dominant kernel (HIP events around every wavefront launch) --------
+    net.reset_timing()
+    net.set_timing(True)
+    for _ in range(args.timing_runs):
+        net.run(x)
+    net.synchronize()
+    tm = net.timing()
+    net.set_timing(False)
+    launch_ms = tm["kernel_ms"] / max(tm["launches"], 1)
+    bytes_per_launch = BYTES_PER_UNIT * n * args.T * args.timing_runs / max(tm["launches"], 1)
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "kernel": "wavefront_det", "launches_per_step": tm["launches"] / args.timing_runs,
+                "avg_launch_us": round(launch_ms * 1e3, 3),
+                "kernel_ms_per_step": round(tm["kernel_ms"] / args.timing_runs, 4)}
+
+    # ---- CPU baseline (serial transliteration of the reference loop, rank 0 at N=1) --------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        o_s, i_s = o0.copy(), i0.copy()
+        reps, t_cpu = 0, 0.0
+        while t_cpu < args.cpu_seconds or reps == 0:
+            c0 = time.perf_counter()
+            orc.simulate(start, end, indeg, alpha, beta, chi, gamma, o_s, i_s, x, xp, fp,
+                         keep_outputs=False)
+            t_cpu += time.perf_counter() - c0
+            reps += 1
+        cpu = {"value": float(n) * args.T * reps / t_cpu, "unit": "reach·timesteps/s",
+               "cores": 1, "kind": "port",
+               "sample": f"{reps} x full 24 h horizon (T={args.T}) on the same {n}-reach "
+                         f"network, serial C (-O3 -ffp-contract=off), {t_cpu:.1f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "reach·timesteps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "texas-det (BASELINE configs[1]): full-Texas synthetic "
+                                   "network, deterministic, 24 h @ 300 s",
+                       "n_reaches": n, "outlets": int((end == start).sum()),
+                       "max_height": info["max_height"], "T": args.T, "dt_s": dt,
+                       "forcing_rows": rows, "parallelism": f"replicas x{world}",
+                       "slots": info["slots"], "tile": info["tile"], "nwg": info["nwg"],
+                       "schedule_ticks": info["gmax"] + args.T, "setup_s": round(setup_s, 2)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = value / cpu["value"]
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

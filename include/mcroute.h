@@ -1,0 +1,140 @@
+/*
+ * mcroute -- MI355X (gfx950) Muskingum routing engine, C ABI.
+ *
+ * Drop-in boundary for the hot path of future-water/tx-fast-hydrology.  The reference calls a
+ * module-level numba kernel positionally (muskingum.py:10 import, muskingum.py:456-457 call):
+ *
+ *     i_t_next, o_t_next = _ax_bu(sub_startnodes, endnodes, alpha, beta, chi, gamma,
+ *                                 i_t_prev, o_t_prev, p_t_next, indegree)   # nutils.py:64-89
+ *
+ * and drives it once per timestep from Muskingum.step_iter / simulate_iter
+ * (muskingum.py:435-465, 499-536).  This library replaces that call: `mc_ax_bu_f64` is the
+ * stateless mirror of `_ax_bu`; the `mc_net_*` session keeps topology, coefficients, state,
+ * forcing and outputs resident in HBM and runs whole horizons (`mc_run`).
+ *
+ * Conventions
+ *   - plain pointers and sizes; all arrays are C-contiguous, int64 indices, float64 values, in
+ *     the CALLER's reach order (the order of `endnodes`), exactly like the reference arrays;
+ *   - every function returns MC_OK (0) or a negative MC_E_* code; `mc_last_error()` returns a
+ *     thread-local message for the last failure.  No C++ exception crosses the ABI;
+ *   - the library never retains a caller pointer past the call;
+ *   - a session handle is not thread-safe: use one thread per handle (or lock externally);
+ *   - results are bit-identical to the reference's float64 arithmetic (same association, no
+ *     FMA contraction, inflows summed in the reference's finalisation order).
+ */
+#ifndef MCROUTE_H
+#define MCROUTE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MC_OK 0
+#define MC_E_INVALID (-1)   /* bad argument (null pointer, size, range) */
+#define MC_E_TOPOLOGY (-2)  /* topology cannot be scheduled (see mc_last_error) */
+#define MC_E_HIP (-3)       /* HIP runtime error (no device, launch failure, ...) */
+#define MC_E_NOMEM (-4)     /* host or device allocation failed */
+#define MC_E_STATE (-5)     /* call out of order (e.g. mc_run before mc_load_forcing) */
+
+typedef struct mc_plan_params {
+    int32_t slots;    /* reaches per workgroup (multiple of 64, <= 1024); 0 = default */
+    int32_t tile;     /* ticks per launch = slack of a cross-cluster edge; 0 = default */
+    int32_t ext_cap;  /* max cross-cluster inputs per workgroup; 0 = default */
+} mc_plan_params;
+
+typedef struct mc_plan_info {
+    int64_t n;            /* reaches */
+    int64_t n_routed;     /* reaches the reference walk processes (others keep o = 0) */
+    int64_t n_clusters;
+    int64_t n_cross;      /* cross-cluster edges */
+    int64_t nslots;       /* nwg * slots */
+    int32_t nwg;          /* workgroups */
+    int32_t slots;
+    int32_t tile;
+    int32_t gmax;         /* schedule length without the horizon: ticks = gmax + T */
+    int32_t max_height;   /* longest upstream path (network depth - 1) */
+    int32_t max_ext_wg;
+} mc_plan_info;
+
+/* Thread-local description of the last error (never NULL). */
+const char* mc_last_error(void);
+/* ABI version (major * 100 + minor). */
+int mc_version(void);
+
+/* ---- host-only topology compiler (no GPU needed) --------------------------------------- */
+/* Replays the reference walk (nutils.py:72-88) and builds the space-time schedule.
+ * headwaters = the reference's sub_startnodes = startnodes[indegree == 0] (muskingum.py:444). */
+int mc_plan_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                   const int64_t* headwaters, int64_t n_head, const mc_plan_params* params,
+                   void** plan_out);
+int mc_plan_get_info(const void* plan, mc_plan_info* info);
+/* Any output pointer may be NULL.  rank/pos: [n]; G/slot_reach: [nslots]. */
+int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
+                   int64_t* slot_reach);
+int mc_plan_destroy(void* plan);
+
+/* ---- stateless mirror of nutils._ax_bu (nutils.py:64-89) -------------------------------- */
+/* One timestep.  Same arguments and meaning as the reference; outputs are caller-allocated
+ * (the reference returns fresh arrays).  The compiled topology is cached between calls. */
+int mc_ax_bu_f64(int64_t n, const int64_t* headwaters, int64_t n_head, const int64_t* endnodes,
+                 const double* alpha, const double* beta, const double* chi, const double* gamma,
+                 const double* i_t_prev, const double* o_t_prev, const double* q_t_next,
+                 const int64_t* indegree, double* i_t_next_out, double* o_t_next_out);
+
+/* ---- device-resident session ------------------------------------------------------------ */
+/* Creates a session on the calling thread's current HIP device.  params may be NULL. */
+int mc_net_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                  const int64_t* headwaters, int64_t n_head, const mc_plan_params* params,
+                  void** net_out);
+int mc_net_destroy(void* net);
+int mc_net_get_info(const void* net, mc_plan_info* info);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL = the session's own. */
+int mc_net_set_stream(void* net, void* hip_stream);
+
+/* Coefficients alpha, beta, chi, gamma (muskingum.py:332-360), caller order. */
+int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
+                  const double* gamma);
+/* State (o_t_next, i_t_next) of the model, caller order. */
+int mc_set_state(void* net, const double* o_t_next, const double* i_t_next);
+int mc_get_state(void* net, double* o_t_next, double* i_t_next);
+
+/* One timestep with lateral inflow q (muskingum.py:435-465 -> nutils.py:64-89).  If o_prev and
+ * i_prev are non-NULL they replace the session state first.  Writes the new (i, o) and keeps
+ * them as the session state. */
+int mc_step(void* net, const double* o_prev, const double* i_prev, const double* q_t_next,
+            double* i_t_next_out, double* o_t_next_out);
+
+/* Forcing table for mc_run: n_rows timestamps xp (float64 ns, sorted) and values fp
+ * [n_rows][n] (the simulate_iter DataFrame, muskingum.py:526-531). */
+int mc_load_forcing(void* net, int64_t n_rows, const double* xp, const double* fp);
+/* Horizon of T steps from the session state, all on the device: step t interpolates the
+ * forcing at x[t] = float(next_timestep.value) (muskingum.py:528-531) and routes the network.
+ * Outputs stay resident (reach-major); the session state becomes the state after step T-1. */
+int mc_run(void* net, int64_t T, const double* x);
+/* Copy steps [t0, t1) of the last mc_run to the host, step-major: out_o[t - t0][j]. */
+int mc_fetch_outputs(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i);
+/* Copy the full series of the last mc_run, reach-major: out_o[j][t] (either may be NULL). */
+int mc_fetch_series(void* net, double* out_o, double* out_i);
+/* Convenience: mc_load_forcing + mc_run + mc_fetch_outputs(0, T). */
+int mc_simulate(void* net, int64_t T, const double* x, int64_t n_rows, const double* xp,
+                const double* fp, double* out_o, double* out_i);
+
+/* Device pointers of the resident reach-major outputs of the last mc_run ([n][T] each). */
+int mc_output_device_ptrs(void* net, void** o_dev, void** i_dev, int64_t* T);
+/* Blocks until the session's stream is idle. */
+int mc_synchronize(void* net);
+
+/* Per-launch HIP-event timing of the wavefront kernel (off by default).  kernel_ms is the sum
+ * of the wavefront launches of all mc_run calls since the last reset, run_ms the sum of whole
+ * mc_run device times. */
+int mc_set_timing(void* net, int enable);
+int mc_get_timing(void* net, double* kernel_ms, int64_t* launches, double* run_ms);
+int mc_reset_timing(void* net);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCROUTE_H */

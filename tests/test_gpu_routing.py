@@ -1,0 +1,219 @@
+"""GPU parity of the HIP routing path (libmcroute.so) against the oracle and the golden vectors.
+
+Every discharge comparison is BIT-EXACT (np.array_equal on float64): the kernel keeps the
+reference's association, FMA contraction is off, and inflows are summed in the reference's
+finalisation order.  The north-star tolerance (1e-6 relative) is therefore not needed here.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tx_fast_hydrology_amd import engine, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(endnodes, K, X, dt, o0=None, seed=0):
+    n = endnodes.size
+    start = np.arange(n, dtype=np.int64)
+    indeg = orc.compute_indegree(start, endnodes)
+    coef = orc.muskingum_coeffs(K, X, dt)
+    if o0 is None:
+        o0 = np.random.default_rng(seed).uniform(0.5, 5.0, n)
+    i0 = orc.init_inflows(start, endnodes, o0)
+    heads = start[indeg == 0]
+    return indeg, heads, coef, o0, i0
+
+
+def _net(endnodes, indeg, heads, coef, o0, i0, **kw):
+    net = engine.RoutingNet(endnodes, indeg, heads, **kw)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    return net
+
+
+# ---------------------------------------------------------------- stateless _ax_bu mirror
+def test_ax_bu_golden_edge_cases(golden):
+    g = golden("g8_ax_bu_edge.npz")
+    for name in g["names"]:
+        a = g[f"{name}_args"]
+        i_n, o_n = engine.ax_bu(g[f"{name}_heads"], g[f"{name}_endnodes"], a[0], a[1], a[2],
+                                a[3], a[4], a[5], a[6], g[f"{name}_indegree"])
+        assert np.array_equal(i_n, g[f"{name}_i"]), name
+        assert np.array_equal(o_n, g[f"{name}_o"]), name
+
+
+def test_ax_bu_dt_change_sequence(golden):
+    g = golden("g6_dt_change.npz")
+    end = g["endnodes"]
+    indeg, heads, coef, _, _ = _model(end, g["K"], g["X"], 3600.0)
+    o = g["o0"].copy()
+    i = orc.init_inflows(np.arange(end.size), end, o)
+    for k, td in enumerate(g["td"]):
+        if td > 0 and float(td) != 3600.0:
+            coef = orc.muskingum_coeffs(g["K"], g["X"], float(td))
+        i, o = engine.ax_bu(heads, end, *coef, i, o, g["q"][k], indeg)
+        assert np.array_equal(o, g["o"][k]) and np.array_equal(i, g["i"][k])
+
+
+# ---------------------------------------------------------------- fused horizon (mc_run)
+def _golden_run(g, n_steps=None, **kw):
+    end = g["endnodes"]
+    indeg, heads, coef, _, i0 = _model(end, g["K"], g["X"], float(g["dt"]))
+    xs = orc.step_times(int(g["start_ns"]), int(float(g["dt"]) * 1e9), int(g["idx_ns"].max()))
+    if n_steps is not None:
+        xs = xs[:n_steps]
+    net = _net(end, indeg, heads, coef, g["o0"], i0, **kw)
+    return net.simulate(xs.astype(float), g["idx_ns"].astype(float), g["forcing"])
+
+
+@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=1), dict(slots=64, tile=5),
+                                dict(slots=1024, tile=64)])
+def test_run_golden_ynet(golden, kw):
+    g = golden("g1_ynet.npz")
+    o, i = _golden_run(g, **kw)
+    assert np.array_equal(o, g["o"]) and np.array_equal(i, g["i"])
+
+
+@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=8), dict(slots=512, tile=32)])
+def test_run_golden_huc8_every_step(golden, kw):
+    g = golden("g2_huc8.npz")
+    o, i = _golden_run(g, **kw)
+    assert o.shape == (288, 1000)
+    for t in range(288):
+        assert hashlib.sha256(o[t].tobytes()).digest() == g["o_sha"][t].tobytes(), t
+        assert hashlib.sha256(i[t].tobytes()).digest() == g["i_sha"][t].tobytes(), t
+
+
+def test_run_golden_confluence_order(golden):
+    g = golden("g3_confluence.npz")
+    o, i = _golden_run(g, n_steps=int(g["n_steps"]), slots=64, tile=4)
+    assert np.array_equal(o, g["o"]) and np.array_equal(i, g["i"])
+
+
+def _random_case(n, seed, p_chain, outlets):
+    rng = np.random.default_rng(seed)
+    end = synthetic.random_forest(n, outlets, rng, p_chain=p_chain)
+    K = rng.uniform(1800.0, 7200.0, n)
+    X = rng.uniform(0.1, 0.4, n)
+    return end, K, X
+
+
+@pytest.mark.parametrize("n,p_chain,slots,tile,T", [
+    (1, 0.0, 64, 32, 7), (2, 1.0, 64, 1, 3), (300, 0.9, 64, 4, 50), (3000, 0.95, 256, 32, 96),
+    (5000, 0.5, 1024, 16, 40), (2000, 0.99, 128, 64, 1), (800, 0.9, 64, 128, 20)])
+def test_run_random_vs_oracle(n, p_chain, slots, tile, T):
+    end, K, X = _random_case(n, n + T, p_chain, max(1, n // 500))
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=n)
+    xp, fp = synthetic.forcing(n, rows=5, seed=n)
+    xp = xp.astype(float)
+    x = xp[0] - 600e9 + 300e9 * np.arange(1, T + 1)    # spans clamped and interpolated steps
+    want_o, want_i, fo, fi = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=tile)
+    got_o, got_i = net.simulate(x, xp, fp)
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+    so, si = net.get_state()
+    assert np.array_equal(so, fo) and np.array_equal(si, fi)
+    O, I = net.fetch_series()
+    assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
+
+
+def test_run_continuation_equals_one_long_run():
+    n, T = 4000, 60
+    end, K, X = _random_case(n, 7, 0.95, 3)
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0)
+    xp, fp = synthetic.forcing(n, rows=4, seed=3)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=256, tile=16)
+    full_o, full_i = net.simulate(x, xp, fp)
+    net.set_state(o0, i0)
+    net.run(x[:23])
+    a_o, a_i = net.fetch_outputs()
+    net.run(x[23:])
+    b_o, b_i = net.fetch_outputs()
+    assert np.array_equal(np.vstack([a_o, b_o]), full_o)
+    assert np.array_equal(np.vstack([a_i, b_i]), full_i)
+
+
+def test_step_api_matches_run():
+    n, T = 2500, 12
+    end, K, X = _random_case(n, 11, 0.9, 2)
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 900.0)
+    rng = np.random.default_rng(5)
+    qs = rng.gamma(2.0, 0.5, size=(T, n))
+    net = _net(end, indeg, heads, coef, o0, i0, slots=128, tile=8)
+    o, i = o0.copy(), i0.copy()
+    for t in range(T):
+        i_w, o_w = orc.ax_bu(heads, end, *coef, i, o, qs[t], indeg)
+        i_g, o_g = net.step(qs[t], o_t_prev=o, i_t_prev=i)
+        assert np.array_equal(o_g, o_w) and np.array_equal(i_g, i_w)
+        o, i = o_w, i_w
+    # state-carrying form (no explicit previous state)
+    net.set_state(o0, i0)
+    o, i = o0.copy(), i0.copy()
+    for t in range(T):
+        i, o = orc.ax_bu(heads, end, *coef, i, o, qs[t], indeg)
+        i_g, o_g = net.step(qs[t])
+        assert np.array_equal(o_g, o) and np.array_equal(i_g, i)
+
+
+def test_unrouted_reaches_cycle_and_bad_indegree(golden):
+    g = golden("g8_ax_bu_edge.npz")
+    for name in ("cycle", "bigindeg"):
+        end = g[f"{name}_endnodes"]
+        indeg = g[f"{name}_indegree"]
+        heads = g[f"{name}_heads"]
+        a = g[f"{name}_args"]
+        net = engine.RoutingNet(end, indeg, heads, slots=64, tile=3)
+        net.set_coeffs(a[0], a[1], a[2], a[3])
+        i_g, o_g = net.step(a[6], o_t_prev=a[5], i_t_prev=a[4])
+        assert np.array_equal(o_g, g[f"{name}_o"]) and np.array_equal(i_g, g[f"{name}_i"])
+        # multi-step horizon through the same topology
+        xp = np.array([0.0, 1.0])
+        fp = np.vstack([a[6], a[6] * 2.0])
+        x = np.array([0.25, 0.5, 0.75, 1.5])
+        want_o, want_i, _, _ = orc.simulate(np.arange(end.size), end, indeg, a[0], a[1], a[2],
+                                            a[3], a[5], a[4], x, xp, fp)
+        net.set_state(a[5], a[4])
+        got_o, got_i = net.simulate(x, xp, fp)
+        assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+
+
+def test_texas_scale_bitexact_vs_oracle():
+    """Full Texas-size network (190k reaches, depth ~1500), 24 h @ 300 s: every output of every
+    step bit-identical to the serial oracle."""
+    end = synthetic.texas(seed=0)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=0)
+    indeg, heads, coef, _, i0 = _model(end, K, X, 300.0)
+    i0 = orc.init_inflows(np.arange(n), end, o0)
+    xp, fp = synthetic.forcing(n, rows=25, seed=1)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 289)
+    want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0)
+    got_o, got_i = net.simulate(x, xp, fp)
+    assert np.array_equal(got_o, want_o)
+    assert np.array_equal(got_i, want_i)
+
+
+def test_steady_state_mass_balance():
+    """KAT: constant lateral inflow -> every outlet's outflow -> sum of its basin's q."""
+    end = synthetic.river_network(3000, 4, 60, np.random.default_rng(2))
+    n = end.size
+    indeg, heads, coef, _, _ = _model(end, np.full(n, 1800.0), np.full(n, 0.2), 600.0)
+    q = np.random.default_rng(3).uniform(0.1, 1.0, n)
+    net = _net(end, indeg, heads, coef, np.zeros(n), np.zeros(n))
+    net.load_forcing(np.array([0.0]), q[None, :])
+    net.run(np.arange(1, 4001, dtype=float))
+    o, _ = net.get_state()
+    # basin sums
+    root = np.arange(n)
+    for _ in range(200):
+        root = end[root]
+    outlets = np.flatnonzero(end == np.arange(n))
+    for r in outlets:
+        np.testing.assert_allclose(o[r], q[root == r].sum(), rtol=1e-10)

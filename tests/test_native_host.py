@@ -1,0 +1,116 @@
+"""Host-side checks of libmcroute.so that need no GPU: the library loads, exports every symbol
+declared in include/mcroute.h, and the topology compiler (plan.cpp) honours its invariants."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tx_fast_hydrology_amd import _native as nat
+from tx_fast_hydrology_amd.engine import Plan
+from tx_fast_hydrology_amd import synthetic
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "mcroute.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    L = nat.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(nat.SIGNATURES), set(syms) ^ set(nat.SIGNATURES)
+    assert L.mc_version() == 100
+
+
+def _replay_rank(heads, endnodes, indegree):
+    """Independent replay of nutils.py:72-88 recording the processing order."""
+    deg = list(indegree)
+    rank = [-1] * len(endnodes)
+    r = 0
+    for s in heads:
+        while deg[s] == 0:
+            rank[s] = r
+            r += 1
+            e = endnodes[s]
+            deg[e] -= 1
+            s = e
+    return np.array(rank)
+
+
+def _check_plan(endnodes, indegree, heads, **kw):
+    P = Plan(endnodes, indegree, heads, **kw)
+    info = P.info
+    ex = P.export()
+    n = len(endnodes)
+    assert np.array_equal(ex["rank"], _replay_rank(heads, endnodes, indegree))
+    assert info["n_routed"] == int((ex["rank"] >= 0).sum())
+    # every reach has exactly one slot, slots map back
+    assert np.array_equal(ex["slot_reach"][ex["pos"]], np.arange(n))
+    G = np.full(n, -1)
+    G[ex["slot_reach"][ex["slot_reach"] >= 0]] = ex["G"][ex["slot_reach"] >= 0]
+    slots = info["slots"]
+    tile = info["tile"]
+    wg = ex["pos"] // slots
+    # schedule: consumer runs after producer; same workgroup & unit slack, or slack >= tile
+    rank = ex["rank"]
+    for u in range(n):
+        e = endnodes[u]
+        if rank[u] < 0 or e == u:
+            continue
+        slack = G[e] - G[u]
+        assert slack >= 1
+        assert slack == 1 or slack >= tile, (u, e, slack)
+        if slack == 1 and tile > 1:
+            assert wg[u] == wg[e]
+    assert info["gmax"] == G.max() if n else True
+    return info, ex
+
+
+@pytest.mark.parametrize("slots,tile", [(64, 1), (64, 8), (256, 32), (1024, 64)])
+def test_plan_invariants_random(slots, tile):
+    rng = np.random.default_rng(slots + tile)
+    for trial in range(3):
+        n = int(rng.integers(1, 3000))
+        end = synthetic.random_forest(n, int(rng.integers(1, 5)), rng, p_chain=0.9)
+        deg = orc.compute_indegree(np.arange(n), end)
+        heads = np.flatnonzero(deg == 0)
+        _check_plan(end, deg, heads, slots=slots, tile=tile)
+
+
+def test_plan_golden_edge_topologies(golden):
+    g = golden("g8_ax_bu_edge.npz")
+    for name in g["names"]:
+        _check_plan(g[f"{name}_endnodes"], g[f"{name}_indegree"], g[f"{name}_heads"])
+
+
+def test_plan_deep_chain_and_capacity():
+    n = 5000
+    end = np.arange(1, n + 1)
+    end[-1] = n - 1                       # one 5000-reach chain
+    deg = orc.compute_indegree(np.arange(n), end)
+    info, ex = _check_plan(end, deg, np.flatnonzero(deg == 0), slots=256, tile=16)
+    assert info["max_height"] == n - 1
+    assert info["nwg"] >= n // 256
+    assert info["gmax"] >= n - 1
+
+
+def test_plan_rejects_bad_input():
+    with pytest.raises(nat.TopologyError):
+        Plan(np.array([0, 5]), np.array([1, 0]), np.array([1]))       # endnode out of range
+    with pytest.raises(nat.TopologyError):
+        Plan(np.array([1, 1]), np.array([0, 0]), np.array([0, 0]))    # duplicate headwater
+    with pytest.raises(nat.TopologyError):                            # indegree too small
+        Plan(np.array([2, 2, 2]), np.array([0, 0, 1]), np.array([0, 1]))
+
+
+def test_plan_empty_network():
+    P = Plan(np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64))
+    assert P.info["n"] == 0

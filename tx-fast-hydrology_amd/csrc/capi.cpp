@@ -1,0 +1,629 @@
+// C ABI of the routing engine (include/mcroute.h): sessions, device buffers, launch sequencing.
+#include "mcroute.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "plan.hpp"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Fail : std::runtime_error {
+    int code;
+    Fail(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPC(expr)                                                                   \
+    do {                                                                             \
+        hipError_t e_ = (expr);                                                      \
+        if (e_ != hipSuccess)                                                        \
+            throw Fail(e_ == hipErrorOutOfMemory ? MC_E_NOMEM : MC_E_HIP,            \
+                       std::string(#expr) + ": " + hipGetErrorString(e_));           \
+    } while (0)
+
+#define REQUIRE(cond, msg)                                                           \
+    do {                                                                             \
+        if (!(cond)) throw Fail(MC_E_INVALID, msg);                                  \
+    } while (0)
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return MC_OK;
+    } catch (const Fail& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "host allocation failed";
+        return MC_E_NOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return MC_E_INVALID;
+    } catch (...) {
+        g_err = "unknown error";
+        return MC_E_INVALID;
+    }
+}
+
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    void reserve(size_t k) {
+        if (k <= cap && p) return;
+        release();
+        HIPC(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(k, 1) * sizeof(T)));
+        cap = std::max<size_t>(k, 1);
+    }
+    void upload(const T* src, size_t k, hipStream_t s) {
+        reserve(k);
+        if (k) HIPC(hipMemcpyAsync(p, src, k * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+};
+
+mcr::PlanParams to_params(const mc_plan_params* pp) {
+    mcr::PlanParams p;
+    if (pp) {
+        if (pp->slots) p.slots = pp->slots;
+        if (pp->tile) p.tile = pp->tile;
+        if (pp->ext_cap) p.ext_cap = pp->ext_cap;
+    }
+    return p;
+}
+
+void fill_info(const mcr::Plan& P, mc_plan_info* info) {
+    info->n = P.n;
+    info->n_routed = P.n_routed;
+    info->n_clusters = P.n_clusters;
+    info->n_cross = P.n_cross;
+    info->nslots = P.nslots;
+    info->nwg = P.nwg;
+    info->slots = P.p.slots;
+    info->tile = P.p.tile;
+    info->gmax = P.gmax;
+    info->max_height = P.max_height;
+    info->max_ext_wg = P.max_ext_wg;
+}
+
+void check_topology_args(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                         const int64_t* heads, int64_t n_head) {
+    REQUIRE(n >= 0, "n must be >= 0");
+    REQUIRE(n == 0 || (endnodes && indegree), "endnodes/indegree must not be NULL");
+    REQUIRE(n_head >= 0 && (n_head == 0 || heads), "bad headwater list");
+}
+
+// numpy.searchsorted(xp, x, side='left')
+int64_t searchsorted_left(const double* xp, int64_t n, double x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = lo + ((hi - lo) >> 1);
+        if (xp[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct Net {
+    mcr::Plan plan;
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+
+    // static schedule
+    DBuf<int32_t> G, up_more_off, ext_off, ext_g, active;
+    DBuf<uint8_t> flags, up_cnt;
+    DBuf<uint64_t> up4;
+    DBuf<uint16_t> up_more;
+    DBuf<int64_t> slot_reach, ext_src, pos;
+    // coefficients / state (slot order)
+    DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
+    // forcing (slot order) and single-step forcing
+    DBuf<double> F, Fstep, stage;
+    int64_t n_rows = 0;
+    std::vector<double> xp;
+    // step tables
+    DBuf<int2> srow;
+    DBuf<double2> sw;
+    // outputs (caller order, reach-major) and a step-major scratch for fetches
+    DBuf<double> O, I, outT;
+    int64_t T_out = 0;
+    bool coeffs_set = false;
+
+    // active-workgroup schedule cache
+    int64_t sched_T = -1;
+    std::vector<int64_t> sched_off;
+
+    // timing
+    bool timing = false;
+    double kernel_ms = 0.0, run_ms = 0.0;
+    int64_t launches = 0;
+    std::vector<hipEvent_t> events;
+
+    ~Net() {
+        for (hipEvent_t e : events) (void)hipEventDestroy(e);
+        if (own) (void)hipStreamDestroy(own);
+    }
+
+    void init(int64_t n, const int64_t* endnodes, const int64_t* indegree, const int64_t* heads,
+              int64_t n_head, const mcr::PlanParams& p) {
+        const std::string err = mcr::build_plan(n, endnodes, indegree, heads, n_head, p, plan);
+        if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
+        HIPC(hipGetDevice(&device));
+        HIPC(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+        stream = own;
+        const size_t ns = (size_t)plan.nslots;
+        G.upload(plan.G.data(), ns, stream);
+        flags.upload(plan.flags.data(), ns, stream);
+        up_cnt.upload(plan.up_cnt.data(), ns, stream);
+        up4.upload(plan.up4.data(), ns, stream);
+        up_more_off.upload(plan.up_more_off.data(), plan.up_more_off.size(), stream);
+        up_more.upload(plan.up_more.data(), plan.up_more.size(), stream);
+        slot_reach.upload(plan.slot_reach.data(), ns, stream);
+        ext_off.upload(plan.ext_off.data(), plan.ext_off.size(), stream);
+        ext_src.upload(plan.ext_src.data(), plan.ext_src.size(), stream);
+        ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
+        pos.upload(plan.pos.data(), plan.pos.size(), stream);
+        for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
+            b->reserve(ns);
+            HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
+        }
+        stage.reserve(std::max<int64_t>(plan.n, 1));
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    // caller-order host array -> slot-order device array
+    void to_slots(const double* host, DBuf<double>& dst) {
+        const int64_t n = plan.n;
+        if (n == 0) return;
+        HIPC(hipMemcpyAsync(stage.p, host, n * sizeof(double), hipMemcpyHostToDevice, stream));
+        HIPC(mcr::launch_scatter_to_slots(stage.p, dst.p, slot_reach.p, plan.nslots, stream));
+    }
+    void from_slots(const DBuf<double>& src, double* host) {
+        const int64_t n = plan.n;
+        if (n == 0) return;
+        HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, stream));
+        HIPC(hipMemcpyAsync(host, stage.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    void set_coeffs(const double* a, const double* b, const double* c, const double* g) {
+        REQUIRE(plan.n == 0 || (a && b && c && g), "coefficient arrays must not be NULL");
+        to_slots(a, alpha);
+        to_slots(b, beta);
+        to_slots(c, chi);
+        to_slots(g, gamma);
+        HIPC(hipStreamSynchronize(stream));  // `stage` is reused by the next call
+        coeffs_set = true;
+    }
+
+    void set_state(const double* o, const double* i) {
+        REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
+        to_slots(o, st_o);
+        HIPC(hipStreamSynchronize(stream));
+        to_slots(i, st_i);
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    void ensure_schedule(int64_t T) {
+        if (sched_T == T) return;
+        std::vector<int32_t> list;
+        mcr::active_schedule(plan, T, list, sched_off);
+        active.upload(list.data(), list.size(), stream);
+        HIPC(hipStreamSynchronize(stream));
+        sched_T = T;
+    }
+
+    void ensure_events(size_t k) {
+        while (events.size() < k) {
+            hipEvent_t e;
+            HIPC(hipEventCreate(&e));
+            events.push_back(e);
+        }
+    }
+
+    // Run T steps using forcing buffer `Fsrc` with `rows` rows and host step tables.
+    void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int2>& hr,
+                    const std::vector<double2>& hw) {
+        REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
+        REQUIRE(T >= 1 && T < (1ll << 30), "T out of range");
+        const int64_t n = plan.n;
+        O.reserve((size_t)n * T);
+        I.reserve((size_t)n * T);
+        T_out = 0;
+        if (n == 0) {
+            T_out = T;
+            return;
+        }
+        srow.upload(hr.data(), hr.size(), stream);
+        sw.upload(hw.data(), hw.size(), stream);
+        HIPC(hipStreamSynchronize(stream));  // host tables are freed when the caller returns
+        ensure_schedule(T);
+        const int64_t nl = (int64_t)sched_off.size() - 1;
+        mcr::WaveArgs a{};
+        a.G = G.p;
+        a.flags = flags.p;
+        a.up_cnt = up_cnt.p;
+        a.up4 = up4.p;
+        a.up_more_off = up_more_off.p;
+        a.up_more = up_more.p;
+        a.slot_reach = slot_reach.p;
+        a.ext_off = ext_off.p;
+        a.ext_src = ext_src.p;
+        a.ext_g = ext_g.p;
+        a.alpha = alpha.p;
+        a.beta = beta.p;
+        a.chi = chi.p;
+        a.gamma = gamma.p;
+        a.st_o = st_o.p;
+        a.st_i = st_i.p;
+        a.F = Fsrc;
+        a.srow = srow.p;
+        a.sw = sw.p;
+        a.O = O.p;
+        a.I = I.p;
+        a.nslots = plan.nslots;
+        a.n_rows = (int32_t)rows;
+        a.T = (int32_t)T;
+        a.tile = plan.p.tile;
+        const size_t lds = (2 * (size_t)plan.p.slots + (size_t)plan.max_ext_wg * plan.p.tile) *
+                           sizeof(double);
+        if (timing) ensure_events(2 * (size_t)nl + 2);
+        if (timing) HIPC(hipEventRecord(events[2 * nl], stream));
+        int64_t launched = 0;
+        for (int64_t k = 0; k < nl; ++k) {
+            const int64_t grid = sched_off[k + 1] - sched_off[k];
+            if (grid == 0) continue;
+            a.active = active.p + sched_off[k];
+            a.kappa0 = (int32_t)(k * plan.p.tile);
+            if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
+            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, stream));
+            if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
+            ++launched;
+        }
+        HIPC(mcr::launch_final_state(O.p, I.p, st_o.p, st_i.p, slot_reach.p, plan.nslots, T,
+                                     stream));
+        if (timing) {
+            HIPC(hipEventRecord(events[2 * nl + 1], stream));
+            HIPC(hipEventSynchronize(events[2 * nl + 1]));
+            for (int64_t k = 0; k < launched; ++k) {
+                float ms = 0.f;
+                HIPC(hipEventElapsedTime(&ms, events[2 * k], events[2 * k + 1]));
+                kernel_ms += ms;
+            }
+            float ms = 0.f;
+            HIPC(hipEventElapsedTime(&ms, events[2 * nl], events[2 * nl + 1]));
+            run_ms += ms;
+            launches += launched;
+        }
+        T_out = T;
+    }
+
+    void load_forcing(int64_t rows, const double* xps, const double* fp) {
+        REQUIRE(rows >= 1 && rows < (1ll << 31), "n_rows must be >= 1");
+        REQUIRE(xps && (plan.n == 0 || fp), "xp/fp must not be NULL");
+        for (int64_t r = 1; r < rows; ++r)
+            REQUIRE(!(xps[r] < xps[r - 1]), "xp must be sorted ascending");
+        const int64_t n = plan.n;
+        xp.assign(xps, xps + rows);
+        n_rows = rows;
+        F.reserve((size_t)rows * plan.nslots);
+        if (n == 0) return;
+        DBuf<double> tmp;
+        tmp.upload(fp, (size_t)rows * n, stream);
+        HIPC(mcr::launch_forcing_to_slots(tmp.p, F.p, slot_reach.p, n, plan.nslots, rows,
+                                          stream));
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    void run(int64_t T, const double* x) {
+        REQUIRE(n_rows > 0, "mc_load_forcing must be called before mc_run");
+        REQUIRE(x != nullptr, "x must not be NULL");
+        std::vector<int2> hr(T);
+        std::vector<double2> hw(T);
+        for (int64_t t = 0; t < T; ++t) {  // nutils.py:21-33
+            const double xt = x[t];
+            const int64_t ix = searchsorted_left(xp.data(), n_rows, xt);
+            if (ix == 0) {
+                hr[t] = make_int2(0, -1);
+                hw[t] = make_double2(1.0, 0.0);
+            } else if (ix >= n_rows) {
+                hr[t] = make_int2((int)(n_rows - 1), -1);
+                hw[t] = make_double2(1.0, 0.0);
+            } else {
+                const double dx0 = xt - xp[ix - 1];
+                const double dx1 = xp[ix] - xt;
+                const double frac = dx0 / (dx0 + dx1);
+                hr[t] = make_int2((int)(ix - 1), (int)ix);
+                hw[t] = make_double2(1 - frac, frac);
+            }
+        }
+        run_tables(T, F.p, n_rows, hr, hw);
+    }
+
+    void step(const double* q, double* i_out, double* o_out) {
+        REQUIRE(plan.n == 0 || (q && i_out && o_out), "q/outputs must not be NULL");
+        const int64_t n = plan.n;
+        Fstep.reserve(std::max<int64_t>(plan.nslots, 1));
+        if (n) to_slots(q, Fstep);
+        std::vector<int2> hr(1, make_int2(0, -1));
+        std::vector<double2> hw(1, make_double2(1.0, 0.0));
+        run_tables(1, Fstep.p, 1, hr, hw);
+        if (n) {
+            HIPC(hipMemcpyAsync(o_out, O.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+            HIPC(hipMemcpyAsync(i_out, I.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+        }
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    void fetch(int64_t t0, int64_t t1, double* oo, double* io) {
+        REQUIRE(T_out > 0, "no outputs: call mc_run first");
+        REQUIRE(0 <= t0 && t0 <= t1 && t1 <= T_out, "step range out of bounds");
+        const int64_t n = plan.n;
+        const int64_t k = t1 - t0;
+        if (n == 0 || k == 0) return;
+        outT.reserve((size_t)n * k);
+        if (oo) {
+            HIPC(mcr::launch_transpose(O.p, outT.p, n, T_out, t0, t1, stream));
+            HIPC(hipMemcpyAsync(oo, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
+                                stream));
+            HIPC(hipStreamSynchronize(stream));
+        }
+        if (io) {
+            HIPC(mcr::launch_transpose(I.p, outT.p, n, T_out, t0, t1, stream));
+            HIPC(hipMemcpyAsync(io, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
+                                stream));
+            HIPC(hipStreamSynchronize(stream));
+        }
+    }
+
+    void fetch_series(double* oo, double* io) {
+        REQUIRE(T_out > 0, "no outputs: call mc_run first");
+        const size_t bytes = (size_t)plan.n * T_out * sizeof(double);
+        if (oo && bytes)
+            HIPC(hipMemcpyAsync(oo, O.p, bytes, hipMemcpyDeviceToHost, stream));
+        if (io && bytes)
+            HIPC(hipMemcpyAsync(io, I.p, bytes, hipMemcpyDeviceToHost, stream));
+        HIPC(hipStreamSynchronize(stream));
+    }
+};
+
+Net* as_net(void* h) {
+    if (!h) throw Fail(MC_E_INVALID, "null session handle");
+    return static_cast<Net*>(h);
+}
+
+// cache for the stateless mc_ax_bu_f64 mirror: recompiled only when the topology changes
+struct AxBuCache {
+    std::mutex mu;
+    std::unique_ptr<Net> net;
+    std::vector<int64_t> endnodes, indegree, heads;
+    int device = -1;
+};
+AxBuCache& axbu_cache() {
+    static AxBuCache c;
+    return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mc_last_error(void) { return g_err.c_str(); }
+
+int mc_version(void) { return 100; }
+
+int mc_plan_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                   const int64_t* headwaters, int64_t n_head, const mc_plan_params* params,
+                   void** plan_out) {
+    return guarded([&] {
+        REQUIRE(plan_out, "plan_out must not be NULL");
+        check_topology_args(n, endnodes, indegree, headwaters, n_head);
+        auto p = std::make_unique<mcr::Plan>();
+        const std::string err =
+            mcr::build_plan(n, endnodes, indegree, headwaters, n_head, to_params(params), *p);
+        if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
+        *plan_out = p.release();
+    });
+}
+
+int mc_plan_get_info(const void* plan, mc_plan_info* info) {
+    return guarded([&] {
+        REQUIRE(plan && info, "null argument");
+        fill_info(*static_cast<const mcr::Plan*>(plan), info);
+    });
+}
+
+int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
+                   int64_t* slot_reach) {
+    return guarded([&] {
+        REQUIRE(plan, "null plan");
+        const mcr::Plan& P = *static_cast<const mcr::Plan*>(plan);
+        if (rank) std::memcpy(rank, P.rank.data(), P.rank.size() * sizeof(int64_t));
+        if (pos) std::memcpy(pos, P.pos.data(), P.pos.size() * sizeof(int64_t));
+        if (G) std::memcpy(G, P.G.data(), P.G.size() * sizeof(int32_t));
+        if (slot_reach)
+            std::memcpy(slot_reach, P.slot_reach.data(), P.slot_reach.size() * sizeof(int64_t));
+    });
+}
+
+int mc_plan_destroy(void* plan) {
+    return guarded([&] { delete static_cast<mcr::Plan*>(plan); });
+}
+
+int mc_net_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                  const int64_t* headwaters, int64_t n_head, const mc_plan_params* params,
+                  void** net_out) {
+    return guarded([&] {
+        REQUIRE(net_out, "net_out must not be NULL");
+        check_topology_args(n, endnodes, indegree, headwaters, n_head);
+        auto net = std::make_unique<Net>();
+        net->init(n, endnodes, indegree, headwaters, n_head, to_params(params));
+        *net_out = net.release();
+    });
+}
+
+int mc_net_destroy(void* net) {
+    return guarded([&] { delete static_cast<Net*>(net); });
+}
+
+int mc_net_get_info(const void* net, mc_plan_info* info) {
+    return guarded([&] {
+        REQUIRE(net && info, "null argument");
+        fill_info(static_cast<const Net*>(net)->plan, info);
+    });
+}
+
+int mc_net_set_stream(void* net, void* s) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        HIPC(hipStreamSynchronize(N->stream));
+        N->stream = s ? static_cast<hipStream_t>(s) : N->own;
+    });
+}
+
+int mc_set_coeffs(void* net, const double* a, const double* b, const double* c,
+                  const double* g) {
+    return guarded([&] { as_net(net)->set_coeffs(a, b, c, g); });
+}
+
+int mc_set_state(void* net, const double* o, const double* i) {
+    return guarded([&] { as_net(net)->set_state(o, i); });
+}
+
+int mc_get_state(void* net, double* o, double* i) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        REQUIRE(N->plan.n == 0 || (o && i), "state arrays must not be NULL");
+        N->from_slots(N->st_o, o);
+        N->from_slots(N->st_i, i);
+    });
+}
+
+int mc_step(void* net, const double* o_prev, const double* i_prev, const double* q,
+            double* i_out, double* o_out) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        if (o_prev || i_prev) N->set_state(o_prev, i_prev);
+        N->step(q, i_out, o_out);
+    });
+}
+
+int mc_load_forcing(void* net, int64_t n_rows, const double* xp, const double* fp) {
+    return guarded([&] { as_net(net)->load_forcing(n_rows, xp, fp); });
+}
+
+int mc_run(void* net, int64_t T, const double* x) {
+    return guarded([&] { as_net(net)->run(T, x); });
+}
+
+int mc_fetch_outputs(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i) {
+    return guarded([&] { as_net(net)->fetch(t0, t1, out_o, out_i); });
+}
+
+int mc_fetch_series(void* net, double* out_o, double* out_i) {
+    return guarded([&] { as_net(net)->fetch_series(out_o, out_i); });
+}
+
+int mc_simulate(void* net, int64_t T, const double* x, int64_t n_rows, const double* xp,
+                const double* fp, double* out_o, double* out_i) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        N->load_forcing(n_rows, xp, fp);
+        N->run(T, x);
+        N->fetch(0, T, out_o, out_i);
+    });
+}
+
+int mc_output_device_ptrs(void* net, void** o_dev, void** i_dev, int64_t* T) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        if (o_dev) *o_dev = N->O.p;
+        if (i_dev) *i_dev = N->I.p;
+        if (T) *T = N->T_out;
+    });
+}
+
+int mc_synchronize(void* net) {
+    return guarded([&] { HIPC(hipStreamSynchronize(as_net(net)->stream)); });
+}
+
+int mc_set_timing(void* net, int enable) {
+    return guarded([&] { as_net(net)->timing = enable != 0; });
+}
+
+int mc_get_timing(void* net, double* kernel_ms, int64_t* launches, double* run_ms) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        if (kernel_ms) *kernel_ms = N->kernel_ms;
+        if (launches) *launches = N->launches;
+        if (run_ms) *run_ms = N->run_ms;
+    });
+}
+
+int mc_reset_timing(void* net) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        N->kernel_ms = N->run_ms = 0.0;
+        N->launches = 0;
+    });
+}
+
+int mc_ax_bu_f64(int64_t n, const int64_t* heads, int64_t n_head, const int64_t* endnodes,
+                 const double* alpha, const double* beta, const double* chi, const double* gamma,
+                 const double* i_prev, const double* o_prev, const double* q,
+                 const int64_t* indegree, double* i_out, double* o_out) {
+    return guarded([&] {
+        check_topology_args(n, endnodes, indegree, heads, n_head);
+        REQUIRE(n == 0 || (alpha && beta && chi && gamma && i_prev && o_prev && q && i_out &&
+                           o_out),
+                "null array argument");
+        AxBuCache& c = axbu_cache();
+        std::lock_guard<std::mutex> lock(c.mu);
+        int dev = 0;
+        HIPC(hipGetDevice(&dev));
+        const bool same = c.net && c.device == dev && (int64_t)c.endnodes.size() == n &&
+                          (int64_t)c.heads.size() == n_head &&
+                          std::equal(endnodes, endnodes + n, c.endnodes.begin()) &&
+                          std::equal(indegree, indegree + n, c.indegree.begin()) &&
+                          std::equal(heads, heads + n_head, c.heads.begin());
+        if (!same) {
+            c.net.reset();
+            auto net = std::make_unique<Net>();
+            net->init(n, endnodes, indegree, heads, n_head, mcr::PlanParams());
+            c.net = std::move(net);
+            c.endnodes.assign(endnodes, endnodes + n);
+            c.indegree.assign(indegree, indegree + n);
+            c.heads.assign(heads, heads + n_head);
+            c.device = dev;
+        }
+        Net* N = c.net.get();
+        N->set_coeffs(alpha, beta, chi, gamma);
+        N->set_state(o_prev, i_prev);
+        N->step(q, i_out, o_out);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,339 @@
+// Topology compiler: reference-walk replay, rank-ordered upstream lists, clustering, space-time
+// schedule and workgroup packing.  See plan.hpp for the model.
+#include "plan.hpp"
+
+#include <algorithm>
+#include <numeric>
+#include <sstream>
+
+namespace mcr {
+
+namespace {
+
+struct Cluster {
+    int64_t root = -1;
+    int64_t size = 0;
+    int64_t ext = 0;        // cross-cluster inputs
+    int64_t wg = -1;
+    int32_t off = 0;        // G offset
+    int32_t dmax = 0;       // deepest in-cluster distance to the root
+};
+
+}  // namespace
+
+std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                       const int64_t* heads, int64_t n_heads, const PlanParams& params,
+                       Plan& P) {
+    P = Plan();
+    P.n = n;
+    P.p = params;
+    const int64_t C = params.slots;
+    const int32_t B = params.tile;
+    if (n < 0) return "n must be >= 0";
+    if (C < 64 || C > 1024 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 1024]";
+    if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
+    if (params.ext_cap < 1 || params.ext_cap > 0x7fff) return "ext_cap out of range";
+    for (int64_t j = 0; j < n; ++j)
+        if (endnodes[j] < 0 || endnodes[j] >= n) {
+            std::ostringstream s;
+            s << "endnodes[" << j << "] = " << endnodes[j] << " is out of range [0, " << n << ")";
+            return s.str();
+        }
+
+    // ---- 1. replay the reference walk (nutils.py:72-88) -----------------------------------
+    std::vector<int64_t> deg(indegree, indegree + n);
+    P.rank.assign(n, -1);
+    std::vector<int64_t> order;
+    order.reserve(n);
+    for (int64_t k = 0; k < n_heads; ++k) {
+        int64_t s = heads[k];
+        if (s < 0 || s >= n) {
+            std::ostringstream m;
+            m << "headwater index " << s << " out of range";
+            return m.str();
+        }
+        while (deg[s] == 0) {
+            if (P.rank[s] >= 0) {
+                std::ostringstream m;
+                m << "reach " << s << " would be processed twice in one step (duplicate or "
+                  << "inconsistent headwater list / indegree)";
+                return m.str();
+            }
+            P.rank[s] = (int64_t)order.size();
+            order.push_back(s);
+            const int64_t e = endnodes[s];
+            deg[e] -= 1;
+            s = e;
+        }
+    }
+    P.n_routed = (int64_t)order.size();
+
+    // ---- 2. rank-ordered upstream lists ---------------------------------------------------
+    // contribution s -> e happens when s is processed (s routed, e != s).
+    std::vector<int64_t> up_off(n + 1, 0);
+    for (int64_t s : order)
+        if (endnodes[s] != s) up_off[endnodes[s] + 1]++;
+    for (int64_t j = 0; j < n; ++j) up_off[j + 1] += up_off[j];
+    std::vector<int64_t> up_list(up_off[n]);
+    {
+        std::vector<int64_t> fill(up_off.begin(), up_off.end() - 1);
+        for (int64_t s : order)  // rank order -> each list sorted by rank
+            if (endnodes[s] != s) up_list[fill[endnodes[s]]++] = s;
+    }
+    for (int64_t s : order) {
+        const int64_t e = endnodes[s];
+        if (e != s && P.rank[e] >= 0 && P.rank[e] < P.rank[s]) {
+            std::ostringstream m;
+            m << "reach " << e << " is processed before its upstream reach " << s
+              << " (indegree inconsistent with endnodes)";
+            return m.str();
+        }
+    }
+    // node order for the compiler: routed reaches in rank order, then the never-processed ones
+    std::vector<int64_t> nodes(order);
+    for (int64_t j = 0; j < n; ++j)
+        if (P.rank[j] < 0) nodes.push_back(j);
+    // consumer of j inside the schedule (-1 if none)
+    auto consumer = [&](int64_t j) -> int64_t {
+        if (P.rank[j] < 0) return -1;
+        const int64_t e = endnodes[j];
+        return e == j ? -1 : e;
+    };
+
+    // ---- 3. heights -----------------------------------------------------------------------
+    std::vector<int32_t> h(n, 0);
+    for (int64_t j : nodes) {
+        int32_t hj = 0;
+        for (int64_t k = up_off[j]; k < up_off[j + 1]; ++k) hj = std::max(hj, h[up_list[k]] + 1);
+        h[j] = hj;
+        P.max_height = std::max(P.max_height, hj);
+    }
+
+    // ---- 4. clustering (bottom-up greedy) -------------------------------------------------
+    // Each reach starts a cluster that absorbs the clusters of its upstream reaches while the
+    // slot and external-input budgets allow.  The deepest upstream is tried first; a shallow
+    // upstream whose value can arrive `tile` ticks late without delaying j is cut for free.
+    std::vector<int64_t> cl(n, -1);
+    std::vector<Cluster> clusters;
+    std::vector<int32_t> eh(n, 0);          // critical-path estimate (ticks)
+    std::vector<uint8_t> merged(n, 0);      // edge (j -> consumer) is inside a cluster
+    std::vector<std::vector<int64_t>> members;
+    std::vector<int64_t> ups;
+    for (int64_t j : nodes) {
+        ups.assign(up_list.begin() + up_off[j], up_list.begin() + up_off[j + 1]);
+        std::stable_sort(ups.begin(), ups.end(),
+                         [&](int64_t a, int64_t b) { return eh[a] > eh[b]; });
+        Cluster c;
+        c.root = j;
+        c.size = 1;
+        std::vector<int64_t> absorb;
+        int32_t best = ups.empty() ? -1 : eh[ups[0]];
+        int32_t ehj = 0;
+        bool first = true;
+        for (int64_t u : ups) {
+            const Cluster& cu = clusters[cl[u]];
+            const bool costly = first || (eh[u] + B > best + 1);
+            first = false;
+            if (costly && c.size + cu.size <= C && c.ext + cu.ext <= params.ext_cap) {
+                c.size += cu.size;
+                c.ext += cu.ext;
+                absorb.push_back(cl[u]);
+                merged[u] = 1;
+                ehj = std::max(ehj, eh[u] + 1);
+            } else {
+                c.ext += 1;
+                ehj = std::max(ehj, eh[u] + B);
+            }
+        }
+        if (c.ext > params.ext_cap) {
+            // a single reach with more external inputs than the budget: cannot be scheduled
+            std::ostringstream m;
+            m << "reach " << j << " has " << c.ext << " external inputs (ext_cap "
+              << params.ext_cap << ")";
+            return m.str();
+        }
+        eh[j] = ehj;
+        // merge small-to-large: the largest absorbed cluster keeps its id and member list
+        int64_t id;
+        if (absorb.empty()) {
+            id = (int64_t)clusters.size();
+            clusters.push_back(c);
+            members.emplace_back();
+        } else {
+            id = absorb[0];
+            for (int64_t a : absorb)
+                if (clusters[a].size > clusters[id].size) id = a;
+            for (int64_t a : absorb) {
+                if (a == id) continue;
+                for (int64_t v : members[a]) {
+                    cl[v] = id;
+                    members[id].push_back(v);
+                }
+                std::vector<int64_t>().swap(members[a]);
+                clusters[a].size = 0;  // dead
+            }
+            clusters[id] = c;
+        }
+        members[id].push_back(j);
+        cl[j] = id;
+    }
+
+    // ---- 5. schedule: local ALAP skew + cluster offsets -----------------------------------
+    // distance to the cluster root: walk nodes in reverse (downstream first)
+    std::vector<int32_t> dist(n, 0);
+    for (auto it = nodes.rbegin(); it != nodes.rend(); ++it) {
+        const int64_t j = *it;
+        const int64_t e = consumer(j);
+        dist[j] = (e >= 0 && merged[j]) ? dist[e] + 1 : 0;
+        Cluster& c = clusters[cl[j]];
+        c.dmax = std::max(c.dmax, dist[j]);
+    }
+    std::vector<int32_t> G(n, 0);
+    // live clusters in root rank order (roots appear in `nodes` order)
+    std::vector<int64_t> live;
+    for (int64_t j : nodes)
+        if (clusters[cl[j]].root == j) live.push_back(cl[j]);
+    P.n_clusters = (int64_t)live.size();
+    for (int64_t id : live) {
+        Cluster& c = clusters[id];
+        int64_t off = 0;
+        for (int64_t v : members[id]) {
+            const int32_t s = c.dmax - dist[v];
+            for (int64_t k = up_off[v]; k < up_off[v + 1]; ++k) {
+                const int64_t u = up_list[k];
+                if (cl[u] != id) off = std::max<int64_t>(off, (int64_t)G[u] + B - s);
+            }
+        }
+        if (off > (int64_t)1 << 30) return "schedule overflow (network too deep)";
+        c.off = (int32_t)off;
+        for (int64_t v : members[id]) G[v] = c.off + c.dmax - dist[v];
+    }
+    for (int64_t j = 0; j < n; ++j) P.gmax = std::max(P.gmax, G[j]);
+
+    // ---- 6. pack clusters into workgroups (first fit, largest first) ---------------------
+    std::vector<int64_t> by_size(live);
+    std::stable_sort(by_size.begin(), by_size.end(), [&](int64_t a, int64_t b) {
+        return clusters[a].size > clusters[b].size;
+    });
+    std::vector<int64_t> wg_fill, wg_ext;
+    // bounded first-fit: try the last few open bins only (keeps packing O(n))
+    const int kProbe = 64;
+    for (int64_t id : by_size) {
+        Cluster& c = clusters[id];
+        int64_t w = -1;
+        const int64_t nb = (int64_t)wg_fill.size();
+        for (int64_t b = std::max<int64_t>(0, nb - kProbe); b < nb; ++b)
+            if (wg_fill[b] + c.size <= C && wg_ext[b] + c.ext <= params.ext_cap) {
+                w = b;
+                break;
+            }
+        if (w < 0) {
+            w = nb;
+            wg_fill.push_back(0);
+            wg_ext.push_back(0);
+        }
+        wg_fill[w] += c.size;
+        wg_ext[w] += c.ext;
+        c.wg = w;
+    }
+    P.nwg = (int32_t)wg_fill.size();
+    P.nslots = (int64_t)P.nwg * C;
+
+    // ---- 7. slot assignment (sorted by G inside each workgroup) ---------------------------
+    std::vector<std::vector<int64_t>> wg_nodes(P.nwg);
+    for (int64_t id : live)
+        for (int64_t v : members[id]) wg_nodes[clusters[id].wg].push_back(v);
+    P.slot_reach.assign(P.nslots, -1);
+    P.G.assign(P.nslots, 0);
+    P.flags.assign(P.nslots, kSlotPad);
+    P.up_cnt.assign(P.nslots, 0);
+    P.up4.assign(P.nslots, 0);
+    P.up_more_off.assign(P.nslots + 1, 0);
+    P.pos.assign(n, -1);
+    P.wg_gmin.assign(P.nwg, 0);
+    P.wg_gmax.assign(P.nwg, 0);
+    for (int32_t w = 0; w < P.nwg; ++w) {
+        auto& v = wg_nodes[w];
+        std::stable_sort(v.begin(), v.end(), [&](int64_t a, int64_t b) { return G[a] < G[b]; });
+        for (size_t k = 0; k < v.size(); ++k) {
+            const int64_t d = (int64_t)w * C + (int64_t)k;
+            P.slot_reach[d] = v[k];
+            P.pos[v[k]] = d;
+            P.G[d] = G[v[k]];
+            P.flags[d] = P.rank[v[k]] >= 0 ? kSlotRouted : kSlotUnrouted;
+        }
+        P.wg_gmin[w] = v.empty() ? 0 : G[v.front()];
+        P.wg_gmax[w] = v.empty() ? 0 : G[v.back()];
+    }
+    // upstream codes and external lists
+    P.ext_off.assign(P.nwg + 1, 0);
+    std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src slot, consumer G)
+    std::vector<uint16_t> codes;
+    for (int64_t d = 0; d < P.nslots; ++d) {
+        const int64_t j = P.slot_reach[d];
+        P.up_more_off[d + 1] = P.up_more_off[d];
+        if (j < 0) continue;
+        const int32_t w = (int32_t)(d / C);
+        codes.clear();
+        for (int64_t k = up_off[j]; k < up_off[j + 1]; ++k) {
+            const int64_t u = up_list[k];
+            if (cl[u] == cl[j]) {
+                if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";
+                codes.push_back((uint16_t)(P.pos[u] - (int64_t)w * C));
+            } else {
+                if (G[j] < G[u] + B) return "internal: cross-cluster edge without tile slack";
+                const size_t e = ext[w].size();
+                if (e >= (size_t)params.ext_cap) return "internal: ext_cap exceeded";
+                ext[w].push_back({P.pos[u], G[j]});
+                codes.push_back((uint16_t)(kExtBit | e));
+                P.n_cross++;
+            }
+        }
+        if (codes.size() > 255) return "a reach has more than 255 upstream reaches";
+        P.up_cnt[d] = (uint8_t)codes.size();
+        uint64_t packed = 0;
+        for (size_t k = 0; k < codes.size() && k < (size_t)kUpInline; ++k)
+            packed |= (uint64_t)codes[k] << (16 * k);
+        P.up4[d] = packed;
+        for (size_t k = kUpInline; k < codes.size(); ++k) P.up_more.push_back(codes[k]);
+        P.up_more_off[d + 1] = (int32_t)P.up_more.size();
+    }
+    for (int32_t w = 0; w < P.nwg; ++w) {
+        P.ext_off[w + 1] = P.ext_off[w] + (int32_t)ext[w].size();
+        P.max_ext_wg = std::max(P.max_ext_wg, (int32_t)ext[w].size());
+        for (auto& pr : ext[w]) {
+            P.ext_src.push_back(pr.first);
+            P.ext_g.push_back(pr.second);
+        }
+    }
+    return std::string();
+}
+
+int64_t active_schedule(const Plan& P, int64_t T, std::vector<int32_t>& list,
+                        std::vector<int64_t>& off) {
+    list.clear();
+    off.assign(1, 0);
+    if (T <= 0 || P.nwg == 0) return 0;
+    const int64_t B = P.p.tile;
+    const int64_t ticks = (int64_t)P.gmax + T;
+    const int64_t nl = (ticks + B - 1) / B;
+    // bucket each workgroup into the launches its window [gmin, gmax + T) overlaps
+    std::vector<int64_t> cnt(nl + 1, 0);
+    for (int32_t w = 0; w < P.nwg; ++w) {
+        const int64_t a = P.wg_gmin[w] / B;
+        const int64_t b = ((int64_t)P.wg_gmax[w] + T - 1) / B;
+        for (int64_t k = a; k <= b && k < nl; ++k) cnt[k + 1]++;
+    }
+    for (int64_t k = 0; k < nl; ++k) cnt[k + 1] += cnt[k];
+    off = cnt;
+    list.assign(off[nl], 0);
+    std::vector<int64_t> fill(off.begin(), off.end() - 1);
+    for (int32_t w = 0; w < P.nwg; ++w) {
+        const int64_t a = P.wg_gmin[w] / B;
+        const int64_t b = ((int64_t)P.wg_gmax[w] + T - 1) / B;
+        for (int64_t k = a; k <= b && k < nl; ++k) list[fill[k]++] = w;
+    }
+    return nl;
+}
+
+}  // namespace mcr

@@ -1,0 +1,88 @@
+// Host-side topology compiler for the Muskingum wavefront sweep.
+//
+// The reference walks the forest once per timestep from every headwater, processing a reach as
+// soon as its indegree countdown reaches zero (nutils.py:64-89).  This compiler replays that walk
+// ONCE on the host (integer work only), records which reaches it processes and in which order,
+// and turns the result into a static space-time schedule for the GPU:
+//
+//   * every reach j gets an upstream list sorted by the reference's finalisation rank, so the
+//     inflow sum  i_next[j] = ((0 + o[u1]) + o[u2]) + ...  is formed in exactly the reference's
+//     order (bitwise identical for >= 3-way confluences);
+//   * reaches are grouped into clusters (connected sub-trees of at most `slots` reaches); a
+//     cluster is swept by one workgroup with a time-skewed wavefront: reach j handles model step
+//     t at global tick  G[j] + t.  Inside a cluster G[j] = G[down(j)] - 1, so every upstream
+//     value is consumed exactly one tick after it is produced (one LDS double buffer);
+//   * edges between clusters get slack  G[j] >= G[u] + tile,  so a value crossing clusters is
+//     always produced in an earlier launch of `tile` ticks (the kernel boundary is the only
+//     inter-workgroup synchronisation; no in-kernel hand-offs);
+//   * clusters are packed into workgroups of `slots` threads.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mcr {
+
+struct PlanParams {
+    int32_t slots = 256;       // reaches (threads) per workgroup
+    int32_t tile = 32;         // ticks per launch; also the slack of a cross-cluster edge
+    int32_t ext_cap = 128;     // max cross-cluster inputs per workgroup (LDS budget)
+};
+
+// upstream code: bit 15 set -> index into the workgroup's external-input list, else the
+// workgroup-local slot of the upstream reach.
+constexpr uint16_t kExtBit = 0x8000;
+constexpr int kUpInline = 4;  // upstream codes kept in registers; more go to an overflow list
+
+enum SlotFlags : uint8_t {
+    kSlotPad = 0,        // unused thread slot
+    kSlotRouted = 1,     // reach processed by the reference walk: o = 0 + (((a I + b Ip) + c Op) + g q)
+    kSlotUnrouted = 2,   // reach never processed (cycle / unreachable): o stays 0, I = sum of inflows
+};
+
+struct Plan {
+    int64_t n = 0;
+    PlanParams p;
+    int32_t nwg = 0;
+    int64_t nslots = 0;            // nwg * slots
+    int32_t gmax = 0;              // max G over real reaches
+    int64_t n_routed = 0;
+    int64_t n_clusters = 0;
+    int64_t n_cross = 0;           // cross-cluster edges
+    int32_t max_height = 0;        // longest upstream path (levels - 1)
+    int32_t max_ext_wg = 0;
+
+    // replay of the reference walk (original reach order)
+    std::vector<int64_t> rank;     // -1 if never processed
+
+    // per device slot d in [0, nslots)
+    std::vector<int64_t> slot_reach;   // original reach index, -1 for padding
+    std::vector<int32_t> G;            // tick of model step 0
+    std::vector<uint8_t> flags;
+    std::vector<uint8_t> up_cnt;
+    std::vector<uint64_t> up4;         // first kUpInline codes, 16 bits each
+    std::vector<int32_t> up_more_off;  // overflow list offset (codes kUpInline..)
+    std::vector<uint16_t> up_more;
+
+    // per workgroup
+    std::vector<int32_t> wg_gmin, wg_gmax;  // G range of the workgroup's real reaches
+    std::vector<int32_t> ext_off;           // [nwg + 1]
+    std::vector<int64_t> ext_src;           // device slot of the upstream reach
+    std::vector<int32_t> ext_g;             // G of the consuming reach
+
+    // original reach -> device slot
+    std::vector<int64_t> pos;
+};
+
+// Build the plan.  Returns an empty string on success, otherwise an error message.
+std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                       const int64_t* heads, int64_t n_heads, const PlanParams& params,
+                       Plan& out);
+
+// Workgroups with work in launch k (ticks [k*tile, (k+1)*tile)) for a horizon of T steps.
+// Fills `list` (concatenated) and `off` ([n_launch + 1]); returns the number of launches.
+int64_t active_schedule(const Plan& plan, int64_t T, std::vector<int32_t>& list,
+                        std::vector<int64_t>& off);
+
+}  // namespace mcr

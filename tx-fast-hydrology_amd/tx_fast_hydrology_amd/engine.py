@@ -1,0 +1,215 @@
+"""Python handles over the C ABI (include/mcroute.h).
+
+* ``ax_bu``      -- drop-in for ``tx_fast_hydrology.nutils._ax_bu`` (nutils.py:64-89): same
+                    positional arguments, returns fresh ``(i_t_next, o_t_next)`` arrays.
+* ``Plan``       -- host-only topology compiler (usable without a GPU).
+* ``RoutingNet`` -- device-resident session: coefficients, state, forcing and outputs live in
+                    HBM; ``run`` routes a whole horizon in one call.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+from ._native import f64, i64, ptr
+
+
+def _params(slots=0, tile=0, ext_cap=0):
+    return nat.PlanParams(int(slots), int(tile), int(ext_cap))
+
+
+class Plan:
+    """Compiled schedule of a network (no device memory)."""
+
+    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0):
+        L = nat.lib()
+        self._end = i64(endnodes)
+        self._deg = i64(indegree)
+        self._heads = i64(headwaters)
+        self.n = self._end.size
+        if self._deg.size != self.n:
+            raise ValueError("indegree and endnodes must have the same length")
+        h = ctypes.c_void_p()
+        p = _params(slots, tile, ext_cap)
+        nat.check(L.mc_plan_create(self.n, ptr(self._end), ptr(self._deg), ptr(self._heads),
+                                   self._heads.size, ctypes.byref(p), ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def info(self) -> dict:
+        info = nat.PlanInfo()
+        nat.check(nat.lib().mc_plan_get_info(self._h, ctypes.byref(info)))
+        return info.as_dict()
+
+    def export(self) -> dict:
+        info = self.info
+        rank = np.empty(self.n, dtype=np.int64)
+        pos = np.empty(self.n, dtype=np.int64)
+        G = np.empty(info["nslots"], dtype=np.int32)
+        slot_reach = np.empty(info["nslots"], dtype=np.int64)
+        nat.check(nat.lib().mc_plan_export(self._h, ptr(rank), ptr(pos), ptr(G),
+                                           ptr(slot_reach)))
+        return dict(rank=rank, pos=pos, G=G, slot_reach=slot_reach)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.lib().mc_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+class RoutingNet:
+    """Device-resident routing session for one network (one HIP device, one stream)."""
+
+    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0):
+        L = nat.lib()
+        end = i64(endnodes)
+        deg = i64(indegree)
+        heads = i64(headwaters)
+        self.n = end.size
+        if deg.size != self.n:
+            raise ValueError("indegree and endnodes must have the same length")
+        h = ctypes.c_void_p()
+        p = _params(slots, tile, ext_cap)
+        nat.check(L.mc_net_create(self.n, ptr(end), ptr(deg), ptr(heads), heads.size,
+                                  ctypes.byref(p), ctypes.byref(h)))
+        self._h = h
+        self.T = 0
+
+    # -- configuration -------------------------------------------------------------------
+    @property
+    def info(self) -> dict:
+        info = nat.PlanInfo()
+        nat.check(nat.lib().mc_net_get_info(self._h, ctypes.byref(info)))
+        return info.as_dict()
+
+    def set_stream(self, hip_stream: int | None):
+        nat.check(nat.lib().mc_net_set_stream(self._h, ctypes.c_void_p(hip_stream or 0)))
+
+    def set_coeffs(self, alpha, beta, chi, gamma):
+        a, b, c, g = f64(alpha), f64(beta), f64(chi), f64(gamma)
+        for v in (a, b, c, g):
+            if v.size != self.n:
+                raise ValueError("coefficient arrays must have n entries")
+        nat.check(nat.lib().mc_set_coeffs(self._h, ptr(a), ptr(b), ptr(c), ptr(g)))
+
+    def set_state(self, o_t_next, i_t_next):
+        o, i = f64(o_t_next), f64(i_t_next)
+        if o.size != self.n or i.size != self.n:
+            raise ValueError("state arrays must have n entries")
+        nat.check(nat.lib().mc_set_state(self._h, ptr(o), ptr(i)))
+
+    def get_state(self):
+        o = np.empty(self.n)
+        i = np.empty(self.n)
+        nat.check(nat.lib().mc_get_state(self._h, ptr(o), ptr(i)))
+        return o, i
+
+    # -- routing -------------------------------------------------------------------------
+    def step(self, q_t_next, o_t_prev=None, i_t_prev=None):
+        """One timestep; returns fresh (i_t_next, o_t_next) like nutils._ax_bu."""
+        q = f64(q_t_next)
+        if q.size != self.n:
+            raise ValueError("q must have n entries")
+        o = None if o_t_prev is None else f64(o_t_prev)
+        i = None if i_t_prev is None else f64(i_t_prev)
+        if (o is None) != (i is None):
+            raise ValueError("pass both o_t_prev and i_t_prev, or neither")
+        i_out = np.empty(self.n)
+        o_out = np.empty(self.n)
+        nat.check(nat.lib().mc_step(self._h, ptr(o), ptr(i), ptr(q), ptr(i_out), ptr(o_out)))
+        return i_out, o_out
+
+    def load_forcing(self, xp, fp):
+        xp = f64(xp)
+        fp = f64(fp)
+        if fp.ndim != 2 or fp.shape != (xp.size, self.n):
+            raise ValueError(f"forcing must be [{xp.size}][{self.n}], got {fp.shape}")
+        nat.check(nat.lib().mc_load_forcing(self._h, xp.size, ptr(xp), ptr(fp)))
+
+    def run(self, x):
+        """Route len(x) steps on the device (asynchronous; outputs stay resident)."""
+        x = f64(x)
+        nat.check(nat.lib().mc_run(self._h, x.size, ptr(x)))
+        self.T = x.size
+
+    def fetch_outputs(self, t0=0, t1=None):
+        """Step-major host copies (out_o[t][j], out_i[t][j]) of steps [t0, t1)."""
+        t1 = self.T if t1 is None else t1
+        out_o = np.empty((t1 - t0, self.n))
+        out_i = np.empty((t1 - t0, self.n))
+        nat.check(nat.lib().mc_fetch_outputs(self._h, t0, t1, ptr(out_o), ptr(out_i)))
+        return out_o, out_i
+
+    def fetch_series(self):
+        """Reach-major host copies (O[j][t], I[j][t]) of the last run."""
+        O = np.empty((self.n, self.T))
+        I = np.empty((self.n, self.T))
+        nat.check(nat.lib().mc_fetch_series(self._h, ptr(O), ptr(I)))
+        return O, I
+
+    def simulate(self, x, xp, fp):
+        self.load_forcing(xp, fp)
+        self.run(x)
+        return self.fetch_outputs()
+
+    def device_outputs(self):
+        o = ctypes.c_void_p()
+        i = ctypes.c_void_p()
+        T = ctypes.c_int64()
+        nat.check(nat.lib().mc_output_device_ptrs(self._h, ctypes.byref(o), ctypes.byref(i),
+                                                  ctypes.byref(T)))
+        return o.value, i.value, T.value
+
+    def synchronize(self):
+        nat.check(nat.lib().mc_synchronize(self._h))
+
+    # -- timing --------------------------------------------------------------------------
+    def set_timing(self, enable: bool):
+        nat.check(nat.lib().mc_set_timing(self._h, 1 if enable else 0))
+
+    def reset_timing(self):
+        nat.check(nat.lib().mc_reset_timing(self._h))
+
+    def timing(self) -> dict:
+        k = ctypes.c_double()
+        n = ctypes.c_int64()
+        r = ctypes.c_double()
+        nat.check(nat.lib().mc_get_timing(self._h, ctypes.byref(k), ctypes.byref(n),
+                                          ctypes.byref(r)))
+        return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.lib().mc_net_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def ax_bu(startnodes, endnodes, alpha, beta, chi, gamma, i_t_prev, o_t_prev, q_t_next,
+          indegree):
+    """Drop-in for nutils._ax_bu (nutils.py:64-89) on the GPU: returns (i_t_next, o_t_next)."""
+    heads = i64(startnodes)
+    end = i64(endnodes)
+    deg = i64(indegree)
+    n = end.size
+    a, b, c, g = f64(alpha), f64(beta), f64(chi), f64(gamma)
+    ip, op, q = f64(i_t_prev), f64(o_t_prev), f64(q_t_next)
+    i_out = np.empty(n)
+    o_out = np.empty(n)
+    nat.check(nat.lib().mc_ax_bu_f64(n, ptr(heads), heads.size, ptr(end), ptr(a), ptr(b), ptr(c),
+                                     ptr(g), ptr(ip), ptr(op), ptr(q), ptr(deg), ptr(i_out),
+                                     ptr(o_out)))
+    return i_out, o_out
