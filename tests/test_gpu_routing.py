@@ -61,7 +61,7 @@ def test_ax_bu_dt_change_sequence(golden):
 # ---------------------------------------------------------------- fused horizon (mc_run)
 def _golden_run(g, n_steps=None, **kw):
     end = g["endnodes"]
-    indeg, heads, coef, _, i0 = _model(end, g["K"], g["X"], float(g["dt"]))
+    indeg, heads, coef, _, i0 = _model(end, g["K"], g["X"], float(g["dt"]), o0=g["o0"])
     xs = orc.step_times(int(g["start_ns"]), int(float(g["dt"]) * 1e9), int(g["idx_ns"].max()))
     if n_steps is not None:
         xs = xs[:n_steps]

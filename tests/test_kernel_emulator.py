@@ -1,0 +1,62 @@
+"""CPU check of the schedule + kernel protocol: the host model of the HIP wavefront kernel
+(tests/kernel_emulator.py), driven by the C++ plan, must reproduce the oracle bit-for-bit."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tx_fast_hydrology_amd import engine, synthetic
+
+import kernel_emulator as emu
+
+
+def _case(end, K, X, dt, o0):
+    n = end.size
+    start = np.arange(n)
+    indeg = orc.compute_indegree(start, end)
+    coef = orc.muskingum_coeffs(K, X, dt)
+    i0 = orc.init_inflows(start, end, o0)
+    return start, indeg, coef, i0
+
+
+@pytest.mark.parametrize("n,p_chain,slots,tile,T,rows", [
+    (1, 0.0, 64, 32, 7, 3), (2, 1.0, 64, 1, 3, 2), (300, 0.9, 64, 4, 50, 5),
+    (1500, 0.95, 128, 16, 40, 4), (900, 0.5, 64, 8, 13, 1), (700, 0.99, 64, 64, 1, 2),
+    (2000, 0.97, 256, 32, 70, 7)])
+def test_emulator_matches_oracle(n, p_chain, slots, tile, T, rows):
+    rng = np.random.default_rng(n * 7 + T)
+    end = synthetic.random_forest(n, max(1, n // 400), rng, p_chain=p_chain)
+    K = rng.uniform(1800, 7200, n)
+    X = rng.uniform(0.1, 0.4, n)
+    o0 = rng.uniform(0.5, 5, n)
+    start, indeg, coef, i0 = _case(end, K, X, 300.0, o0)
+    xp, fp = synthetic.forcing(n, rows=rows, seed=n)
+    xp = xp.astype(float)
+    x = xp[0] - 600e9 + 300e9 * np.arange(1, T + 1)
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile)
+    O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
+    assert np.array_equal(O.T, want_o)
+    assert np.array_equal(I.T, want_i)
+
+
+def test_emulator_river_network_and_golden_edges(golden):
+    end = synthetic.river_network(4000, 6, 150, np.random.default_rng(9))
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=3)
+    start, indeg, coef, i0 = _case(end, K, X, 300.0, o0)
+    xp, fp = synthetic.forcing(n, rows=3, seed=4)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 31)
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=128, tile=8)
+    O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
+    assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
+    g = golden("g8_ax_bu_edge.npz")
+    for name in g["names"]:
+        a = g[f"{name}_args"]
+        plan = engine.Plan(g[f"{name}_endnodes"], g[f"{name}_indegree"], g[f"{name}_heads"],
+                           slots=64, tile=4)
+        O, I = emu.run(plan, a[0], a[1], a[2], a[3], a[5], a[4], np.array([0.0]),
+                       np.array([0.0]), a[6][None, :])
+        assert np.array_equal(O[:, 0], g[f"{name}_o"]), name
+        assert np.array_equal(I[:, 0], g[f"{name}_i"]), name

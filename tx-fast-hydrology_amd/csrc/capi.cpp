@@ -106,6 +106,8 @@ void fill_info(const mcr::Plan& P, mc_plan_info* info) {
     info->gmax = P.gmax;
     info->max_height = P.max_height;
     info->max_ext_wg = P.max_ext_wg;
+    info->n_up_more = (int64_t)P.up_more.size();
+    info->n_ext = (int64_t)P.ext_src.size();
 }
 
 void check_topology_args(int64_t n, const int64_t* endnodes, const int64_t* indegree,
@@ -466,6 +468,41 @@ int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
         if (G) std::memcpy(G, P.G.data(), P.G.size() * sizeof(int32_t));
         if (slot_reach)
             std::memcpy(slot_reach, P.slot_reach.data(), P.slot_reach.size() * sizeof(int64_t));
+    });
+}
+
+int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint64_t* up4,
+                         int32_t* up_more_off, uint16_t* up_more, int32_t* ext_off,
+                         int64_t* ext_src, int32_t* ext_g) {
+    return guarded([&] {
+        REQUIRE(plan, "null plan");
+        const mcr::Plan& P = *static_cast<const mcr::Plan*>(plan);
+        auto cp = [](auto* dst, const auto& v) {
+            if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+        };
+        cp(flags, P.flags);
+        cp(up_cnt, P.up_cnt);
+        cp(up4, P.up4);
+        cp(up_more_off, P.up_more_off);
+        cp(up_more, P.up_more);
+        cp(ext_off, P.ext_off);
+        cp(ext_src, P.ext_src);
+        cp(ext_g, P.ext_g);
+    });
+}
+
+int mc_plan_schedule(const void* plan, int64_t T, int64_t* n_launch, int64_t* n_list,
+                     int64_t* off, int32_t* list) {
+    return guarded([&] {
+        REQUIRE(plan && n_launch && n_list, "null argument");
+        REQUIRE(T >= 1, "T must be >= 1");
+        std::vector<int32_t> l;
+        std::vector<int64_t> o;
+        const int64_t nl = mcr::active_schedule(*static_cast<const mcr::Plan*>(plan), T, l, o);
+        *n_launch = nl;
+        *n_list = (int64_t)l.size();
+        if (off) std::memcpy(off, o.data(), o.size() * sizeof(int64_t));
+        if (list && !l.empty()) std::memcpy(list, l.data(), l.size() * sizeof(int32_t));
     });
 }
 

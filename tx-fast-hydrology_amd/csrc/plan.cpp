@@ -32,7 +32,14 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     if (n < 0) return "n must be >= 0";
     if (C < 64 || C > 1024 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 1024]";
     if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
-    if (params.ext_cap < 1 || params.ext_cap > 0x7fff) return "ext_cap out of range";
+    if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";
+    // LDS budget of one workgroup: 2 * slots outflows + ext_cap * tile external inputs
+    const int64_t lds_words = 160 * 1024 / 8;
+    if (2 * C + (int64_t)P.p.ext_cap * B > lds_words) {
+        const int64_t cap = (lds_words - 2 * C) / B;
+        if (cap < 1) return "slots/tile too large for the 160 KiB LDS of a workgroup";
+        P.p.ext_cap = (int32_t)cap;
+    }
     for (int64_t j = 0; j < n; ++j)
         if (endnodes[j] < 0 || endnodes[j] >= n) {
             std::ostringstream s;
@@ -134,7 +141,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             const Cluster& cu = clusters[cl[u]];
             const bool costly = first || (eh[u] + B > best + 1);
             first = false;
-            if (costly && c.size + cu.size <= C && c.ext + cu.ext <= params.ext_cap) {
+            if (costly && c.size + cu.size <= C && c.ext + cu.ext <= P.p.ext_cap) {
                 c.size += cu.size;
                 c.ext += cu.ext;
                 absorb.push_back(cl[u]);
@@ -145,11 +152,11 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
                 ehj = std::max(ehj, eh[u] + B);
             }
         }
-        if (c.ext > params.ext_cap) {
+        if (c.ext > P.p.ext_cap) {
             // a single reach with more external inputs than the budget: cannot be scheduled
             std::ostringstream m;
             m << "reach " << j << " has " << c.ext << " external inputs (ext_cap "
-              << params.ext_cap << ")";
+              << P.p.ext_cap << ")";
             return m.str();
         }
         eh[j] = ehj;
@@ -223,7 +230,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int64_t w = -1;
         const int64_t nb = (int64_t)wg_fill.size();
         for (int64_t b = std::max<int64_t>(0, nb - kProbe); b < nb; ++b)
-            if (wg_fill[b] + c.size <= C && wg_ext[b] + c.ext <= params.ext_cap) {
+            if (wg_fill[b] + c.size <= C && wg_ext[b] + c.ext <= P.p.ext_cap) {
                 w = b;
                 break;
             }
@@ -283,8 +290,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             } else {
                 if (G[j] < G[u] + B) return "internal: cross-cluster edge without tile slack";
                 const size_t e = ext[w].size();
-                if (e >= (size_t)params.ext_cap) return "internal: ext_cap exceeded";
-                ext[w].push_back({P.pos[u], G[j]});
+                if (e >= (size_t)P.p.ext_cap) return "internal: ext_cap exceeded";
+                ext[w].push_back({u, G[j]});
                 codes.push_back((uint16_t)(kExtBit | e));
                 P.n_cross++;
             }

@@ -68,7 +68,7 @@ struct Plan {
     // per workgroup
     std::vector<int32_t> wg_gmin, wg_gmax;  // G range of the workgroup's real reaches
     std::vector<int32_t> ext_off;           // [nwg + 1]
-    std::vector<int64_t> ext_src;           // device slot of the upstream reach
+    std::vector<int64_t> ext_src;           // caller index of the upstream reach (row of O)
     std::vector<int32_t> ext_g;             // G of the consuming reach
 
     // original reach -> device slot

@@ -53,6 +53,32 @@ class Plan:
                                            ptr(slot_reach)))
         return dict(rank=rank, pos=pos, G=G, slot_reach=slot_reach)
 
+    def export_links(self) -> dict:
+        info = self.info
+        ns, nwg = info["nslots"], info["nwg"]
+        out = dict(flags=np.empty(ns, np.uint8), up_cnt=np.empty(ns, np.uint8),
+                   up4=np.empty(ns, np.uint64), up_more_off=np.empty(ns + 1, np.int32),
+                   up_more=np.empty(info["n_up_more"], np.uint16),
+                   ext_off=np.empty(nwg + 1, np.int32), ext_src=np.empty(info["n_ext"], np.int64),
+                   ext_g=np.empty(info["n_ext"], np.int32))
+        nat.check(nat.lib().mc_plan_export_links(
+            self._h, *(ptr(out[k]) for k in ("flags", "up_cnt", "up4", "up_more_off", "up_more",
+                                             "ext_off", "ext_src", "ext_g"))))
+        return out
+
+    def schedule(self, T: int):
+        """(off [n_launch + 1], list): workgroups run by each launch of a T-step horizon."""
+        nl = ctypes.c_int64()
+        nls = ctypes.c_int64()
+        L = nat.lib()
+        nat.check(L.mc_plan_schedule(self._h, int(T), ctypes.byref(nl), ctypes.byref(nls), None,
+                                     None))
+        off = np.empty(nl.value + 1, dtype=np.int64)
+        lst = np.empty(max(nls.value, 1), dtype=np.int32)
+        nat.check(L.mc_plan_schedule(self._h, int(T), ctypes.byref(nl), ctypes.byref(nls),
+                                     ptr(off), ptr(lst)))
+        return off, lst[: nls.value]
+
     def close(self):
         if getattr(self, "_h", None):
             nat.lib().mc_plan_destroy(self._h)
