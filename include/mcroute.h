@@ -40,7 +40,8 @@ extern "C" {
 
 typedef struct mc_plan_params {
     int32_t slots;    /* reaches per workgroup (multiple of 64, <= 1024); 0 = default */
-    int32_t tile;     /* ticks per launch = slack of a cross-cluster edge; 0 = default */
+    int32_t tile;     /* ticks per launch = slack of a cross-cluster edge; 0 = default.
+                         Device sessions need a multiple of 16. */
     int32_t ext_cap;  /* max cross-cluster inputs per workgroup; 0 = default */
 } mc_plan_params;
 
@@ -133,8 +134,6 @@ int mc_fetch_series(void* net, double* out_o, double* out_i);
 int mc_simulate(void* net, int64_t T, const double* x, int64_t n_rows, const double* xp,
                 const double* fp, double* out_o, double* out_i);
 
-/* Device pointers of the resident reach-major outputs of the last mc_run ([n][T] each). */
-int mc_output_device_ptrs(void* net, void** o_dev, void** i_dev, int64_t* T);
 /* Blocks until the session's stream is idle. */
 int mc_synchronize(void* net);
 

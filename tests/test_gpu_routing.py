@@ -69,7 +69,7 @@ def _golden_run(g, n_steps=None, **kw):
     return net.simulate(xs.astype(float), g["idx_ns"].astype(float), g["forcing"])
 
 
-@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=1), dict(slots=64, tile=5),
+@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=16), dict(slots=64, tile=48),
                                 dict(slots=1024, tile=64)])
 def test_run_golden_ynet(golden, kw):
     g = golden("g1_ynet.npz")
@@ -77,7 +77,7 @@ def test_run_golden_ynet(golden, kw):
     assert np.array_equal(o, g["o"]) and np.array_equal(i, g["i"])
 
 
-@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=8), dict(slots=512, tile=32)])
+@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=16), dict(slots=512, tile=32)])
 def test_run_golden_huc8_every_step(golden, kw):
     g = golden("g2_huc8.npz")
     o, i = _golden_run(g, **kw)
@@ -89,7 +89,7 @@ def test_run_golden_huc8_every_step(golden, kw):
 
 def test_run_golden_confluence_order(golden):
     g = golden("g3_confluence.npz")
-    o, i = _golden_run(g, n_steps=int(g["n_steps"]), slots=64, tile=4)
+    o, i = _golden_run(g, n_steps=int(g["n_steps"]), slots=64, tile=16)
     assert np.array_equal(o, g["o"]) and np.array_equal(i, g["i"])
 
 
@@ -102,8 +102,9 @@ def _random_case(n, seed, p_chain, outlets):
 
 
 @pytest.mark.parametrize("n,p_chain,slots,tile,T", [
-    (1, 0.0, 64, 32, 7), (2, 1.0, 64, 1, 3), (300, 0.9, 64, 4, 50), (3000, 0.95, 256, 32, 96),
-    (5000, 0.5, 1024, 16, 40), (2000, 0.99, 128, 64, 1), (800, 0.9, 64, 128, 20)])
+    (1, 0.0, 64, 32, 7), (2, 1.0, 64, 16, 3), (300, 0.9, 64, 16, 50), (3000, 0.95, 256, 32, 96),
+    (5000, 0.5, 1024, 16, 40), (2000, 0.99, 128, 64, 1), (800, 0.9, 64, 128, 20),
+    (6000, 0.98, 512, 48, 333)])
 def test_run_random_vs_oracle(n, p_chain, slots, tile, T):
     end, K, X = _random_case(n, n + T, p_chain, max(1, n // 500))
     indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=n)
@@ -144,7 +145,7 @@ def test_step_api_matches_run():
     indeg, heads, coef, o0, i0 = _model(end, K, X, 900.0)
     rng = np.random.default_rng(5)
     qs = rng.gamma(2.0, 0.5, size=(T, n))
-    net = _net(end, indeg, heads, coef, o0, i0, slots=128, tile=8)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=128, tile=16)
     o, i = o0.copy(), i0.copy()
     for t in range(T):
         i_w, o_w = orc.ax_bu(heads, end, *coef, i, o, qs[t], indeg)
@@ -167,7 +168,7 @@ def test_unrouted_reaches_cycle_and_bad_indegree(golden):
         indeg = g[f"{name}_indegree"]
         heads = g[f"{name}_heads"]
         a = g[f"{name}_args"]
-        net = engine.RoutingNet(end, indeg, heads, slots=64, tile=3)
+        net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16)
         net.set_coeffs(a[0], a[1], a[2], a[3])
         i_g, o_g = net.step(a[6], o_t_prev=a[5], i_t_prev=a[4])
         assert np.array_equal(o_g, g[f"{name}_o"]) and np.array_equal(i_g, g[f"{name}_i"])
@@ -180,6 +181,12 @@ def test_unrouted_reaches_cycle_and_bad_indegree(golden):
         net.set_state(a[5], a[4])
         got_o, got_i = net.simulate(x, xp, fp)
         assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+
+
+def test_session_rejects_unaligned_tile():
+    from tx_fast_hydrology_amd import _native as nat
+    with pytest.raises(nat.RoutingError):
+        engine.RoutingNet(np.array([0]), np.array([0]), np.array([0]), tile=5)
 
 
 def test_texas_scale_bitexact_vs_oracle():

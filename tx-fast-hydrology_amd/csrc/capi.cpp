@@ -140,6 +140,8 @@ struct Net {
     DBuf<uint64_t> up4;
     DBuf<uint16_t> up_more;
     DBuf<int64_t> slot_reach, ext_src, pos;
+    DBuf<uint8_t> rpad;            // [n] output row pad (G & 15) of each caller reach
+    int32_t more_cap = 0;          // max overflow upstream codes of one workgroup
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
     // forcing (slot order) and single-step forcing
@@ -148,10 +150,11 @@ struct Net {
     std::vector<double> xp;
     // step tables
     DBuf<int2> srow;
-    DBuf<double2> sw;
-    // outputs (caller order, reach-major) and a step-major scratch for fetches
-    DBuf<double> O, I, outT;
-    int64_t T_out = 0;
+    DBuf<double> sfrac;
+    // interpolated lateral inflow [nslots][Tp], outputs [n][Tp] (caller order, padded rows),
+    // a step-major scratch for fetches and the dummy line of out-of-row chunks
+    DBuf<double> Q, O, I, outT, dummy;
+    int64_t T_out = 0, Tp_out = 0;
     bool coeffs_set = false;
 
     // active-workgroup schedule cache
@@ -173,6 +176,8 @@ struct Net {
               int64_t n_head, const mcr::PlanParams& p) {
         const std::string err = mcr::build_plan(n, endnodes, indegree, heads, n_head, p, plan);
         if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
+        if (plan.p.tile % mcr::kChunk != 0)
+            throw Fail(MC_E_INVALID, "tile must be a multiple of 16 for the device sweep");
         HIPC(hipGetDevice(&device));
         HIPC(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
         stream = own;
@@ -185,7 +190,25 @@ struct Net {
         up_more.upload(plan.up_more.data(), plan.up_more.size(), stream);
         slot_reach.upload(plan.slot_reach.data(), ns, stream);
         ext_off.upload(plan.ext_off.data(), plan.ext_off.size(), stream);
-        ext_src.upload(plan.ext_src.data(), plan.ext_src.size(), stream);
+        {
+            // external input source: caller row * 16 + row pad (one load in the prologue)
+            std::vector<int64_t> code(plan.ext_src.size());
+            for (size_t e = 0; e < code.size(); ++e) {
+                const int64_t j = plan.ext_src[e];
+                code[e] = j * 16 + (plan.G[plan.pos[j]] & (mcr::kChunk - 1));
+            }
+            ext_src.upload(code.data(), code.size(), stream);
+            std::vector<uint8_t> pad(plan.n);
+            for (int64_t j = 0; j < plan.n; ++j)
+                pad[j] = (uint8_t)(plan.G[plan.pos[j]] & (mcr::kChunk - 1));
+            rpad.upload(pad.data(), pad.size(), stream);
+            for (int32_t w = 0; w < plan.nwg; ++w) {
+                const int64_t a0 = plan.up_more_off[(int64_t)w * plan.p.slots];
+                const int64_t a1 = plan.up_more_off[(int64_t)(w + 1) * plan.p.slots];
+                more_cap = std::max<int32_t>(more_cap, (int32_t)(a1 - a0));
+            }
+            HIPC(hipStreamSynchronize(stream));
+        }
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
@@ -193,6 +216,7 @@ struct Net {
             HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
         }
         stage.reserve(std::max<int64_t>(plan.n, 1));
+        dummy.reserve(4 * mcr::kChunk);
         HIPC(hipStreamSynchronize(stream));
     }
 
@@ -248,22 +272,39 @@ struct Net {
 
     // Run T steps using forcing buffer `Fsrc` with `rows` rows and host step tables.
     void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int2>& hr,
-                    const std::vector<double2>& hw) {
+                    const std::vector<double>& hf) {
         REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
         REQUIRE(T >= 1 && T < (1ll << 30), "T out of range");
         const int64_t n = plan.n;
-        O.reserve((size_t)n * T);
-        I.reserve((size_t)n * T);
+        const int64_t Tp = mcr::padded_steps(T);
         T_out = 0;
         if (n == 0) {
             T_out = T;
+            Tp_out = Tp;
             return;
         }
+        O.reserve((size_t)n * Tp);
+        I.reserve((size_t)n * Tp);
+        Q.reserve((size_t)plan.nslots * Tp);
         srow.upload(hr.data(), hr.size(), stream);
-        sw.upload(hw.data(), hw.size(), stream);
+        sfrac.upload(hf.data(), hf.size(), stream);
         HIPC(hipStreamSynchronize(stream));  // host tables are freed when the caller returns
         ensure_schedule(T);
         const int64_t nl = (int64_t)sched_off.size() - 1;
+        if (timing) ensure_events(2 * (size_t)nl + 2);
+        if (timing) HIPC(hipEventRecord(events[2 * nl], stream));
+
+        mcr::InterpArgs ia{};
+        ia.F = Fsrc;
+        ia.srow = srow.p;
+        ia.sfrac = sfrac.p;
+        ia.G = G.p;
+        ia.Q = Q.p;
+        ia.nslots = plan.nslots;
+        ia.T = (int32_t)T;
+        ia.Tp = (int32_t)Tp;
+        HIPC(mcr::launch_interp(ia, stream));
+
         mcr::WaveArgs a{};
         a.G = G.p;
         a.flags = flags.p;
@@ -275,25 +316,26 @@ struct Net {
         a.ext_off = ext_off.p;
         a.ext_src = ext_src.p;
         a.ext_g = ext_g.p;
+        a.rpad = rpad.p;
         a.alpha = alpha.p;
         a.beta = beta.p;
         a.chi = chi.p;
         a.gamma = gamma.p;
         a.st_o = st_o.p;
         a.st_i = st_i.p;
-        a.F = Fsrc;
-        a.srow = srow.p;
-        a.sw = sw.p;
+        a.Q = Q.p;
         a.O = O.p;
         a.I = I.p;
+        a.dummy = dummy.p;
         a.nslots = plan.nslots;
-        a.n_rows = (int32_t)rows;
         a.T = (int32_t)T;
+        a.Tp = (int32_t)Tp;
         a.tile = plan.p.tile;
-        const size_t lds = (2 * (size_t)plan.p.slots + (size_t)plan.max_ext_wg * plan.p.tile) *
-                           sizeof(double);
-        if (timing) ensure_events(2 * (size_t)nl + 2);
-        if (timing) HIPC(hipEventRecord(events[2 * nl], stream));
+        a.ext_cap = plan.max_ext_wg;
+        a.more_cap = more_cap;
+        const size_t lds = (2 * (size_t)plan.p.slots + (size_t)a.ext_cap * a.tile) *
+                               sizeof(double) +
+                           (size_t)a.more_cap * sizeof(unsigned);
         int64_t launched = 0;
         for (int64_t k = 0; k < nl; ++k) {
             const int64_t grid = sched_off[k + 1] - sched_off[k];
@@ -305,8 +347,8 @@ struct Net {
             if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
             ++launched;
         }
-        HIPC(mcr::launch_final_state(O.p, I.p, st_o.p, st_i.p, slot_reach.p, plan.nslots, T,
-                                     stream));
+        HIPC(mcr::launch_final_state(O.p, I.p, st_o.p, st_i.p, slot_reach.p, G.p, plan.nslots,
+                                     Tp, T, stream));
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
             HIPC(hipEventSynchronize(events[2 * nl + 1]));
@@ -321,6 +363,7 @@ struct Net {
             launches += launched;
         }
         T_out = T;
+        Tp_out = Tp;
     }
 
     void load_forcing(int64_t rows, const double* xps, const double* fp) {
@@ -344,25 +387,23 @@ struct Net {
         REQUIRE(n_rows > 0, "mc_load_forcing must be called before mc_run");
         REQUIRE(x != nullptr, "x must not be NULL");
         std::vector<int2> hr(T);
-        std::vector<double2> hw(T);
+        std::vector<double> hf(T, 0.0);
         for (int64_t t = 0; t < T; ++t) {  // nutils.py:21-33
             const double xt = x[t];
             const int64_t ix = searchsorted_left(xp.data(), n_rows, xt);
             if (ix == 0) {
                 hr[t] = make_int2(0, -1);
-                hw[t] = make_double2(1.0, 0.0);
             } else if (ix >= n_rows) {
                 hr[t] = make_int2((int)(n_rows - 1), -1);
-                hw[t] = make_double2(1.0, 0.0);
             } else {
+                // the device forms (1 - frac) * f[ix-1] + frac * f[ix] exactly as numpy does
                 const double dx0 = xt - xp[ix - 1];
                 const double dx1 = xp[ix] - xt;
-                const double frac = dx0 / (dx0 + dx1);
                 hr[t] = make_int2((int)(ix - 1), (int)ix);
-                hw[t] = make_double2(1 - frac, frac);
+                hf[t] = dx0 / (dx0 + dx1);
             }
         }
-        run_tables(T, F.p, n_rows, hr, hw);
+        run_tables(T, F.p, n_rows, hr, hf);
     }
 
     void step(const double* q, double* i_out, double* o_out) {
@@ -371,11 +412,11 @@ struct Net {
         Fstep.reserve(std::max<int64_t>(plan.nslots, 1));
         if (n) to_slots(q, Fstep);
         std::vector<int2> hr(1, make_int2(0, -1));
-        std::vector<double2> hw(1, make_double2(1.0, 0.0));
-        run_tables(1, Fstep.p, 1, hr, hw);
-        if (n) {
-            HIPC(hipMemcpyAsync(o_out, O.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
-            HIPC(hipMemcpyAsync(i_out, I.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+        std::vector<double> hf(1, 0.0);
+        run_tables(1, Fstep.p, 1, hr, hf);
+        if (n) {  // the new state is the output of the step
+            from_slots(st_o, o_out);
+            from_slots(st_i, i_out);
         }
         HIPC(hipStreamSynchronize(stream));
     }
@@ -388,13 +429,13 @@ struct Net {
         if (n == 0 || k == 0) return;
         outT.reserve((size_t)n * k);
         if (oo) {
-            HIPC(mcr::launch_transpose(O.p, outT.p, n, T_out, t0, t1, stream));
+            HIPC(mcr::launch_transpose(O.p, rpad.p, outT.p, n, Tp_out, t0, t1, stream));
             HIPC(hipMemcpyAsync(oo, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             HIPC(hipStreamSynchronize(stream));
         }
         if (io) {
-            HIPC(mcr::launch_transpose(I.p, outT.p, n, T_out, t0, t1, stream));
+            HIPC(mcr::launch_transpose(I.p, rpad.p, outT.p, n, Tp_out, t0, t1, stream));
             HIPC(hipMemcpyAsync(io, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             HIPC(hipStreamSynchronize(stream));
@@ -403,12 +444,18 @@ struct Net {
 
     void fetch_series(double* oo, double* io) {
         REQUIRE(T_out > 0, "no outputs: call mc_run first");
-        const size_t bytes = (size_t)plan.n * T_out * sizeof(double);
-        if (oo && bytes)
-            HIPC(hipMemcpyAsync(oo, O.p, bytes, hipMemcpyDeviceToHost, stream));
-        if (io && bytes)
-            HIPC(hipMemcpyAsync(io, I.p, bytes, hipMemcpyDeviceToHost, stream));
-        HIPC(hipStreamSynchronize(stream));
+        const int64_t n = plan.n;
+        if (n == 0) return;
+        outT.reserve((size_t)n * T_out);
+        const size_t bytes = (size_t)n * T_out * sizeof(double);
+        for (int k = 0; k < 2; ++k) {
+            double* dst = k == 0 ? oo : io;
+            if (!dst) continue;
+            HIPC(mcr::launch_compact(k == 0 ? O.p : I.p, rpad.p, outT.p, n, Tp_out, T_out,
+                                     stream));
+            HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
+            HIPC(hipStreamSynchronize(stream));
+        }
     }
 };
 
@@ -591,15 +638,6 @@ int mc_simulate(void* net, int64_t T, const double* x, int64_t n_rows, const dou
         N->load_forcing(n_rows, xp, fp);
         N->run(T, x);
         N->fetch(0, T, out_o, out_i);
-    });
-}
-
-int mc_output_device_ptrs(void* net, void** o_dev, void** i_dev, int64_t* T) {
-    return guarded([&] {
-        Net* N = as_net(net);
-        if (o_dev) *o_dev = N->O.p;
-        if (i_dev) *i_dev = N->I.p;
-        if (T) *T = N->T_out;
     });
 }
 

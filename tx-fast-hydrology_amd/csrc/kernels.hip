@@ -20,125 +20,169 @@ namespace mcr {
 
 namespace {
 
+// Loads/stores of one 16-tick chunk (128 B): 8 x 16-byte accesses, addresses 16-B aligned.
+__device__ __forceinline__ void load_chunk(double (&v)[kChunk], const double* p) {
+    const double2* q = reinterpret_cast<const double2*>(p);
+#pragma unroll
+    for (int k = 0; k < kChunk / 2; ++k) {
+        const double2 x = q[k];
+        v[2 * k] = x.x;
+        v[2 * k + 1] = x.y;
+    }
+}
+
+__device__ __forceinline__ void store_chunk(double* p, const double (&v)[kChunk]) {
+    double2* q = reinterpret_cast<double2*>(p);
+#pragma unroll
+    for (int k = 0; k < kChunk / 2; ++k) q[k] = make_double2(v[2 * k], v[2 * k + 1]);
+}
+
 template <int SLOTS>
 __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* xb = smem;                  // [2][SLOTS] outflow of the previous / current tick
-    double* xe = smem + 2 * SLOTS;      // [n_ext][tile] external inputs of this launch
+    const int tile = a.tile;
+    double* xb = smem;                                  // [2][SLOTS] outflows, tick parity
+    double* xe = smem + 2 * SLOTS;                      // [ext_cap][tile] external inputs
+    unsigned* xm = reinterpret_cast<unsigned*>(xe + (size_t)a.ext_cap * tile);  // overflow codes
 
     const int tid = threadIdx.x;
     const int w = a.active[blockIdx.x];
     const int64_t d = (int64_t)w * SLOTS + tid;
-    const int tile = a.tile;
     const int T = a.T;
+    const int64_t Tp = a.Tp;
     const int k0 = a.kappa0;
 
-    // ---- prologue: external inputs (produced by earlier launches) -> LDS
+    // ---- prologue 1: external inputs (produced by earlier launches) -> LDS
     const int e0 = a.ext_off[w];
     const int ne = a.ext_off[w + 1] - e0;
     for (int idx = tid; idx < ne * tile; idx += SLOTS) {
         const int e = idx / tile;
         const int i = idx - e * tile;
         const int t = k0 + i - a.ext_g[e0 + e];
-        double v = 0.0;
-        if (t >= 0 && t < T) v = a.O[a.ext_src[e0 + e] * (int64_t)T + t];
-        xe[idx] = v;
+        const int64_t code = a.ext_src[e0 + e];          // caller row * 16 + pad
+        const bool ok = t >= 0 && t < T;
+        const double v = a.O[ok ? (code >> 4) * Tp + (code & 15) + t : 0];
+        xe[idx] = ok ? v : 0.0;
     }
+    // ---- prologue 2: overflow upstream codes of this workgroup -> LDS
+    const int m0 = a.up_more_off[(int64_t)w * SLOTS];
+    const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
+    for (int idx = tid; idx < nm; idx += SLOTS) xm[idx] = a.up_more[m0 + idx];
 
     // ---- per-reach registers
     const uint8_t fl = a.flags[d];
     const int G = a.G[d];
+    const int gq = G & ~(kChunk - 1);                   // padded position p = tick - gq
     const int64_t row = a.slot_reach[d];
-    const int t_first = k0 - G;               // model step at the first tick of this launch
-    double al = 0.0, be = 0.0, ch = 0.0, ga = 0.0, op = 0.0, ip = 0.0;
-    int cnt = 0, more = 0;
-    uint64_t up4 = 0;
-    // live: the reach has at least one model step inside this launch's ticks
-    const bool live = (fl != kSlotPad) && (t_first < T) && (t_first + tile > 0);
-    if (live) {
-        al = a.alpha[d];
-        be = a.beta[d];
-        ch = a.chi[d];
-        ga = a.gamma[d];
-        cnt = a.up_cnt[d];
-        up4 = a.up4[d];
-        more = a.up_more_off[d];
-    }
-    // state at step t_first - 1: initial state, or this reach's output from an earlier launch
-    if (fl != kSlotPad && t_first <= T && t_first + tile > 0) {
-        if (t_first <= 0) {
-            op = a.st_o[d];
-            ip = a.st_i[d];
-        } else {
-            op = a.O[row * T + (t_first - 1)];
-            ip = a.I[row * T + (t_first - 1)];
-        }
-    }
-    // the downstream reach (one tick behind) reads this reach's step t_first - 1 outflow at the
-    // first tick of the launch
-    xb[((k0 - 1) & 1) * SLOTS + tid] = op;
+    const bool real = fl != kSlotPad;
+    const int t_first = k0 - G;                         // step at this launch's first tick
+    const bool live = real && (t_first < T) && (t_first + tile > 0);
+    const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
+    const int cnt = a.up_cnt[d];
+    const uint64_t up4 = a.up4[d];
+    const int more = a.up_more_off[d] - m0;
+    // state at step t_first - 1: initial state or this reach's output from an earlier launch
+    const bool from_out = real && t_first >= 1 && t_first <= T;
+    const int64_t obase = real ? row * Tp : 0;
+    const double o_ld = a.O[from_out ? obase + (k0 - gq) - 1 : 0];
+    const double i_ld = a.I[from_out ? obase + (k0 - gq) - 1 : 0];
+    double op = from_out ? o_ld : a.st_o[d];
+    double ip = from_out ? i_ld : a.st_i[d];
+    const double* qrow = a.Q + d * Tp;
 
-    // forcing bracket kept in registers; step table prefetched one tick ahead
-    int r_lo = -1, r_hi = -1, r_nx = -1;
-    double f_lo = 0.0, f_hi = 0.0, f_nx = 0.0;
-    int tc = t_first < 0 ? 0 : (t_first >= T ? T - 1 : t_first);
-    int2 rr_n = make_int2(0, -1);
-    double2 ww_n = make_double2(0.0, 0.0);
-    if (live) {
-        rr_n = a.srow[tc];
-        ww_n = a.sw[tc];
+    // first chunk of lateral inflow
+    double qn[kChunk];
+    {
+        const int p = k0 - gq;
+        load_chunk(qn, (real && p >= 0 && p < Tp) ? qrow + p : a.dummy);
     }
+    // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
+    xb[((k0 - 1) & 1) * SLOTS + tid] = op;
+    // drain every prologue load here: otherwise the wait-count pass carries "pending" state for
+    // op/ip into the tick loop and waits for each chunk's stores at every tick
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 
-    for (int i = 0; i < tile; ++i) {
-        const int k = k0 + i;
-        const int t = k - G;
-        const int2 rr = rr_n;
-        const double2 ww = ww_n;
-        if (live && t >= 0 && t < T) {
-            if (t + 1 < T) {                  // prefetch next tick's step table entry
-                rr_n = a.srow[t + 1];
-                ww_n = a.sw[t + 1];
-            }
-            // inflow: upstream outflows in reference finalisation order
-            double I = 0.0;
-            const double* prev = xb + ((k - 1) & 1) * SLOTS;
-            for (int u = 0; u < cnt; ++u) {
-                const unsigned code = u < kUpInline ? (unsigned)((up4 >> (16 * u)) & 0xffffu)
-                                                    : (unsigned)a.up_more[more + u - kUpInline];
-                const double v = (code & kExtBit) ? xe[(code & 0x7fffu) * tile + i] : prev[code];
-                I = I + v;
-            }
-            // lateral inflow (interpolate_sample, linear)
-            if (rr.x != r_lo) {
-                if (rr.x == r_hi) f_lo = f_hi;
-                else if (rr.x == r_nx) f_lo = f_nx;
-                else f_lo = a.F[(int64_t)rr.x * a.nslots + d];
-                r_lo = rr.x;
-            }
-            double q;
-            if (rr.y < 0) {
-                q = f_lo;
-            } else {
-                if (rr.y != r_hi) {
-                    f_hi = (rr.y == r_nx) ? f_nx : a.F[(int64_t)rr.y * a.nslots + d];
-                    r_hi = rr.y;
-                    if (r_hi + 1 < a.n_rows && r_nx != r_hi + 1) {   // next row, ~1 bracket ahead
-                        r_nx = r_hi + 1;
-                        f_nx = a.F[(int64_t)r_nx * a.nslots + d];
-                    }
-                }
-                q = ww.x * f_lo + ww.y * f_hi;
-            }
-            double o = 0.0;
-            if (fl == kSlotRouted) o = 0.0 + (((al * I + be * ip) + ch * op) + ga * q);
-            xb[(k & 1) * SLOTS + tid] = o;
-            a.O[row * T + t] = o;
-            a.I[row * T + t] = I;
-            op = o;
-            ip = I;
+    for (int c = 0; c < tile; c += kChunk) {
+        const int kc = k0 + c;
+        const int pc = kc - gq;                         // multiple of kChunk
+        double qc[kChunk];
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) qc[i] = qn[i];
+        {                                               // prefetch the next chunk
+            const int p = pc + kChunk;
+            load_chunk(qn, (real && p >= 0 && p < Tp) ? qrow + p : a.dummy);
         }
-        __syncthreads();
+        double ob[kChunk], ib[kChunk];
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) {
+            const int k = kc + i;
+            const int t = k - G;
+            const bool act = live && t >= 0 && t < T;
+            double I = 0.0, o = 0.0;
+            if (act) {
+                // inflow: upstream outflows in reference finalisation order
+                const double* prev = xb + ((k - 1) & 1) * SLOTS;
+                const int col = c + i;
+                double v[kUpInline];
+#pragma unroll
+                for (int u = 0; u < kUpInline; ++u) {
+                    const unsigned code = (unsigned)((up4 >> (16 * u)) & 0xffffu);
+                    const double* src = (code & kExtBit) ? xe + (code & 0x7fffu) * tile + col
+                                                         : prev + (code & (SLOTS - 1));
+                    v[u] = *src;
+                }
+#pragma unroll
+                for (int u = 0; u < kUpInline; ++u)
+                    if (u < cnt) I = I + v[u];
+                for (int u = kUpInline; u < cnt; ++u) {
+                    const unsigned code = xm[more + u - kUpInline];
+                    const double* src = (code & kExtBit) ? xe + (code & 0x7fffu) * tile + col
+                                                         : prev + (code & (SLOTS - 1));
+                    I = I + *src;
+                }
+                if (fl == kSlotRouted) o = 0.0 + (((al * I + be * ip) + ch * op) + ga * qc[i]);
+                xb[(k & 1) * SLOTS + tid] = o;
+                op = o;
+                ip = I;
+            }
+            ob[i] = o;
+            ib[i] = I;
+            __syncthreads();
+        }
+        // whole aligned line per row and array; out-of-row chunks go to the dummy line
+        const bool in_row = real && pc >= 0 && pc < Tp;
+        store_chunk(in_row ? a.O + obase + pc : a.dummy, ob);
+        store_chunk(in_row ? a.I + obase + pc : a.dummy + kChunk, ib);
+    }
+}
+
+// Q[d][t + pad] = interpolated lateral inflow of step t; whole aligned chunks per slot.
+__global__ __launch_bounds__(256) void interp_q(InterpArgs a) {
+    const int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (d >= a.nslots) return;
+    const int pad = a.G[d] & (kChunk - 1);
+    double* qrow = a.Q + d * (int64_t)a.Tp;
+    for (int p0 = 0; p0 < a.Tp; p0 += kChunk) {
+        double v[kChunk];
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) {
+            const int t = p0 + i - pad;
+            double q = 0.0;
+            if (t >= 0 && t < a.T) {
+                const int2 rr = a.srow[t];
+                const double flo = a.F[(int64_t)rr.x * a.nslots + d];
+                if (rr.y < 0) {
+                    q = flo;
+                } else {
+                    const double fr = a.sfrac[t];
+                    const double fhi = a.F[(int64_t)rr.y * a.nslots + d];
+                    q = (1.0 - fr) * flo + fr * fhi;
+                }
+            }
+            v[i] = q;
+        }
+        store_chunk(qrow + p0, v);
     }
 }
 
@@ -173,21 +217,24 @@ __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restri
 
 __global__ void final_state(const double* __restrict__ O, const double* __restrict__ I,
                             double* __restrict__ st_o, double* __restrict__ st_i,
-                            const int64_t* __restrict__ slot_reach, int64_t nslots, int64_t T) {
+                            const int64_t* __restrict__ slot_reach, const int32_t* __restrict__ G,
+                            int64_t nslots, int64_t Tp, int64_t T) {
     for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < nslots;
          d += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = slot_reach[d];
         if (j >= 0) {
-            st_o[d] = O[j * T + (T - 1)];
-            st_i[d] = I[j * T + (T - 1)];
+            const int64_t at = j * Tp + (G[d] & (kChunk - 1)) + (T - 1);
+            st_o[d] = O[at];
+            st_i[d] = I[at];
         }
     }
 }
 
-// 64 x 64 tile transpose through LDS: reads 512-B row segments of O, writes 512-B rows of out.
-__global__ __launch_bounds__(256) void transpose_rt(const double* __restrict__ O,
+// 64 x 64 tile transpose through LDS: reads row segments of S, writes 512-B rows of out.
+__global__ __launch_bounds__(256) void transpose_rt(const double* __restrict__ S,
+                                                    const uint8_t* __restrict__ rpad,
                                                     double* __restrict__ out, int64_t n,
-                                                    int64_t T, int64_t t0, int64_t t1) {
+                                                    int64_t Tp, int64_t t0, int64_t t1) {
     __shared__ double tileb[64][65];
     const int64_t j0 = (int64_t)blockIdx.x * 64;
     const int64_t tb = t0 + (int64_t)blockIdx.y * 64;
@@ -196,13 +243,24 @@ __global__ __launch_bounds__(256) void transpose_rt(const double* __restrict__ O
     for (int r = ly; r < 64; r += 4) {
         const int64_t j = j0 + r;
         const int64_t t = tb + lx;
-        tileb[r][lx] = (j < n && t < t1) ? O[j * T + t] : 0.0;
+        tileb[r][lx] = (j < n && t < t1) ? S[j * Tp + rpad[j] + t] : 0.0;
     }
     __syncthreads();
     for (int r = ly; r < 64; r += 4) {
         const int64_t t = tb + r;
         const int64_t j = j0 + lx;
         if (t < t1 && j < n) out[(t - t0) * n + j] = tileb[lx][r];
+    }
+}
+
+__global__ void compact_rows(const double* __restrict__ S, const uint8_t* __restrict__ rpad,
+                             double* __restrict__ out, int64_t n, int64_t Tp, int64_t T) {
+    const int64_t total = n * T;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = x / T;
+        const int64_t t = x - j * T;
+        out[x] = S[j * Tp + rpad[j] + t];
     }
 }
 
@@ -227,6 +285,12 @@ hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds, 
     return hipGetLastError();
 }
 
+hipError_t launch_interp(const InterpArgs& a, hipStream_t s) {
+    if (a.nslots <= 0) return hipSuccess;
+    hipLaunchKernelGGL(interp_q, (unsigned)((a.nslots + 255) / 256), 256, 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,
                                    int64_t nslots, hipStream_t s) {
     hipLaunchKernelGGL(scatter_to_slots, grid_for(nslots, 256), 256, 0, s, src, dst, slot_reach,
@@ -248,18 +312,25 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
 }
 
 hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,
-                              const int64_t* slot_reach, int64_t nslots, int64_t T,
-                              hipStream_t s) {
+                              const int64_t* slot_reach, const int32_t* G, int64_t nslots,
+                              int64_t Tp, int64_t T, hipStream_t s) {
     hipLaunchKernelGGL(final_state, grid_for(nslots, 256), 256, 0, s, O, I, st_o, st_i,
-                       slot_reach, nslots, T);
+                       slot_reach, G, nslots, Tp, T);
     return hipGetLastError();
 }
 
-hipError_t launch_transpose(const double* O, double* out, int64_t n, int64_t T, int64_t t0,
-                            int64_t t1, hipStream_t s) {
+hipError_t launch_transpose(const double* S, const uint8_t* rpad, double* out, int64_t n,
+                            int64_t Tp, int64_t t0, int64_t t1, hipStream_t s) {
     if (n <= 0 || t1 <= t0) return hipSuccess;
     dim3 grid((unsigned)((n + 63) / 64), (unsigned)((t1 - t0 + 63) / 64));
-    hipLaunchKernelGGL(transpose_rt, grid, 256, 0, s, O, out, n, T, t0, t1);
+    hipLaunchKernelGGL(transpose_rt, grid, 256, 0, s, S, rpad, out, n, Tp, t0, t1);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const double* S, const uint8_t* rpad, double* out, int64_t n,
+                          int64_t Tp, int64_t T, hipStream_t s) {
+    if (n <= 0 || T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(compact_rows, grid_for(n * T, 256), 256, 0, s, S, rpad, out, n, Tp, T);
     return hipGetLastError();
 }
 

@@ -8,8 +8,16 @@
 
 namespace mcr {
 
+// Ticks per register chunk.  Series rows are padded so that a chunk always covers one aligned
+// 128-byte line: step t of reach j lives at  row(j) * Tp + t + (G[j] & (kChunk - 1)).
+constexpr int kChunk = 16;
+
+inline int64_t padded_steps(int64_t T) {  // Tp: room for the pad and a full trailing chunk
+    return ((T + 2 * kChunk - 1) / kChunk) * kChunk;
+}
+
 // Everything the wavefront kernel reads, by value.  Per-slot arrays are in device-slot order
-// (plan.hpp), outputs are reach-major in the caller's reach order: O[j * T + t].
+// (plan.hpp); the output series are reach-major in the CALLER's order, padded as above.
 struct WaveArgs {
     const int32_t* active;        // workgroup ids of this launch
     const int32_t* G;             // [nslots]
@@ -20,29 +28,44 @@ struct WaveArgs {
     const uint16_t* up_more;
     const int64_t* slot_reach;    // [nslots] caller reach index or -1
     const int32_t* ext_off;       // [nwg + 1]
-    const int64_t* ext_src;       // caller reach index of the upstream reach
+    const int64_t* ext_src;       // caller index of the upstream reach
     const int32_t* ext_g;         // G of the consuming reach
+    const uint8_t* rpad;          // [n] pad of each caller reach (G & 15)
     const double* alpha;          // [nslots]
     const double* beta;
     const double* chi;
     const double* gamma;
     const double* st_o;           // state at step -1 (o_t_next before the horizon) [nslots]
     const double* st_i;
-    const double* F;              // forcing rows, device-slot order [n_rows][nslots]
-    const int2* srow;             // per step: (row_lo, row_hi) or (row, -1) = copy row
-    const double2* sw;            // per step: (1 - frac, frac)
-    double* O;                    // [n][T]
-    double* I;                    // [n][T]
+    const double* Q;              // lateral inflow per step, [nslots][Tp] padded like O
+    double* O;                    // [n][Tp]
+    double* I;                    // [n][Tp]
+    double* dummy;                // >= 2 * kChunk doubles: target of out-of-range chunks
     int64_t nslots;
-    int32_t n_rows;
     int32_t T;
-    int32_t kappa0;               // first tick of this launch
-    int32_t tile;                 // ticks in this launch
+    int32_t Tp;
+    int32_t kappa0;               // first tick of this launch (multiple of kChunk)
+    int32_t tile;                 // ticks in this launch (multiple of kChunk)
+    int32_t ext_cap;              // LDS rows reserved for external inputs
+    int32_t more_cap;             // LDS words reserved for overflow upstream codes
 };
 
-// One launch: `grid` workgroups of `slots` threads sweep ticks [kappa0, kappa0 + tile).
+// Interpolated lateral inflow (nutils.py:23-33) for every slot and step:
+//   Q[d][t + pad] = row copy, or (1 - frac) * F[lo][d] + frac * F[hi][d]
+struct InterpArgs {
+    const double* F;              // [n_rows][nslots] forcing in slot order
+    const int2* srow;             // [T] (row_lo, row_hi) or (row, -1) = copy
+    const double* sfrac;          // [T]
+    const int32_t* G;             // [nslots] (pad = G & 15)
+    double* Q;                    // [nslots][Tp]
+    int64_t nslots;
+    int32_t T;
+    int32_t Tp;
+};
+
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
                             hipStream_t s);
+hipError_t launch_interp(const InterpArgs& a, hipStream_t s);
 
 // st[d] = src[slot_reach[d]] for real slots (caller order -> slot order)
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,
@@ -53,12 +76,15 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 // F[r][d] = fp[r][slot_reach[d]]  (forcing table to slot order; 0 for padding slots)
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, hipStream_t s);
-// st[d] = O[slot_reach[d] * T + (T - 1)]   (state after the last step)
+// state after the last step: st[d] = O[row(d)][T - 1]
 hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,
-                              const int64_t* slot_reach, int64_t nslots, int64_t T,
-                              hipStream_t s);
-// out[t - t0][j] = O[j * T + t]  for t in [t0, t1), j in [0, n)   (reach-major -> step-major)
-hipError_t launch_transpose(const double* O, double* out, int64_t n, int64_t T, int64_t t0,
-                            int64_t t1, hipStream_t s);
+                              const int64_t* slot_reach, const int32_t* G, int64_t nslots,
+                              int64_t Tp, int64_t T, hipStream_t s);
+// out[t - t0][j] = S[j][t]  for t in [t0, t1)   (padded reach-major -> step-major)
+hipError_t launch_transpose(const double* S, const uint8_t* rpad, double* out, int64_t n,
+                            int64_t Tp, int64_t t0, int64_t t1, hipStream_t s);
+// out[j][t] = S[j][t] for t in [0, T)   (drop the padding)
+hipError_t launch_compact(const double* S, const uint8_t* rpad, double* out, int64_t n,
+                          int64_t Tp, int64_t T, hipStream_t s);
 
 }  // namespace mcr

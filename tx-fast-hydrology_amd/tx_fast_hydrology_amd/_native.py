@@ -83,7 +83,6 @@ SIGNATURES = {
     "mc_fetch_outputs": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "mc_fetch_series": (_i32, [_vp, _vp, _vp]),
     "mc_simulate": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
-    "mc_output_device_ptrs": (_i32, [_vp, _pp, _pp, ctypes.POINTER(ctypes.c_int64)]),
     "mc_synchronize": (_i32, [_vp]),
     "mc_set_timing": (_i32, [_vp, ctypes.c_int]),
     "mc_get_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),

@@ -186,14 +186,6 @@ class RoutingNet:
         self.run(x)
         return self.fetch_outputs()
 
-    def device_outputs(self):
-        o = ctypes.c_void_p()
-        i = ctypes.c_void_p()
-        T = ctypes.c_int64()
-        nat.check(nat.lib().mc_output_device_ptrs(self._h, ctypes.byref(o), ctypes.byref(i),
-                                                  ctypes.byref(T)))
-        return o.value, i.value, T.value
-
     def synchronize(self):
         nat.check(nat.lib().mc_synchronize(self._h))
 
