@@ -128,6 +128,13 @@ int64_t searchsorted_left(const double* xp, int64_t n, double x) {
     return lo;
 }
 
+// {row_lo, row_hi (-1: copy row_lo), frac as two 32-bit halves (lo, hi)}
+int4 step_entry(int lo, int hi, double frac) {
+    uint64_t bits;
+    std::memcpy(&bits, &frac, sizeof(bits));
+    return make_int4(lo, hi, (int)(uint32_t)(bits & 0xffffffffu), (int)(uint32_t)(bits >> 32));
+}
+
 struct Net {
     mcr::Plan plan;
     int device = 0;
@@ -135,7 +142,7 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, up_more_off, ext_off, ext_g, active;
+    DBuf<int32_t> G, up_more_off, ext_off, ext_g, active, wg_gmin, wg_gmax;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
     DBuf<uint16_t> up_more;
@@ -148,12 +155,11 @@ struct Net {
     DBuf<double> F, Fstep, stage;
     int64_t n_rows = 0;
     std::vector<double> xp;
-    // step tables
-    DBuf<int2> srow;
-    DBuf<double> sfrac;
-    // interpolated lateral inflow [nslots][Tp], outputs [n][Tp] (caller order, padded rows),
-    // a step-major scratch for fetches and the dummy line of out-of-row chunks
-    DBuf<double> Q, O, I, outT, dummy;
+    // per-step interpolation table {row_lo, row_hi, frac}
+    DBuf<int4> stab;
+    // outputs [n][Tp] (caller order, padded rows), a step-major scratch for fetches and the
+    // dummy line of out-of-row chunks
+    DBuf<double> O, I, outT, dummy;
     int64_t T_out = 0, Tp_out = 0;
     bool coeffs_set = false;
 
@@ -211,6 +217,8 @@ struct Net {
         }
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
+        wg_gmin.upload(plan.wg_gmin.data(), plan.wg_gmin.size(), stream);
+        wg_gmax.upload(plan.wg_gmax.data(), plan.wg_gmax.size(), stream);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
             b->reserve(ns);
             HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
@@ -270,9 +278,8 @@ struct Net {
         }
     }
 
-    // Run T steps using forcing buffer `Fsrc` with `rows` rows and host step tables.
-    void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int2>& hr,
-                    const std::vector<double>& hf) {
+    // Run T steps using forcing buffer `Fsrc` with `rows` rows and the host step table.
+    void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int4>& tabh) {
         REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
         REQUIRE(T >= 1 && T < (1ll << 30), "T out of range");
         const int64_t n = plan.n;
@@ -285,25 +292,12 @@ struct Net {
         }
         O.reserve((size_t)n * Tp);
         I.reserve((size_t)n * Tp);
-        Q.reserve((size_t)plan.nslots * Tp);
-        srow.upload(hr.data(), hr.size(), stream);
-        sfrac.upload(hf.data(), hf.size(), stream);
-        HIPC(hipStreamSynchronize(stream));  // host tables are freed when the caller returns
+        stab.upload(tabh.data(), tabh.size(), stream);
+        HIPC(hipStreamSynchronize(stream));  // the host table is freed when the caller returns
         ensure_schedule(T);
         const int64_t nl = (int64_t)sched_off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
         if (timing) HIPC(hipEventRecord(events[2 * nl], stream));
-
-        mcr::InterpArgs ia{};
-        ia.F = Fsrc;
-        ia.srow = srow.p;
-        ia.sfrac = sfrac.p;
-        ia.G = G.p;
-        ia.Q = Q.p;
-        ia.nslots = plan.nslots;
-        ia.T = (int32_t)T;
-        ia.Tp = (int32_t)Tp;
-        HIPC(mcr::launch_interp(ia, stream));
 
         mcr::WaveArgs a{};
         a.G = G.p;
@@ -323,19 +317,23 @@ struct Net {
         a.gamma = gamma.p;
         a.st_o = st_o.p;
         a.st_i = st_i.p;
-        a.Q = Q.p;
+        a.F = Fsrc;
+        a.stab = stab.p;
+        a.wg_gmin = wg_gmin.p;
+        a.wg_gmax = wg_gmax.p;
         a.O = O.p;
         a.I = I.p;
         a.dummy = dummy.p;
         a.nslots = plan.nslots;
+        a.n_rows = (int32_t)rows;
         a.T = (int32_t)T;
         a.Tp = (int32_t)Tp;
         a.tile = plan.p.tile;
+        a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
         a.ext_cap = plan.max_ext_wg;
         a.more_cap = more_cap;
-        const size_t lds = (2 * (size_t)plan.p.slots + (size_t)a.ext_cap * a.tile) *
-                               sizeof(double) +
-                           (size_t)a.more_cap * sizeof(unsigned);
+        const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
+                                                    a.tile, a.more_cap);
         int64_t launched = 0;
         for (int64_t k = 0; k < nl; ++k) {
             const int64_t grid = sched_off[k + 1] - sched_off[k];
@@ -386,24 +384,24 @@ struct Net {
     void run(int64_t T, const double* x) {
         REQUIRE(n_rows > 0, "mc_load_forcing must be called before mc_run");
         REQUIRE(x != nullptr, "x must not be NULL");
-        std::vector<int2> hr(T);
-        std::vector<double> hf(T, 0.0);
+        for (int64_t t = 1; t < T; ++t)
+            REQUIRE(!(x[t] < x[t - 1]), "step times x must be non-decreasing");
+        std::vector<int4> tab(T);
         for (int64_t t = 0; t < T; ++t) {  // nutils.py:21-33
             const double xt = x[t];
             const int64_t ix = searchsorted_left(xp.data(), n_rows, xt);
             if (ix == 0) {
-                hr[t] = make_int2(0, -1);
+                tab[t] = step_entry(0, -1, 0.0);
             } else if (ix >= n_rows) {
-                hr[t] = make_int2((int)(n_rows - 1), -1);
+                tab[t] = step_entry((int)(n_rows - 1), -1, 0.0);
             } else {
                 // the device forms (1 - frac) * f[ix-1] + frac * f[ix] exactly as numpy does
                 const double dx0 = xt - xp[ix - 1];
                 const double dx1 = xp[ix] - xt;
-                hr[t] = make_int2((int)(ix - 1), (int)ix);
-                hf[t] = dx0 / (dx0 + dx1);
+                tab[t] = step_entry((int)(ix - 1), (int)ix, dx0 / (dx0 + dx1));
             }
         }
-        run_tables(T, F.p, n_rows, hr, hf);
+        run_tables(T, F.p, n_rows, tab);
     }
 
     void step(const double* q, double* i_out, double* o_out) {
@@ -411,9 +409,7 @@ struct Net {
         const int64_t n = plan.n;
         Fstep.reserve(std::max<int64_t>(plan.nslots, 1));
         if (n) to_slots(q, Fstep);
-        std::vector<int2> hr(1, make_int2(0, -1));
-        std::vector<double> hf(1, 0.0);
-        run_tables(1, Fstep.p, 1, hr, hf);
+        run_tables(1, Fstep.p, 1, std::vector<int4>(1, step_entry(0, -1, 0.0)));
         if (n) {  // the new state is the output of the step
             from_slots(st_o, o_out);
             from_slots(st_i, i_out);

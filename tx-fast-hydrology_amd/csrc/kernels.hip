@@ -5,7 +5,10 @@
 // One workgroup owns up to SLOTS reaches (one per lane).  Reach j handles model step t at tick
 // G[j] + t; an upstream reach in the same cluster runs one tick ahead, so its outflow is read
 // from an LDS double buffer written in the previous tick.  Inputs from other clusters were
-// produced in an earlier launch and are staged in LDS in the launch prologue.
+// produced in an earlier launch and are staged in LDS in the launch prologue, together with the
+// window of the per-step interpolation table this workgroup needs.  The tick loop issues no
+// global loads except the per-chunk forcing-row prefetch; outputs leave in whole 128-byte lines
+// (16 ticks per chunk, rows padded so every chunk is line aligned).
 //
 // Arithmetic follows the reference exactly (FMA contraction is off for this file):
 //   I = ((0 + o[u1]) + o[u2]) + ...          upstream reaches in reference finalisation order
@@ -20,29 +23,41 @@ namespace mcr {
 
 namespace {
 
-// Loads/stores of one 16-tick chunk (128 B): 8 x 16-byte accesses, addresses 16-B aligned.
-__device__ __forceinline__ void load_chunk(double (&v)[kChunk], const double* p) {
-    const double2* q = reinterpret_cast<const double2*>(p);
-#pragma unroll
-    for (int k = 0; k < kChunk / 2; ++k) {
-        const double2 x = q[k];
-        v[2 * k] = x.x;
-        v[2 * k + 1] = x.y;
-    }
-}
-
+// Store of one 16-tick chunk (128 B): 8 x 16-byte accesses, address 16-B aligned.
 __device__ __forceinline__ void store_chunk(double* p, const double (&v)[kChunk]) {
     double2* q = reinterpret_cast<double2*>(p);
 #pragma unroll
     for (int k = 0; k < kChunk / 2; ++k) q[k] = make_double2(v[2 * k], v[2 * k + 1]);
 }
 
+// Forcing rows a lane needs for the chunk starting at tick kc: [rb, rb + nr).  Rows are
+// non-decreasing in t (step times are increasing), so the first step's row_lo and the last
+// step's max(row_lo, row_hi) bound them.  nr = 0 when the lane has no step in the chunk.
+__device__ __forceinline__ void chunk_rows(const int4* tab, int tw0, int kc, int G, int T,
+                                           int& rb, int& nr) {
+    int ta = kc - G, tb = kc + kChunk - 1 - G;
+    if (tb < 0 || ta >= T) {
+        rb = 0;
+        nr = 0;
+        return;
+    }
+    ta = ta < 0 ? 0 : ta;
+    tb = tb >= T ? T - 1 : tb;
+    const int4 ea = tab[ta - tw0];
+    const int4 eb = tab[tb - tw0];
+    rb = ea.x;
+    nr = (eb.y > eb.x ? eb.y : eb.x) - rb + 1;
+}
+
+__device__ __forceinline__ int clamp_row(int r, int n_rows) { return r < n_rows ? r : n_rows - 1; }
+
 template <int SLOTS>
 __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tile = a.tile;
-    double* xb = smem;                                  // [2][SLOTS] outflows, tick parity
-    double* xe = smem + 2 * SLOTS;                      // [ext_cap][tile] external inputs
+    double* xb = smem;                                            // [2][SLOTS] outflows
+    int4* tab = reinterpret_cast<int4*>(smem + 2 * SLOTS);        // [table_cap] step table
+    double* xe = reinterpret_cast<double*>(tab + a.table_cap);    // [ext_cap][tile] ext inputs
     unsigned* xm = reinterpret_cast<unsigned*>(xe + (size_t)a.ext_cap * tile);  // overflow codes
 
     const int tid = threadIdx.x;
@@ -51,25 +66,10 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int T = a.T;
     const int64_t Tp = a.Tp;
     const int k0 = a.kappa0;
+    const int64_t ns = a.nslots;
+    const int nrow = a.n_rows;
 
-    // ---- prologue 1: external inputs (produced by earlier launches) -> LDS
-    const int e0 = a.ext_off[w];
-    const int ne = a.ext_off[w + 1] - e0;
-    for (int idx = tid; idx < ne * tile; idx += SLOTS) {
-        const int e = idx / tile;
-        const int i = idx - e * tile;
-        const int t = k0 + i - a.ext_g[e0 + e];
-        const int64_t code = a.ext_src[e0 + e];          // caller row * 16 + pad
-        const bool ok = t >= 0 && t < T;
-        const double v = a.O[ok ? (code >> 4) * Tp + (code & 15) + t : 0];
-        xe[idx] = ok ? v : 0.0;
-    }
-    // ---- prologue 2: overflow upstream codes of this workgroup -> LDS
-    const int m0 = a.up_more_off[(int64_t)w * SLOTS];
-    const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
-    for (int idx = tid; idx < nm; idx += SLOTS) xm[idx] = a.up_more[m0 + idx];
-
-    // ---- per-reach registers
+    // ---- per-reach registers and state at step t_first - 1 (issued first: longest latency)
     const uint8_t fl = a.flags[d];
     const int G = a.G[d];
     const int gq = G & ~(kChunk - 1);                   // padded position p = tick - gq
@@ -77,42 +77,81 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const bool real = fl != kSlotPad;
     const int t_first = k0 - G;                         // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
-    const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
-    const int cnt = a.up_cnt[d];
-    const uint64_t up4 = a.up4[d];
-    const int more = a.up_more_off[d] - m0;
-    // state at step t_first - 1: initial state or this reach's output from an earlier launch
     const bool from_out = real && t_first >= 1 && t_first <= T;
     const int64_t obase = real ? row * Tp : 0;
     const double o_ld = a.O[from_out ? obase + (k0 - gq) - 1 : 0];
     const double i_ld = a.I[from_out ? obase + (k0 - gq) - 1 : 0];
-    double op = from_out ? o_ld : a.st_o[d];
-    double ip = from_out ? i_ld : a.st_i[d];
-    const double* qrow = a.Q + d * Tp;
+    const double st_o = a.st_o[d], st_i = a.st_i[d];
+    const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
+    const int cnt = a.up_cnt[d];
+    const uint64_t up4 = a.up4[d];
+    const int m0 = a.up_more_off[(int64_t)w * SLOTS];
+    const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
+    const int more = a.up_more_off[d] - m0;
 
-    // first chunk of lateral inflow
-    double qn[kChunk];
-    {
-        const int p = k0 - gq;
-        load_chunk(qn, (real && p >= 0 && p < Tp) ? qrow + p : a.dummy);
+    // ---- step-table window of this workgroup -> LDS
+    const int gmin = a.wg_gmin[w], gmax = a.wg_gmax[w];
+    int tw0 = k0 - gmax, tw1 = k0 + tile - gmin;
+    tw0 = tw0 < 0 ? 0 : (tw0 > T ? T : tw0);
+    tw1 = tw1 < 0 ? 0 : (tw1 > T ? T : tw1);
+    for (int idx = tid; idx < tw1 - tw0; idx += SLOTS) tab[idx] = a.stab[tw0 + idx];
+
+    // ---- external inputs (produced by earlier launches) -> LDS, 8 loads in flight per lane
+    const int e0 = a.ext_off[w];
+    const int ntot = (a.ext_off[w + 1] - e0) * tile;
+    for (int base = tid; base < ntot; base += 8 * SLOTS) {
+        int ti[8], eg[8];
+        int64_t code[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {   // unconditional (clamped) loads: one wait per batch
+            const int idx = min(base + k * SLOTS, ntot - 1);
+            const int e = idx / tile;
+            ti[k] = k0 + (idx - e * tile);
+            eg[k] = a.ext_g[e0 + e];
+            code[k] = a.ext_src[e0 + e];                  // caller row * 16 + pad
+        }
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int t = ti[k] - eg[k];
+            const bool ok = t >= 0 && t < T;
+            v[k] = a.O[ok ? (code[k] >> 4) * Tp + (code[k] & 15) + t : 0];
+            v[k] = ok ? v[k] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (base + k * SLOTS < ntot) xe[base + k * SLOTS] = v[k];
     }
+    // ---- overflow upstream codes of this workgroup -> LDS
+    for (int idx = tid; idx < nm; idx += SLOTS) xm[idx] = a.up_more[m0 + idx];
+
+    double op = from_out ? o_ld : st_o;
+    double ip = from_out ? i_ld : st_i;
     // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
     xb[((k0 - 1) & 1) * SLOTS + tid] = op;
-    // drain every prologue load here: otherwise the wait-count pass carries "pending" state for
-    // op/ip into the tick loop and waits for each chunk's stores at every tick
+    // drain every prologue load: otherwise the wait-count pass carries "pending" state into
+    // the tick loop and waits for each chunk's stores at every tick
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+
+    // forcing rows of the first chunk (rows rb .. rb + 2 kept in registers)
+    int rb, nr;
+    chunk_rows(tab, tw0, k0, G, live ? T : 0, rb, nr);
+    double f0 = a.F[(int64_t)clamp_row(rb, nrow) * ns + d];
+    double f1 = a.F[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
+    double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
+    __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
 
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         const int pc = kc - gq;                         // multiple of kChunk
-        double qc[kChunk];
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) qc[i] = qn[i];
-        {                                               // prefetch the next chunk
-            const int p = pc + kChunk;
-            load_chunk(qn, (real && p >= 0 && p < Tp) ? qrow + p : a.dummy);
-        }
+        // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
+        int rbn, nrn;
+        chunk_rows(tab, tw0, kc + kChunk, G, (live && c + kChunk < tile) ? T : 0, rbn, nrn);
+        const double g0 = a.F[(int64_t)clamp_row(rbn, nrow) * ns + d];
+        const double g1 = a.F[(int64_t)clamp_row(rbn + 1, nrow) * ns + d];
+        const double g2 = a.F[(int64_t)clamp_row(rbn + 2, nrow) * ns + d];
+        const bool slow = nr > 3;                       // more rows than registers: load direct
         double ob[kChunk], ib[kChunk];
 #pragma unroll
         for (int i = 0; i < kChunk; ++i) {
@@ -121,6 +160,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
             const bool act = live && t >= 0 && t < T;
             double I = 0.0, o = 0.0;
             if (act) {
+                const int4 e = tab[t - tw0];
                 // inflow: upstream outflows in reference finalisation order
                 const double* prev = xb + ((k - 1) & 1) * SLOTS;
                 const int col = c + i;
@@ -141,7 +181,26 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                                                          : prev + (code & (SLOTS - 1));
                     I = I + *src;
                 }
-                if (fl == kSlotRouted) o = 0.0 + (((al * I + be * ip) + ch * op) + ga * qc[i]);
+                // lateral inflow, interpolate_sample (nutils.py:23-33)
+                double flo, fhi;
+                if (slow) {
+                    flo = a.F[(int64_t)e.x * ns + d];
+                    fhi = a.F[(int64_t)(e.y < 0 ? e.x : e.y) * ns + d];
+                    // settle these loads here so the common path inherits no pending state
+                    __builtin_amdgcn_s_waitcnt(0);
+                } else {
+                    const int kl = e.x - rb, kh = e.y - rb;
+                    flo = kl == 0 ? f0 : (kl == 1 ? f1 : f2);
+                    fhi = kh == 0 ? f0 : (kh == 1 ? f1 : f2);
+                }
+                double q;
+                if (e.y < 0) {
+                    q = flo;
+                } else {
+                    const double fr = __hiloint2double(e.w, e.z);
+                    q = (1.0 - fr) * flo + fr * fhi;
+                }
+                if (fl == kSlotRouted) o = 0.0 + (((al * I + be * ip) + ch * op) + ga * q);
                 xb[(k & 1) * SLOTS + tid] = o;
                 op = o;
                 ip = I;
@@ -154,35 +213,11 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         const bool in_row = real && pc >= 0 && pc < Tp;
         store_chunk(in_row ? a.O + obase + pc : a.dummy, ob);
         store_chunk(in_row ? a.I + obase + pc : a.dummy + kChunk, ib);
-    }
-}
-
-// Q[d][t + pad] = interpolated lateral inflow of step t; whole aligned chunks per slot.
-__global__ __launch_bounds__(256) void interp_q(InterpArgs a) {
-    const int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (d >= a.nslots) return;
-    const int pad = a.G[d] & (kChunk - 1);
-    double* qrow = a.Q + d * (int64_t)a.Tp;
-    for (int p0 = 0; p0 < a.Tp; p0 += kChunk) {
-        double v[kChunk];
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-            const int t = p0 + i - pad;
-            double q = 0.0;
-            if (t >= 0 && t < a.T) {
-                const int2 rr = a.srow[t];
-                const double flo = a.F[(int64_t)rr.x * a.nslots + d];
-                if (rr.y < 0) {
-                    q = flo;
-                } else {
-                    const double fr = a.sfrac[t];
-                    const double fhi = a.F[(int64_t)rr.y * a.nslots + d];
-                    q = (1.0 - fr) * flo + fr * fhi;
-                }
-            }
-            v[i] = q;
-        }
-        store_chunk(qrow + p0, v);
+        rb = rbn;
+        nr = nrn;
+        f0 = g0;
+        f1 = g1;
+        f2 = g2;
     }
 }
 
@@ -282,12 +317,6 @@ hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds, 
         case 1024: hipLaunchKernelGGL(wavefront_det<1024>, grid, 1024, lds, s, a); break;
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
-}
-
-hipError_t launch_interp(const InterpArgs& a, hipStream_t s) {
-    if (a.nslots <= 0) return hipSuccess;
-    hipLaunchKernelGGL(interp_q, (unsigned)((a.nslots + 255) / 256), 256, 0, s, a);
     return hipGetLastError();
 }
 

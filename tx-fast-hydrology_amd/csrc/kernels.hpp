@@ -37,35 +37,32 @@ struct WaveArgs {
     const double* gamma;
     const double* st_o;           // state at step -1 (o_t_next before the horizon) [nslots]
     const double* st_i;
-    const double* Q;              // lateral inflow per step, [nslots][Tp] padded like O
+    const double* F;              // forcing rows in slot order [n_rows][nslots]
+    const int4* stab;             // per step {row_lo, row_hi (-1 = copy row_lo), frac (f64)}
+    const int32_t* wg_gmin;       // [nwg] G range of each workgroup (step-table window)
+    const int32_t* wg_gmax;
     double* O;                    // [n][Tp]
     double* I;                    // [n][Tp]
     double* dummy;                // >= 2 * kChunk doubles: target of out-of-range chunks
     int64_t nslots;
+    int32_t n_rows;
     int32_t T;
     int32_t Tp;
     int32_t kappa0;               // first tick of this launch (multiple of kChunk)
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
+    int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
     int32_t more_cap;             // LDS words reserved for overflow upstream codes
 };
 
-// Interpolated lateral inflow (nutils.py:23-33) for every slot and step:
-//   Q[d][t + pad] = row copy, or (1 - frac) * F[lo][d] + frac * F[hi][d]
-struct InterpArgs {
-    const double* F;              // [n_rows][nslots] forcing in slot order
-    const int2* srow;             // [T] (row_lo, row_hi) or (row, -1) = copy
-    const double* sfrac;          // [T]
-    const int32_t* G;             // [nslots] (pad = G & 15)
-    double* Q;                    // [nslots][Tp]
-    int64_t nslots;
-    int32_t T;
-    int32_t Tp;
-};
+inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile,
+                                  int more_cap) {
+    return 16 * (size_t)slots + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile +
+           4 * (size_t)more_cap;
+}
 
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
                             hipStream_t s);
-hipError_t launch_interp(const InterpArgs& a, hipStream_t s);
 
 // st[d] = src[slot_reach[d]] for real slots (caller order -> slot order)
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,

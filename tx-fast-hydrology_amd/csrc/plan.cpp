@@ -33,13 +33,17 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     if (C < 64 || C > 1024 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 1024]";
     if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
     if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";
-    // LDS budget of one workgroup: 2 * slots outflows + ext_cap * tile external inputs
-    const int64_t lds_words = 160 * 1024 / 8;
-    if (2 * C + (int64_t)P.p.ext_cap * B > lds_words) {
-        const int64_t cap = (lds_words - 2 * C) / B;
-        if (cap < 1) return "slots/tile too large for the 160 KiB LDS of a workgroup";
-        P.p.ext_cap = (int32_t)cap;
+    // hard cap of external inputs: what is left of the LDS after the outflow double buffer,
+    // the step-table window and a reserve for overflow upstream codes
+    {
+        const int64_t left = kLdsBudget - 16 * C - kTableEntryBytes * table_entries(C, B) - 4096;
+        const int64_t hard = std::min<int64_t>(left / (8 * (int64_t)B), 0x7fff);
+        if (hard < 1) return "slots/tile too large for the 160 KiB LDS of a workgroup";
+        P.ext_hard = (int32_t)hard;
+        P.p.ext_cap = (int32_t)std::min<int64_t>(P.p.ext_cap, hard);
     }
+    const int32_t soft = P.p.ext_cap;
+    const int32_t hard = P.ext_hard;
     for (int64_t j = 0; j < n; ++j)
         if (endnodes[j] < 0 || endnodes[j] >= n) {
             std::ostringstream s;
@@ -139,9 +143,11 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         bool first = true;
         for (int64_t u : ups) {
             const Cluster& cu = clusters[cl[u]];
-            const bool costly = first || (eh[u] + B > best + 1);
+            // merge the deepest upstream, any upstream a cut would delay, and any upstream
+            // once the external-input budget is used up
+            const bool want = first || (eh[u] + B > best + 1) || (c.ext + 1 > soft);
             first = false;
-            if (costly && c.size + cu.size <= C && c.ext + cu.ext <= P.p.ext_cap) {
+            if (want && c.size + cu.size <= C && c.ext + cu.ext <= hard) {
                 c.size += cu.size;
                 c.ext += cu.ext;
                 absorb.push_back(cl[u]);
@@ -152,11 +158,11 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
                 ehj = std::max(ehj, eh[u] + B);
             }
         }
-        if (c.ext > P.p.ext_cap) {
-            // a single reach with more external inputs than the budget: cannot be scheduled
+        if (c.ext > hard) {
+            // more external inputs than the LDS can stage: cannot be scheduled
             std::ostringstream m;
-            m << "reach " << j << " has " << c.ext << " external inputs (ext_cap "
-              << P.p.ext_cap << ")";
+            m << "reach " << j << " needs " << c.ext << " external inputs (LDS cap " << hard
+              << " for slots=" << C << ", tile=" << B << ")";
             return m.str();
         }
         eh[j] = ehj;
@@ -217,20 +223,24 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     }
     for (int64_t j = 0; j < n; ++j) P.gmax = std::max(P.gmax, G[j]);
 
-    // ---- 6. pack clusters into workgroups (first fit, largest first) ---------------------
-    std::vector<int64_t> by_size(live);
-    std::stable_sort(by_size.begin(), by_size.end(), [&](int64_t a, int64_t b) {
-        return clusters[a].size > clusters[b].size;
+    // ---- 6. pack clusters into workgroups --------------------------------------------------
+    // First fit in order of schedule offset, so a workgroup holds clusters that are active at
+    // the same ticks; its G span is capped so the step-table window fits the LDS.
+    std::vector<int64_t> by_off(live);
+    std::stable_sort(by_off.begin(), by_off.end(), [&](int64_t a, int64_t b) {
+        return clusters[a].off < clusters[b].off;
     });
-    std::vector<int64_t> wg_fill, wg_ext;
-    // bounded first-fit: try the last few open bins only (keeps packing O(n))
-    const int kProbe = 64;
-    for (int64_t id : by_size) {
+    const int64_t scap = span_cap(C);
+    std::vector<int64_t> wg_fill, wg_ext, bin_lo, bin_hi;
+    const int kProbe = 64;  // bounded first fit over the most recent bins keeps packing O(n)
+    for (int64_t id : by_off) {
         Cluster& c = clusters[id];
+        const int64_t lo = c.off, hi = (int64_t)c.off + c.dmax;
         int64_t w = -1;
         const int64_t nb = (int64_t)wg_fill.size();
         for (int64_t b = std::max<int64_t>(0, nb - kProbe); b < nb; ++b)
-            if (wg_fill[b] + c.size <= C && wg_ext[b] + c.ext <= P.p.ext_cap) {
+            if (wg_fill[b] + c.size <= C && wg_ext[b] + c.ext <= std::max<int64_t>(soft, c.ext) &&
+                std::max(bin_hi[b], hi) - std::min(bin_lo[b], lo) <= scap) {
                 w = b;
                 break;
             }
@@ -238,9 +248,13 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             w = nb;
             wg_fill.push_back(0);
             wg_ext.push_back(0);
+            bin_lo.push_back(lo);
+            bin_hi.push_back(hi);
         }
         wg_fill[w] += c.size;
         wg_ext[w] += c.ext;
+        bin_lo[w] = std::min(bin_lo[w], lo);
+        bin_hi[w] = std::max(bin_hi[w], hi);
         c.wg = w;
     }
     P.nwg = (int32_t)wg_fill.size();
@@ -271,6 +285,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         }
         P.wg_gmin[w] = v.empty() ? 0 : G[v.front()];
         P.wg_gmax[w] = v.empty() ? 0 : G[v.back()];
+        P.max_span = std::max(P.max_span, P.wg_gmax[w] - P.wg_gmin[w]);
+        if ((int64_t)P.wg_gmax[w] - P.wg_gmin[w] > scap) return "internal: workgroup G span";
     }
     // upstream codes and external lists
     P.ext_off.assign(P.nwg + 1, 0);
@@ -290,7 +306,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             } else {
                 if (G[j] < G[u] + B) return "internal: cross-cluster edge without tile slack";
                 const size_t e = ext[w].size();
-                if (e >= (size_t)P.p.ext_cap) return "internal: ext_cap exceeded";
+                if (e >= (size_t)hard) return "internal: external-input cap exceeded";
                 ext[w].push_back({u, G[j]});
                 codes.push_back((uint16_t)(kExtBit | e));
                 P.n_cross++;

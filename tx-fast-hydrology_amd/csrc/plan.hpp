@@ -27,8 +27,14 @@ namespace mcr {
 struct PlanParams {
     int32_t slots = 256;       // reaches (threads) per workgroup
     int32_t tile = 32;         // ticks per launch; also the slack of a cross-cluster edge
-    int32_t ext_cap = 128;     // max cross-cluster inputs per workgroup (LDS budget)
+    int32_t ext_cap = 64;      // preferred max cross-cluster inputs per workgroup (soft)
 };
+
+// LDS of one workgroup (bytes): outflow double buffer, step-table window, external inputs.
+constexpr int64_t kLdsBudget = 160 * 1024;
+inline int64_t span_cap(int64_t slots) { return slots < 256 ? 255 : slots - 1; }
+inline int64_t table_entries(int64_t slots, int64_t tile) { return tile + span_cap(slots); }
+constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 frac}
 
 // upstream code: bit 15 set -> index into the workgroup's external-input list, else the
 // workgroup-local slot of the upstream reach.
@@ -52,6 +58,8 @@ struct Plan {
     int64_t n_cross = 0;           // cross-cluster edges
     int32_t max_height = 0;        // longest upstream path (levels - 1)
     int32_t max_ext_wg = 0;
+    int32_t ext_hard = 0;          // LDS-derived hard cap of cross-cluster inputs per workgroup
+    int32_t max_span = 0;          // max G span inside one workgroup
 
     // replay of the reference walk (original reach order)
     std::vector<int64_t> rank;     // -1 if never processed
