@@ -147,7 +147,7 @@ struct Net {
     DBuf<uint64_t> up4;
     DBuf<uint16_t> up_more;
     DBuf<int64_t> slot_reach, ext_src, pos;
-    DBuf<uint8_t> rpad;            // [n] output row pad (G & 15) of each caller reach
+    DBuf<uint8_t> rpad;            // [n] output row pad (G & (kChunk - 1)) of each caller reach
     int32_t more_cap = 0;          // max overflow upstream codes of one workgroup
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;

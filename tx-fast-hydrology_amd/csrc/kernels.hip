@@ -7,8 +7,8 @@
 // from an LDS double buffer written in the previous tick.  Inputs from other clusters were
 // produced in an earlier launch and are staged in LDS in the launch prologue, together with the
 // window of the per-step interpolation table this workgroup needs.  The tick loop issues no
-// global loads except the per-chunk forcing-row prefetch; outputs leave in whole 128-byte lines
-// (16 ticks per chunk, rows padded so every chunk is line aligned).
+// global loads except the per-chunk forcing-row prefetch; outputs leave in whole aligned 64-byte
+// segments (8 ticks per chunk, rows padded so every chunk is aligned).
 //
 // Arithmetic follows the reference exactly (FMA contraction is off for this file):
 //   I = ((0 + o[u1]) + o[u2]) + ...          upstream reaches in reference finalisation order
@@ -23,7 +23,7 @@ namespace mcr {
 
 namespace {
 
-// Store of one 16-tick chunk (128 B): 8 x 16-byte accesses, address 16-B aligned.
+// Store of one chunk (kChunk doubles) as 16-byte accesses; the address is 16-B aligned.
 __device__ __forceinline__ void store_chunk(double* p, const double (&v)[kChunk]) {
     double2* q = reinterpret_cast<double2*>(p);
 #pragma unroll
@@ -51,14 +51,31 @@ __device__ __forceinline__ void chunk_rows(const int4* tab, int tw0, int kc, int
 
 __device__ __forceinline__ int clamp_row(int r, int n_rows) { return r < n_rows ? r : n_rows - 1; }
 
+constexpr int kHalf = kChunk;  // ticks whose lateral inflow is formed in one burst
+
+__device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
+    return *reinterpret_cast<const double*>(lds + byte);
+}
+
+// LDS layout of one workgroup (bytes):
+//   XB  [SLOTS + 1][2] f64  outflow of each slot at tick parity 0/1; slot SLOTS stays 0.0
+//   FR  [SLOTS][3]     f64  the lane's forcing rows rb .. rb + 2 of the current chunk
+//   TAB [table_cap]    int4 step-table window {row_lo, row_hi, frac}
+//   XE  [ext_cap][tile] f64 external inputs of this launch
+//   XM  [more_cap]     u32  overflow upstream codes (5th and later upstream reaches)
 template <int SLOTS>
 __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
+    extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tile = a.tile;
-    double* xb = smem;                                            // [2][SLOTS] outflows
-    int4* tab = reinterpret_cast<int4*>(smem + 2 * SLOTS);        // [table_cap] step table
-    double* xe = reinterpret_cast<double*>(tab + a.table_cap);    // [ext_cap][tile] ext inputs
-    unsigned* xm = reinterpret_cast<unsigned*>(xe + (size_t)a.ext_cap * tile);  // overflow codes
+    constexpr unsigned XB = 0;
+    constexpr unsigned FR = XB + (SLOTS + 1) * 16;
+    constexpr unsigned TAB = FR + SLOTS * 24;
+    const unsigned XE = TAB + (unsigned)a.table_cap * 16;
+    const unsigned XM = XE + (unsigned)a.ext_cap * (unsigned)tile * 8;
+    double* xbp = reinterpret_cast<double*>(lds + XB);
+    int4* tab = reinterpret_cast<int4*>(lds + TAB);
+    double* xe = reinterpret_cast<double*>(lds + XE);
+    unsigned* xm = reinterpret_cast<unsigned*>(lds + XM);
 
     const int tid = threadIdx.x;
     const int w = a.active[blockIdx.x];
@@ -71,19 +88,21 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
 
     // ---- per-reach registers and state at step t_first - 1 (issued first: longest latency)
     const uint8_t fl = a.flags[d];
-    const int G = a.G[d];
-    const int gq = G & ~(kChunk - 1);                   // padded position p = tick - gq
+    const int Gr = a.G[d];
+    const int gq = Gr & ~(kChunk - 1);                  // padded position p = tick - gq
     const int64_t row = a.slot_reach[d];
     const bool real = fl != kSlotPad;
-    const int t_first = k0 - G;                         // step at this launch's first tick
+    const bool routed = fl == kSlotRouted;
+    const int t_first = k0 - Gr;                        // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
+    const int G = live ? Gr : (1 << 29);                // never active when not live
     const bool from_out = real && t_first >= 1 && t_first <= T;
     const int64_t obase = real ? row * Tp : 0;
     const double o_ld = a.O[from_out ? obase + (k0 - gq) - 1 : 0];
     const double i_ld = a.I[from_out ? obase + (k0 - gq) - 1 : 0];
     const double st_o = a.st_o[d], st_i = a.st_i[d];
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
-    const int cnt = a.up_cnt[d];
+    const int cnt = live ? a.up_cnt[d] : 0;
     const uint64_t up4 = a.up4[d];
     const int m0 = a.up_more_off[(int64_t)w * SLOTS];
     const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
@@ -128,15 +147,30 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     double op = from_out ? o_ld : st_o;
     double ip = from_out ? i_ld : st_i;
     // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
-    xb[((k0 - 1) & 1) * SLOTS + tid] = op;
+    xbp[tid * 2 + ((k0 - 1) & 1)] = op;
+    if (tid < 2) xbp[SLOTS * 2 + tid] = 0.0;            // zero slot for unused upstream codes
     // drain every prologue load: otherwise the wait-count pass carries "pending" state into
     // the tick loop and waits for each chunk's stores at every tick
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 
-    // forcing rows of the first chunk (rows rb .. rb + 2 kept in registers)
+    // upstream codes -> LDS byte bases; unused codes read the zero slot (adding +0.0 to a sum
+    // that started as 0.0 + v is exact, so the sum needs no predicate)
+    unsigned ubase[kUpInline], uinc[kUpInline];
+#pragma unroll
+    for (int u = 0; u < kUpInline; ++u) {
+        const unsigned code = u < cnt ? (unsigned)((up4 >> (16 * u)) & 0xffffu) : (unsigned)SLOTS;
+        const bool ext = (code & kExtBit) != 0;
+        ubase[u] = ext ? XE + (code & 0x7fffu) * (unsigned)tile * 8 : XB + code * 16;
+        uinc[u] = ext ? 16u : 0u;
+    }
+    const bool any3 = __any(cnt > 2);                   // wave-uniform
+    const bool any5 = __any(cnt > kUpInline);
+    const unsigned own = XB + (unsigned)tid * 16;
+
+    // forcing rows of the first chunk
     int rb, nr;
-    chunk_rows(tab, tw0, k0, G, live ? T : 0, rb, nr);
+    chunk_rows(tab, tw0, k0, G, T, rb, nr);
     double f0 = a.F[(int64_t)clamp_row(rb, nrow) * ns + d];
     double f1 = a.F[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
     double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
@@ -145,69 +179,83 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         const int pc = kc - gq;                         // multiple of kChunk
+        // this chunk's forcing rows -> the lane's LDS slots (private: no barrier needed)
+        double* frl = reinterpret_cast<double*>(lds + FR) + tid * 3;
+        frl[0] = f0;
+        frl[1] = f1;
+        frl[2] = f2;
+        const bool slow = __any(nr > 3);                // more rows than slots: load direct
+        const unsigned frp = FR + (unsigned)tid * 24 - (unsigned)rb * 8;
         // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
         int rbn, nrn;
-        chunk_rows(tab, tw0, kc + kChunk, G, (live && c + kChunk < tile) ? T : 0, rbn, nrn);
+        chunk_rows(tab, tw0, kc + kChunk, G, c + kChunk < tile ? T : 0, rbn, nrn);
         const double g0 = a.F[(int64_t)clamp_row(rbn, nrow) * ns + d];
         const double g1 = a.F[(int64_t)clamp_row(rbn + 1, nrow) * ns + d];
         const double g2 = a.F[(int64_t)clamp_row(rbn + 2, nrow) * ns + d];
-        const bool slow = nr > 3;                       // more rows than registers: load direct
+        // per-chunk LDS cursors: upstream value of tick i at m[u] + 8 * ((i + 1) & 1)
+        unsigned m[kUpInline];
+#pragma unroll
+        for (int u = 0; u < kUpInline; ++u) m[u] = uinc[u] ? ubase[u] + 8u * c - 8u : ubase[u];
+        const unsigned tp = TAB + (unsigned)(kc - G - tw0) * 16u;
         double ob[kChunk], ib[kChunk];
 #pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-            const int k = kc + i;
-            const int t = k - G;
-            const bool act = live && t >= 0 && t < T;
-            double I = 0.0, o = 0.0;
-            if (act) {
-                const int4 e = tab[t - tw0];
-                // inflow: upstream outflows in reference finalisation order
-                const double* prev = xb + ((k - 1) & 1) * SLOTS;
-                const int col = c + i;
-                double v[kUpInline];
+        for (int h = 0; h < kChunk; h += kHalf) {
+            // lateral inflow of the next kHalf ticks, interpolate_sample (nutils.py:23-33); it
+            // does not depend on the routing state, so it is formed off the tick's critical path
+            double qv[kHalf];
 #pragma unroll
-                for (int u = 0; u < kUpInline; ++u) {
-                    const unsigned code = (unsigned)((up4 >> (16 * u)) & 0xffffu);
-                    const double* src = (code & kExtBit) ? xe + (code & 0x7fffu) * tile + col
-                                                         : prev + (code & (SLOTS - 1));
-                    v[u] = *src;
-                }
-#pragma unroll
-                for (int u = 0; u < kUpInline; ++u)
-                    if (u < cnt) I = I + v[u];
-                for (int u = kUpInline; u < cnt; ++u) {
-                    const unsigned code = xm[more + u - kUpInline];
-                    const double* src = (code & kExtBit) ? xe + (code & 0x7fffu) * tile + col
-                                                         : prev + (code & (SLOTS - 1));
-                    I = I + *src;
-                }
-                // lateral inflow, interpolate_sample (nutils.py:23-33)
+            for (int j = 0; j < kHalf; ++j) {
+                const int4 e = *reinterpret_cast<const int4*>(lds + tp + 16u * (h + j));
                 double flo, fhi;
                 if (slow) {
-                    flo = a.F[(int64_t)e.x * ns + d];
-                    fhi = a.F[(int64_t)(e.y < 0 ? e.x : e.y) * ns + d];
-                    // settle these loads here so the common path inherits no pending state
-                    __builtin_amdgcn_s_waitcnt(0);
+                    flo = a.F[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + d];
+                    fhi = a.F[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + d];
                 } else {
-                    const int kl = e.x - rb, kh = e.y - rb;
-                    flo = kl == 0 ? f0 : (kl == 1 ? f1 : f2);
-                    fhi = kh == 0 ? f0 : (kh == 1 ? f1 : f2);
+                    flo = lds_f64(lds, frp + 8u * (unsigned)e.x);
+                    fhi = lds_f64(lds, frp + 8u * (unsigned)e.y);
                 }
-                double q;
-                if (e.y < 0) {
-                    q = flo;
-                } else {
-                    const double fr = __hiloint2double(e.w, e.z);
-                    q = (1.0 - fr) * flo + fr * fhi;
-                }
-                if (fl == kSlotRouted) o = 0.0 + (((al * I + be * ip) + ch * op) + ga * q);
-                xb[(k & 1) * SLOTS + tid] = o;
-                op = o;
-                ip = I;
+                const double fr = __hiloint2double(e.w, e.z);
+                const double qi = (1.0 - fr) * flo + fr * fhi;
+                qv[j] = e.y < 0 ? flo : qi;
             }
-            ob[i] = o;
-            ib[i] = I;
-            __syncthreads();
+            if (slow) __builtin_amdgcn_s_waitcnt(0);    // settle the direct loads here
+#pragma unroll
+            for (int j = 0; j < kHalf; ++j) {
+                const int i = h + j;
+                if (i & 1) {
+#pragma unroll
+                    for (int u = 0; u < kUpInline; ++u) m[u] += uinc[u];
+                }
+                const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
+                const int t = kc + i - G;
+                const bool act = (unsigned)t < (unsigned)T;
+                // inflow: upstream outflows in reference finalisation order
+                double I = 0.0 + lds_f64(lds, m[0] + rd);
+                I = I + lds_f64(lds, m[1] + rd);
+                if (any3) {
+                    I = I + lds_f64(lds, m[2] + rd);
+                    I = I + lds_f64(lds, m[3] + rd);
+                }
+                if (any5) {
+                    for (int u = kUpInline; u < cnt; ++u) {
+                        const unsigned code = xm[more + u - kUpInline];
+                        const unsigned at = (code & kExtBit)
+                                                ? XE + ((code & 0x7fffu) * tile + c + i) * 8u
+                                                : XB + code * 16 + rd;
+                        I = I + lds_f64(lds, at);
+                    }
+                }
+                const double ov = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[j]);
+                const double o = routed ? ov : 0.0;
+                // inactive ticks write garbage that no active reach reads (its consumer is
+                // inactive one tick later) and into padding positions of the output row
+                *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = o;
+                op = act ? o : op;
+                ip = act ? I : ip;
+                ob[i] = o;
+                ib[i] = I;
+                __syncthreads();
+            }
         }
         // whole aligned line per row and array; out-of-row chunks go to the dummy line
         const bool in_row = real && pc >= 0 && pc < Tp;

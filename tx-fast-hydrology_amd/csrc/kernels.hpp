@@ -9,8 +9,8 @@
 namespace mcr {
 
 // Ticks per register chunk.  Series rows are padded so that a chunk always covers one aligned
-// 128-byte line: step t of reach j lives at  row(j) * Tp + t + (G[j] & (kChunk - 1)).
-constexpr int kChunk = 16;
+// 64-byte segment: step t of reach j lives at  row(j) * Tp + t + (G[j] & (kChunk - 1)).
+constexpr int kChunk = 8;
 
 inline int64_t padded_steps(int64_t T) {  // Tp: room for the pad and a full trailing chunk
     return ((T + 2 * kChunk - 1) / kChunk) * kChunk;
@@ -57,8 +57,8 @@ struct WaveArgs {
 
 inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile,
                                   int more_cap) {
-    return 16 * (size_t)slots + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile +
-           4 * (size_t)more_cap;
+    return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)table_cap +
+           8 * (size_t)ext_cap * tile + 4 * (size_t)more_cap;
 }
 
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
