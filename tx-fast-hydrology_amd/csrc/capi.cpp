@@ -292,6 +292,13 @@ struct Net {
         }
         O.reserve((size_t)n * Tp);
         I.reserve((size_t)n * Tp);
+        // dense forcing: some window of kChunk consecutive steps spans more than 3 rows
+        bool dense = false;
+        for (int64_t t = 0; t < T && !dense; ++t) {
+            const int64_t t2 = std::min<int64_t>(t + mcr::kChunk - 1, T - 1);
+            const int last = std::max(tabh[t2].x, tabh[t2].y);
+            dense = last - tabh[t].x + 1 > 3;
+        }
         stab.upload(tabh.data(), tabh.size(), stream);
         HIPC(hipStreamSynchronize(stream));  // the host table is freed when the caller returns
         ensure_schedule(T);
@@ -341,7 +348,7 @@ struct Net {
             a.active = active.p + sched_off[k];
             a.kappa0 = (int32_t)(k * plan.p.tile);
             if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, stream));
+            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, dense, stream));
             if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
             ++launched;
         }

@@ -63,7 +63,10 @@ __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
 //   TAB [table_cap]    int4 step-table window {row_lo, row_hi, frac}
 //   XE  [ext_cap][tile] f64 external inputs of this launch
 //   XM  [more_cap]     u32  overflow upstream codes (5th and later upstream reaches)
-template <int SLOTS>
+// DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
+// those lanes read the forcing straight from global memory.  A separate instantiation keeps the
+// direct loads (and the waits they need) out of the common kernel.
+template <int SLOTS, bool DENSE>
 __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tile = a.tile;
@@ -184,7 +187,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         frl[0] = f0;
         frl[1] = f1;
         frl[2] = f2;
-        const bool slow = __any(nr > 3);                // more rows than slots: load direct
+        const bool slow = DENSE && __any(nr > 3);       // more rows than slots: load direct
         const unsigned frp = FR + (unsigned)tid * 24 - (unsigned)rb * 8;
         // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
         int rbn, nrn;
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
             for (int j = 0; j < kHalf; ++j) {
                 const int4 e = *reinterpret_cast<const int4*>(lds + tp + 16u * (h + j));
                 double flo, fhi;
-                if (slow) {
+                if (DENSE && slow) {
                     flo = a.F[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + d];
                     fhi = a.F[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + d];
                 } else {
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                 const double qi = (1.0 - fr) * flo + fr * fhi;
                 qv[j] = e.y < 0 ? flo : qi;
             }
-            if (slow) __builtin_amdgcn_s_waitcnt(0);    // settle the direct loads here
+            if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
 #pragma unroll
             for (int j = 0; j < kHalf; ++j) {
                 const int i = h + j;
@@ -356,16 +359,23 @@ inline int grid_for(int64_t work, int block) {
 
 }  // namespace
 
-hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds, hipStream_t s) {
+template <bool DENSE>
+hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, size_t lds, hipStream_t s) {
     switch (slots) {
-        case 64: hipLaunchKernelGGL(wavefront_det<64>, grid, 64, lds, s, a); break;
-        case 128: hipLaunchKernelGGL(wavefront_det<128>, grid, 128, lds, s, a); break;
-        case 256: hipLaunchKernelGGL(wavefront_det<256>, grid, 256, lds, s, a); break;
-        case 512: hipLaunchKernelGGL(wavefront_det<512>, grid, 512, lds, s, a); break;
-        case 1024: hipLaunchKernelGGL(wavefront_det<1024>, grid, 1024, lds, s, a); break;
+        case 64: hipLaunchKernelGGL((wavefront_det<64, DENSE>), grid, 64, lds, s, a); break;
+        case 128: hipLaunchKernelGGL((wavefront_det<128, DENSE>), grid, 128, lds, s, a); break;
+        case 256: hipLaunchKernelGGL((wavefront_det<256, DENSE>), grid, 256, lds, s, a); break;
+        case 512: hipLaunchKernelGGL((wavefront_det<512, DENSE>), grid, 512, lds, s, a); break;
+        case 1024: hipLaunchKernelGGL((wavefront_det<1024, DENSE>), grid, 1024, lds, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds, bool dense,
+                            hipStream_t s) {
+    return dense ? launch_wavefront_t<true>(a, grid, slots, lds, s)
+                 : launch_wavefront_t<false>(a, grid, slots, lds, s);
 }
 
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,

@@ -61,7 +61,8 @@ inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int til
            8 * (size_t)ext_cap * tile + 4 * (size_t)more_cap;
 }
 
-hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
+// dense: the step table has an 8-step window spanning more than 3 forcing rows
+hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
                             hipStream_t s);
 
 // st[d] = src[slot_reach[d]] for real slots (caller order -> slot order)
