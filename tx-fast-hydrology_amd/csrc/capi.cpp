@@ -147,7 +147,6 @@ struct Net {
     DBuf<uint64_t> up4;
     DBuf<uint16_t> up_more;
     DBuf<int64_t> slot_reach, ext_src, pos;
-    DBuf<uint8_t> rpad;            // [n] output row pad (G & (kChunk - 1)) of each caller reach
     int32_t more_cap = 0;          // max overflow upstream codes of one workgroup
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
@@ -157,10 +156,12 @@ struct Net {
     std::vector<double> xp;
     // per-step interpolation table {row_lo, row_hi, frac}
     DBuf<int4> stab;
-    // outputs [n][Tp] (caller order, padded rows), a step-major scratch for fetches and the
-    // dummy line of out-of-row chunks
+    // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
+    // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
+    // and the dummy row of out-of-window ticks
     DBuf<double> O, I, outT, dummy;
-    int64_t T_out = 0, Tp_out = 0;
+    DBuf<int64_t> wbase, jbase, ext_at;
+    int64_t T_out = 0;
     bool coeffs_set = false;
 
     // active-workgroup schedule cache
@@ -197,17 +198,7 @@ struct Net {
         slot_reach.upload(plan.slot_reach.data(), ns, stream);
         ext_off.upload(plan.ext_off.data(), plan.ext_off.size(), stream);
         {
-            // external input source: caller row * 16 + row pad (one load in the prologue)
-            std::vector<int64_t> code(plan.ext_src.size());
-            for (size_t e = 0; e < code.size(); ++e) {
-                const int64_t j = plan.ext_src[e];
-                code[e] = j * 16 + (plan.G[plan.pos[j]] & (mcr::kChunk - 1));
-            }
-            ext_src.upload(code.data(), code.size(), stream);
-            std::vector<uint8_t> pad(plan.n);
-            for (int64_t j = 0; j < plan.n; ++j)
-                pad[j] = (uint8_t)(plan.G[plan.pos[j]] & (mcr::kChunk - 1));
-            rpad.upload(pad.data(), pad.size(), stream);
+            ext_src.upload(plan.ext_src.data(), plan.ext_src.size(), stream);
             for (int32_t w = 0; w < plan.nwg; ++w) {
                 const int64_t a0 = plan.up_more_off[(int64_t)w * plan.p.slots];
                 const int64_t a1 = plan.up_more_off[(int64_t)(w + 1) * plan.p.slots];
@@ -224,7 +215,7 @@ struct Net {
             HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
         }
         stage.reserve(std::max<int64_t>(plan.n, 1));
-        dummy.reserve(4 * mcr::kChunk);
+        dummy.reserve(2 * 1024);
         HIPC(hipStreamSynchronize(stream));
     }
 
@@ -261,11 +252,26 @@ struct Net {
         HIPC(hipStreamSynchronize(stream));
     }
 
+    // Per-horizon layout: active workgroups of every launch and the output windows.
     void ensure_schedule(int64_t T) {
         if (sched_T == T) return;
         std::vector<int32_t> list;
         mcr::active_schedule(plan, T, list, sched_off);
         active.upload(list.data(), list.size(), stream);
+        std::vector<int64_t> wb(plan.nwg);
+        int64_t total = 0;
+        for (int32_t w = 0; w < plan.nwg; ++w) {
+            wb[w] = total;
+            total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * plan.p.slots;
+        }
+        wbase.upload(wb.data(), wb.size(), stream);
+        O.reserve((size_t)total);
+        I.reserve((size_t)total);
+        jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
+        ext_at.reserve(std::max<size_t>(plan.ext_src.size(), 1));
+        HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, wbase.p, plan.p.slots, plan.n,
+                                      jbase.p, ext_src.p, (int64_t)plan.ext_src.size(), ext_at.p,
+                                      stream));
         HIPC(hipStreamSynchronize(stream));
         sched_T = T;
     }
@@ -283,15 +289,11 @@ struct Net {
         REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
         REQUIRE(T >= 1 && T < (1ll << 30), "T out of range");
         const int64_t n = plan.n;
-        const int64_t Tp = mcr::padded_steps(T);
         T_out = 0;
         if (n == 0) {
             T_out = T;
-            Tp_out = Tp;
             return;
         }
-        O.reserve((size_t)n * Tp);
-        I.reserve((size_t)n * Tp);
         // dense forcing: some window of kChunk consecutive steps spans more than 3 rows
         bool dense = false;
         for (int64_t t = 0; t < T && !dense; ++t) {
@@ -313,11 +315,9 @@ struct Net {
         a.up4 = up4.p;
         a.up_more_off = up_more_off.p;
         a.up_more = up_more.p;
-        a.slot_reach = slot_reach.p;
         a.ext_off = ext_off.p;
-        a.ext_src = ext_src.p;
+        a.ext_at = ext_at.p;
         a.ext_g = ext_g.p;
-        a.rpad = rpad.p;
         a.alpha = alpha.p;
         a.beta = beta.p;
         a.chi = chi.p;
@@ -328,13 +328,13 @@ struct Net {
         a.stab = stab.p;
         a.wg_gmin = wg_gmin.p;
         a.wg_gmax = wg_gmax.p;
+        a.wbase = wbase.p;
         a.O = O.p;
         a.I = I.p;
         a.dummy = dummy.p;
         a.nslots = plan.nslots;
         a.n_rows = (int32_t)rows;
         a.T = (int32_t)T;
-        a.Tp = (int32_t)Tp;
         a.tile = plan.p.tile;
         a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
         a.ext_cap = plan.max_ext_wg;
@@ -352,8 +352,8 @@ struct Net {
             if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
             ++launched;
         }
-        HIPC(mcr::launch_final_state(O.p, I.p, st_o.p, st_i.p, slot_reach.p, G.p, plan.nslots,
-                                     Tp, T, stream));
+        HIPC(mcr::launch_final_state(O.p, I.p, st_o.p, st_i.p, jbase.p, slot_reach.p,
+                                     plan.nslots, plan.p.slots, T, stream));
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
             HIPC(hipEventSynchronize(events[2 * nl + 1]));
@@ -368,7 +368,6 @@ struct Net {
             launches += launched;
         }
         T_out = T;
-        Tp_out = Tp;
     }
 
     void load_forcing(int64_t rows, const double* xps, const double* fp) {
@@ -432,13 +431,13 @@ struct Net {
         if (n == 0 || k == 0) return;
         outT.reserve((size_t)n * k);
         if (oo) {
-            HIPC(mcr::launch_transpose(O.p, rpad.p, outT.p, n, Tp_out, t0, t1, stream));
+            HIPC(mcr::launch_gather_steps(O.p, jbase.p, plan.p.slots, outT.p, n, t0, t1, stream));
             HIPC(hipMemcpyAsync(oo, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             HIPC(hipStreamSynchronize(stream));
         }
         if (io) {
-            HIPC(mcr::launch_transpose(I.p, rpad.p, outT.p, n, Tp_out, t0, t1, stream));
+            HIPC(mcr::launch_gather_steps(I.p, jbase.p, plan.p.slots, outT.p, n, t0, t1, stream));
             HIPC(hipMemcpyAsync(io, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             HIPC(hipStreamSynchronize(stream));
@@ -454,8 +453,8 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_compact(k == 0 ? O.p : I.p, rpad.p, outT.p, n, Tp_out, T_out,
-                                     stream));
+            HIPC(mcr::launch_gather_series(k == 0 ? O.p : I.p, jbase.p, plan.p.slots, outT.p, n,
+                                           T_out, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             HIPC(hipStreamSynchronize(stream));
         }

@@ -7,8 +7,8 @@
 // from an LDS double buffer written in the previous tick.  Inputs from other clusters were
 // produced in an earlier launch and are staged in LDS in the launch prologue, together with the
 // window of the per-step interpolation table this workgroup needs.  The tick loop issues no
-// global loads except the per-chunk forcing-row prefetch; outputs leave in whole aligned 64-byte
-// segments (8 ticks per chunk, rows padded so every chunk is aligned).
+// global loads except the per-chunk forcing-row prefetch; each tick's outputs leave as one
+// contiguous row per wave (workgroup windows, kernels.hpp).
 //
 // Arithmetic follows the reference exactly (FMA contraction is off for this file):
 //   I = ((0 + o[u1]) + o[u2]) + ...          upstream reaches in reference finalisation order
@@ -22,13 +22,6 @@
 namespace mcr {
 
 namespace {
-
-// Store of one chunk (kChunk doubles) as 16-byte accesses; the address is 16-B aligned.
-__device__ __forceinline__ void store_chunk(double* p, const double (&v)[kChunk]) {
-    double2* q = reinterpret_cast<double2*>(p);
-#pragma unroll
-    for (int k = 0; k < kChunk / 2; ++k) q[k] = make_double2(v[2 * k], v[2 * k + 1]);
-}
 
 // Forcing rows a lane needs for the chunk starting at tick kc: [rb, rb + nr).  Rows are
 // non-decreasing in t (step times are increasing), so the first step's row_lo and the last
@@ -84,7 +77,6 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int w = a.active[blockIdx.x];
     const int64_t d = (int64_t)w * SLOTS + tid;
     const int T = a.T;
-    const int64_t Tp = a.Tp;
     const int k0 = a.kappa0;
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
@@ -92,17 +84,18 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     // ---- per-reach registers and state at step t_first - 1 (issued first: longest latency)
     const uint8_t fl = a.flags[d];
     const int Gr = a.G[d];
-    const int gq = Gr & ~(kChunk - 1);                  // padded position p = tick - gq
-    const int64_t row = a.slot_reach[d];
     const bool real = fl != kSlotPad;
     const bool routed = fl == kSlotRouted;
     const int t_first = k0 - Gr;                        // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
     const int G = live ? Gr : (1 << 29);                // never active when not live
     const bool from_out = real && t_first >= 1 && t_first <= T;
-    const int64_t obase = real ? row * Tp : 0;
-    const double o_ld = a.O[from_out ? obase + (k0 - gq) - 1 : 0];
-    const double i_ld = a.I[from_out ? obase + (k0 - gq) - 1 : 0];
+    const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
+    const int64_t wb = a.wbase[w];
+    // previous step = this lane's output at tick k0 - 1 (inside its window when from_out)
+    const int64_t at_prev = from_out ? wb + (int64_t)(k0 - 1 - gminw) * SLOTS + tid : 0;
+    const double o_ld = a.O[at_prev];
+    const double i_ld = a.I[at_prev];
     const double st_o = a.st_o[d], st_i = a.st_i[d];
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
     const int cnt = live ? a.up_cnt[d] : 0;
@@ -112,8 +105,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int more = a.up_more_off[d] - m0;
 
     // ---- step-table window of this workgroup -> LDS
-    const int gmin = a.wg_gmin[w], gmax = a.wg_gmax[w];
-    int tw0 = k0 - gmax, tw1 = k0 + tile - gmin;
+    int tw0 = k0 - gmaxw, tw1 = k0 + tile - gminw;
     tw0 = tw0 < 0 ? 0 : (tw0 > T ? T : tw0);
     tw1 = tw1 < 0 ? 0 : (tw1 > T ? T : tw1);
     for (int idx = tid; idx < tw1 - tw0; idx += SLOTS) tab[idx] = a.stab[tw0 + idx];
@@ -123,21 +115,21 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int ntot = (a.ext_off[w + 1] - e0) * tile;
     for (int base = tid; base < ntot; base += 8 * SLOTS) {
         int ti[8], eg[8];
-        int64_t code[8];
+        int64_t at0[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {   // unconditional (clamped) loads: one wait per batch
             const int idx = min(base + k * SLOTS, ntot - 1);
             const int e = idx / tile;
             ti[k] = k0 + (idx - e * tile);
             eg[k] = a.ext_g[e0 + e];
-            code[k] = a.ext_src[e0 + e];                  // caller row * 16 + pad
+            at0[k] = a.ext_at[e0 + e];                    // source's step 0 in its window
         }
         double v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int t = ti[k] - eg[k];
             const bool ok = t >= 0 && t < T;
-            v[k] = a.O[ok ? (code[k] >> 4) * Tp + (code[k] & 15) + t : 0];
+            v[k] = a.O[ok ? at0[k] + (int64_t)t * SLOTS : 0];
             v[k] = ok ? v[k] : 0.0;
         }
 #pragma unroll
@@ -179,9 +171,9 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
     __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
 
+    const int wend = gmaxw + T;                         // end of this workgroup's window
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
-        const int pc = kc - gq;                         // multiple of kChunk
         // this chunk's forcing rows -> the lane's LDS slots (private: no barrier needed)
         double* frl = reinterpret_cast<double*>(lds + FR) + tid * 3;
         frl[0] = f0;
@@ -200,7 +192,6 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
 #pragma unroll
         for (int u = 0; u < kUpInline; ++u) m[u] = uinc[u] ? ubase[u] + 8u * c - 8u : ubase[u];
         const unsigned tp = TAB + (unsigned)(kc - G - tw0) * 16u;
-        double ob[kChunk], ib[kChunk];
 #pragma unroll
         for (int h = 0; h < kChunk; h += kHalf) {
             // lateral inflow of the next kHalf ticks, interpolate_sample (nutils.py:23-33); it
@@ -249,21 +240,22 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                     }
                 }
                 const double ov = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[j]);
-                const double o = routed ? ov : 0.0;
                 // inactive ticks write garbage that no active reach reads (its consumer is
-                // inactive one tick later) and into padding positions of the output row
-                *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = o;
-                op = act ? o : op;
+                // inactive one tick later); never-processed reaches (no consumer) output 0
+                *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = ov;
+                op = act ? ov : op;
                 ip = act ? I : ip;
-                ob[i] = o;
-                ib[i] = I;
+                // one contiguous row per wave; ticks outside the window go to the dummy row
+                const int k = kc + i;
+                const bool inwin = k >= gminw && k < wend;
+                const int64_t row = inwin ? wb + (int64_t)(k - gminw) * SLOTS : 0;
+                double* orow = inwin ? a.O + row : a.dummy;
+                double* irow = inwin ? a.I + row : a.dummy + SLOTS;
+                orow[tid] = routed ? ov : 0.0;
+                irow[tid] = I;
                 __syncthreads();
             }
         }
-        // whole aligned line per row and array; out-of-row chunks go to the dummy line
-        const bool in_row = real && pc >= 0 && pc < Tp;
-        store_chunk(in_row ? a.O + obase + pc : a.dummy, ob);
-        store_chunk(in_row ? a.I + obase + pc : a.dummy + kChunk, ib);
         rb = rbn;
         nr = nrn;
         f0 = g0;
@@ -301,52 +293,62 @@ __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restri
     }
 }
 
+__global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __restrict__ G,
+                             const int32_t* __restrict__ wg_gmin,
+                             const int64_t* __restrict__ wbase, int slots, int64_t n,
+                             int64_t* __restrict__ jbase) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t d = pos[j];
+        const int64_t w = d / slots;
+        jbase[j] = wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * slots + (d - w * slots);
+    }
+}
+
+__global__ void ext_index(const int64_t* __restrict__ jbase, const int64_t* __restrict__ ext_src,
+                          int64_t n_ext, int64_t* __restrict__ ext_at) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n_ext;
+         e += (int64_t)gridDim.x * blockDim.x)
+        ext_at[e] = jbase[ext_src[e]];
+}
+
 __global__ void final_state(const double* __restrict__ O, const double* __restrict__ I,
                             double* __restrict__ st_o, double* __restrict__ st_i,
-                            const int64_t* __restrict__ slot_reach, const int32_t* __restrict__ G,
-                            int64_t nslots, int64_t Tp, int64_t T) {
+                            const int64_t* __restrict__ jbase,
+                            const int64_t* __restrict__ slot_reach, int64_t nslots, int slots,
+                            int64_t T) {
     for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < nslots;
          d += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = slot_reach[d];
         if (j >= 0) {
-            const int64_t at = j * Tp + (G[d] & (kChunk - 1)) + (T - 1);
+            const int64_t at = jbase[j] + (T - 1) * slots;
             st_o[d] = O[at];
             st_i[d] = I[at];
         }
     }
 }
 
-// 64 x 64 tile transpose through LDS: reads row segments of S, writes 512-B rows of out.
-__global__ __launch_bounds__(256) void transpose_rt(const double* __restrict__ S,
-                                                    const uint8_t* __restrict__ rpad,
-                                                    double* __restrict__ out, int64_t n,
-                                                    int64_t Tp, int64_t t0, int64_t t1) {
-    __shared__ double tileb[64][65];
-    const int64_t j0 = (int64_t)blockIdx.x * 64;
-    const int64_t tb = t0 + (int64_t)blockIdx.y * 64;
-    const int lx = threadIdx.x & 63;
-    const int ly = threadIdx.x >> 6;  // 0..3
-    for (int r = ly; r < 64; r += 4) {
-        const int64_t j = j0 + r;
-        const int64_t t = tb + lx;
-        tileb[r][lx] = (j < n && t < t1) ? S[j * Tp + rpad[j] + t] : 0.0;
-    }
-    __syncthreads();
-    for (int r = ly; r < 64; r += 4) {
-        const int64_t t = tb + r;
-        const int64_t j = j0 + lx;
-        if (t < t1 && j < n) out[(t - t0) * n + j] = tileb[lx][r];
+// out[t - t0][j]: consecutive threads take consecutive j (coalesced writes, gathered reads)
+__global__ void gather_steps(const double* __restrict__ S, const int64_t* __restrict__ jbase,
+                             int slots, double* __restrict__ out, int64_t n, int64_t t0,
+                             int64_t t1) {
+    const int64_t total = n * (t1 - t0);
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = x / n;
+        const int64_t j = x - t * n;
+        out[x] = S[jbase[j] + (t0 + t) * slots];
     }
 }
 
-__global__ void compact_rows(const double* __restrict__ S, const uint8_t* __restrict__ rpad,
-                             double* __restrict__ out, int64_t n, int64_t Tp, int64_t T) {
+__global__ void gather_series(const double* __restrict__ S, const int64_t* __restrict__ jbase,
+                              int slots, double* __restrict__ out, int64_t n, int64_t T) {
     const int64_t total = n * T;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = x / T;
         const int64_t t = x - j * T;
-        out[x] = S[j * Tp + rpad[j] + t];
+        out[x] = S[jbase[j] + t * slots];
     }
 }
 
@@ -398,26 +400,40 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
     return hipGetLastError();
 }
 
+hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
+                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
+                               const int64_t* ext_src, int64_t n_ext, int64_t* ext_at,
+                               hipStream_t s) {
+    if (n > 0)
+        hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
+                           slots, n, jbase);
+    if (n_ext > 0)
+        hipLaunchKernelGGL(ext_index, grid_for(n_ext, 256), 256, 0, s, jbase, ext_src, n_ext,
+                           ext_at);
+    return hipGetLastError();
+}
+
 hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,
-                              const int64_t* slot_reach, const int32_t* G, int64_t nslots,
-                              int64_t Tp, int64_t T, hipStream_t s) {
-    hipLaunchKernelGGL(final_state, grid_for(nslots, 256), 256, 0, s, O, I, st_o, st_i,
-                       slot_reach, G, nslots, Tp, T);
+                              const int64_t* jbase, const int64_t* slot_reach, int64_t nslots,
+                              int slots, int64_t T, hipStream_t s) {
+    hipLaunchKernelGGL(final_state, grid_for(nslots, 256), 256, 0, s, O, I, st_o, st_i, jbase,
+                       slot_reach, nslots, slots, T);
     return hipGetLastError();
 }
 
-hipError_t launch_transpose(const double* S, const uint8_t* rpad, double* out, int64_t n,
-                            int64_t Tp, int64_t t0, int64_t t1, hipStream_t s) {
+hipError_t launch_gather_steps(const double* S, const int64_t* jbase, int slots, double* out,
+                               int64_t n, int64_t t0, int64_t t1, hipStream_t s) {
     if (n <= 0 || t1 <= t0) return hipSuccess;
-    dim3 grid((unsigned)((n + 63) / 64), (unsigned)((t1 - t0 + 63) / 64));
-    hipLaunchKernelGGL(transpose_rt, grid, 256, 0, s, S, rpad, out, n, Tp, t0, t1);
+    hipLaunchKernelGGL(gather_steps, grid_for(n * (t1 - t0), 256), 256, 0, s, S, jbase, slots,
+                       out, n, t0, t1);
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const double* S, const uint8_t* rpad, double* out, int64_t n,
-                          int64_t Tp, int64_t T, hipStream_t s) {
+hipError_t launch_gather_series(const double* S, const int64_t* jbase, int slots, double* out,
+                                int64_t n, int64_t T, hipStream_t s) {
     if (n <= 0 || T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(compact_rows, grid_for(n * T, 256), 256, 0, s, S, rpad, out, n, Tp, T);
+    hipLaunchKernelGGL(gather_series, grid_for(n * T, 256), 256, 0, s, S, jbase, slots, out, n,
+                       T);
     return hipGetLastError();
 }
 

@@ -1,5 +1,12 @@
 // Device-side entry points of the Muskingum routing engine (gfx950).  Launchers are plain host
 // functions so the C-ABI layer (capi.cpp) stays free of kernel syntax.
+//
+// Output layout ("workgroup windows").  Workgroup w owns the ticks [gmin[w], gmax[w] + T) of the
+// space-time schedule; its outputs are stored tick-major inside that window:
+//     O[wbase[w] + (tick - gmin[w]) * SLOTS + lane]
+// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  Step t of the reach in
+// slot d = w * SLOTS + lane lives at tick G[d] + t, i.e. at  jbase[j] + t * SLOTS  for its caller
+// index j (jbase is computed per horizon by launch_window_index).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -8,16 +15,12 @@
 
 namespace mcr {
 
-// Ticks per register chunk.  Series rows are padded so that a chunk always covers one aligned
-// 64-byte segment: step t of reach j lives at  row(j) * Tp + t + (G[j] & (kChunk - 1)).
+// Ticks whose lateral inflow is formed in one burst (and whose forcing rows are prefetched
+// together).  Launch lengths (`tile`) are multiples of it.
 constexpr int kChunk = 8;
 
-inline int64_t padded_steps(int64_t T) {  // Tp: room for the pad and a full trailing chunk
-    return ((T + 2 * kChunk - 1) / kChunk) * kChunk;
-}
-
 // Everything the wavefront kernel reads, by value.  Per-slot arrays are in device-slot order
-// (plan.hpp); the output series are reach-major in the CALLER's order, padded as above.
+// (plan.hpp).
 struct WaveArgs {
     const int32_t* active;        // workgroup ids of this launch
     const int32_t* G;             // [nslots]
@@ -26,11 +29,9 @@ struct WaveArgs {
     const uint64_t* up4;          // [nslots]
     const int32_t* up_more_off;   // [nslots + 1]
     const uint16_t* up_more;
-    const int64_t* slot_reach;    // [nslots] caller reach index or -1
     const int32_t* ext_off;       // [nwg + 1]
-    const int64_t* ext_src;       // caller index of the upstream reach
+    const int64_t* ext_at;        // per external input: window index of its source's step 0
     const int32_t* ext_g;         // G of the consuming reach
-    const uint8_t* rpad;          // [n] pad of each caller reach (G & 15)
     const double* alpha;          // [nslots]
     const double* beta;
     const double* chi;
@@ -39,15 +40,15 @@ struct WaveArgs {
     const double* st_i;
     const double* F;              // forcing rows in slot order [n_rows][nslots]
     const int4* stab;             // per step {row_lo, row_hi (-1 = copy row_lo), frac (f64)}
-    const int32_t* wg_gmin;       // [nwg] G range of each workgroup (step-table window)
+    const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
     const int32_t* wg_gmax;
-    double* O;                    // [n][Tp]
-    double* I;                    // [n][Tp]
-    double* dummy;                // >= 2 * kChunk doubles: target of out-of-range chunks
+    const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
+    double* O;                    // workgroup windows (see above)
+    double* I;
+    double* dummy;                // >= 2 * 1024 doubles: target of out-of-window ticks
     int64_t nslots;
     int32_t n_rows;
     int32_t T;
-    int32_t Tp;
     int32_t kappa0;               // first tick of this launch (multiple of kChunk)
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
@@ -61,7 +62,7 @@ inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int til
            8 * (size_t)ext_cap * tile + 4 * (size_t)more_cap;
 }
 
-// dense: the step table has an 8-step window spanning more than 3 forcing rows
+// dense: the step table has a kChunk-step window spanning more than 3 forcing rows
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
                             hipStream_t s);
 
@@ -74,15 +75,20 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 // F[r][d] = fp[r][slot_reach[d]]  (forcing table to slot order; 0 for padding slots)
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, hipStream_t s);
-// state after the last step: st[d] = O[row(d)][T - 1]
+// jbase[j] = window index of step 0 of caller reach j;  ext_at[e] = jbase[ext_src[e]]
+hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
+                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
+                               const int64_t* ext_src, int64_t n_ext, int64_t* ext_at,
+                               hipStream_t s);
+// state after the last step: st[d] = step T-1 of slot d
 hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,
-                              const int64_t* slot_reach, const int32_t* G, int64_t nslots,
-                              int64_t Tp, int64_t T, hipStream_t s);
-// out[t - t0][j] = S[j][t]  for t in [t0, t1)   (padded reach-major -> step-major)
-hipError_t launch_transpose(const double* S, const uint8_t* rpad, double* out, int64_t n,
-                            int64_t Tp, int64_t t0, int64_t t1, hipStream_t s);
-// out[j][t] = S[j][t] for t in [0, T)   (drop the padding)
-hipError_t launch_compact(const double* S, const uint8_t* rpad, double* out, int64_t n,
-                          int64_t Tp, int64_t T, hipStream_t s);
+                              const int64_t* jbase, const int64_t* slot_reach, int64_t nslots,
+                              int slots, int64_t T, hipStream_t s);
+// out[t - t0][j] = S[jbase[j] + t * slots]  for t in [t0, t1)   (step-major, caller order)
+hipError_t launch_gather_steps(const double* S, const int64_t* jbase, int slots, double* out,
+                               int64_t n, int64_t t0, int64_t t1, hipStream_t s);
+// out[j][t] = S[jbase[j] + t * slots]  for t in [0, T)   (reach-major, caller order)
+hipError_t launch_gather_series(const double* S, const int64_t* jbase, int slots, double* out,
+                                int64_t n, int64_t T, hipStream_t s);
 
 }  // namespace mcr
