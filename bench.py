@@ -52,26 +52,13 @@ def parse():
     return ap.parse_args()
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def build_workload(args, rank=0):
+    """Texas-scale synthetic network, coefficients, state and forcing, loaded into a RoutingNet.
+    Returns (net, w): w holds the host arrays (w.x = step times of one horizon)."""
+    from types import SimpleNamespace
 
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
-
-    from oracle import oracle as orc  # noqa: F401  (cpu_baseline leg only)
     from tx_fast_hydrology_amd import engine, synthetic
 
-    # ---- workload -------------------------------------------------------------------------
-    t_setup = time.time()
     end = synthetic.river_network(args.n, args.basins, args.depth, np.random.default_rng(0))
     n = end.size
     K, X, o0 = synthetic.model_arrays(n, seed=0)
@@ -94,6 +81,32 @@ def main():
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
+    w = SimpleNamespace(n=n, start=start, end=end, indeg=indeg, alpha=alpha, beta=beta, chi=chi,
+                        gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt)
+    return net, w
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+
+    from oracle import oracle as orc  # noqa: F401  (cpu_baseline leg only)
+
+    # ---- workload -------------------------------------------------------------------------
+    t_setup = time.time()
+    net, wl = build_workload(args, rank)
+    n, x = wl.n, wl.x
     info = net.info
     setup_s = time.time() - t_setup
 
@@ -139,12 +152,12 @@ def main():
     # ---- CPU baseline (serial transliteration of the reference loop, rank 0 at N=1) --------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        o_s, i_s = o0.copy(), i0.copy()
+        o_s, i_s = wl.o0.copy(), wl.i0.copy()
         reps, t_cpu = 0, 0.0
         while t_cpu < args.cpu_seconds or reps == 0:
             c0 = time.perf_counter()
-            orc.simulate(start, end, indeg, alpha, beta, chi, gamma, o_s, i_s, x, xp, fp,
-                         keep_outputs=False)
+            orc.simulate(wl.start, wl.end, wl.indeg, wl.alpha, wl.beta, wl.chi, wl.gamma, o_s,
+                         i_s, x, wl.xp, wl.fp, keep_outputs=False)
             t_cpu += time.perf_counter() - c0
             reps += 1
         cpu = {"value": float(n) * args.T * reps / t_cpu, "unit": "reach·timesteps/s",
@@ -168,9 +181,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": "texas-det (BASELINE configs[1]): full-Texas synthetic "
                                    "network, deterministic, 24 h @ 300 s",
-                       "n_reaches": n, "outlets": int((end == start).sum()),
-                       "max_height": info["max_height"], "T": args.T, "dt_s": dt,
-                       "forcing_rows": rows, "parallelism": f"replicas x{world}",
+                       "n_reaches": n, "outlets": int((wl.end == wl.start).sum()),
+                       "max_height": info["max_height"], "T": args.T, "dt_s": wl.dt,
+                       "forcing_rows": wl.rows, "parallelism": f"replicas x{world}",
                        "slots": info["slots"], "tile": info["tile"], "nwg": info["nwg"],
                        "schedule_ticks": info["gmax"] + args.T, "setup_s": round(setup_s, 2)},
             "roofline": roofline,

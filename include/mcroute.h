@@ -144,6 +144,14 @@ int mc_set_timing(void* net, int enable);
 int mc_get_timing(void* net, double* kernel_ms, int64_t* launches, double* run_ms);
 int mc_reset_timing(void* net);
 
+/* Launch trace of the last mc_run (off by default; diagnostic).  One record of 6 int64 per
+ * workgroup per launch: {launch, workgroup, t_start, t_loop, t_end, hw_id}; times are ticks of
+ * the device's constant wall clock (clock_khz), t_loop is the end of the launch prologue, hw_id
+ * is the XCC/SE/CU id of the workgroup's first wave.  n_records receives the record count;
+ * at most `cap` records are copied to `out` (which may be NULL). */
+int mc_set_trace(void* net, int enable);
+int mc_get_trace(void* net, int64_t* out, int64_t cap, int64_t* n_records, int64_t* clock_khz);
+
 #ifdef __cplusplus
 }
 #endif

@@ -142,11 +142,11 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, up_more_off, ext_off, ext_g, active, wg_gmin, wg_gmax;
+    DBuf<int32_t> G, up_more_off, ext_off, ext_g, active, wg_gmin, wg_gmax, xid;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
     DBuf<uint16_t> up_more;
-    DBuf<int64_t> slot_reach, ext_src, pos;
+    DBuf<int64_t> slot_reach, pos;
     int32_t more_cap = 0;          // max overflow upstream codes of one workgroup
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
@@ -160,19 +160,25 @@ struct Net {
     // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
     // and the dummy row of out-of-window ticks
     DBuf<double> O, I, outT, dummy;
-    DBuf<int64_t> wbase, jbase, ext_at;
+    DBuf<int64_t> wbase, jbase;
+    DBuf<double> XS;               // external-input streams [n_ext][T]
     int64_t T_out = 0;
     bool coeffs_set = false;
 
     // active-workgroup schedule cache
     int64_t sched_T = -1;
     std::vector<int64_t> sched_off;
+    std::vector<int32_t> active_list;
 
     // timing
     bool timing = false;
     double kernel_ms = 0.0, run_ms = 0.0;
     int64_t launches = 0;
     std::vector<hipEvent_t> events;
+    // launch trace (mc_set_trace)
+    bool trace = false;
+    DBuf<int64_t> trace_buf;
+    std::vector<int64_t> trace_launch;   // launch index of each traced workgroup record
 
     ~Net() {
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
@@ -197,17 +203,14 @@ struct Net {
         up_more.upload(plan.up_more.data(), plan.up_more.size(), stream);
         slot_reach.upload(plan.slot_reach.data(), ns, stream);
         ext_off.upload(plan.ext_off.data(), plan.ext_off.size(), stream);
-        {
-            ext_src.upload(plan.ext_src.data(), plan.ext_src.size(), stream);
-            for (int32_t w = 0; w < plan.nwg; ++w) {
-                const int64_t a0 = plan.up_more_off[(int64_t)w * plan.p.slots];
-                const int64_t a1 = plan.up_more_off[(int64_t)(w + 1) * plan.p.slots];
-                more_cap = std::max<int32_t>(more_cap, (int32_t)(a1 - a0));
-            }
-            HIPC(hipStreamSynchronize(stream));
+        for (int32_t w = 0; w < plan.nwg; ++w) {
+            const int64_t a0 = plan.up_more_off[(int64_t)w * plan.p.slots];
+            const int64_t a1 = plan.up_more_off[(int64_t)(w + 1) * plan.p.slots];
+            more_cap = std::max<int32_t>(more_cap, (int32_t)(a1 - a0));
         }
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
+        xid.upload(plan.xid.data(), plan.xid.size(), stream);
         wg_gmin.upload(plan.wg_gmin.data(), plan.wg_gmin.size(), stream);
         wg_gmax.upload(plan.wg_gmax.data(), plan.wg_gmax.size(), stream);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
@@ -255,7 +258,7 @@ struct Net {
     // Per-horizon layout: active workgroups of every launch and the output windows.
     void ensure_schedule(int64_t T) {
         if (sched_T == T) return;
-        std::vector<int32_t> list;
+        std::vector<int32_t>& list = active_list;
         mcr::active_schedule(plan, T, list, sched_off);
         active.upload(list.data(), list.size(), stream);
         std::vector<int64_t> wb(plan.nwg);
@@ -268,10 +271,9 @@ struct Net {
         O.reserve((size_t)total);
         I.reserve((size_t)total);
         jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
-        ext_at.reserve(std::max<size_t>(plan.ext_src.size(), 1));
+        XS.reserve(std::max<size_t>(plan.ext_src.size() * (size_t)T, 1));
         HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, wbase.p, plan.p.slots, plan.n,
-                                      jbase.p, ext_src.p, (int64_t)plan.ext_src.size(), ext_at.p,
-                                      stream));
+                                      jbase.p, stream));
         HIPC(hipStreamSynchronize(stream));
         sched_T = T;
     }
@@ -316,7 +318,8 @@ struct Net {
         a.up_more_off = up_more_off.p;
         a.up_more = up_more.p;
         a.ext_off = ext_off.p;
-        a.ext_at = ext_at.p;
+        a.xid = xid.p;
+        a.XS = XS.p;
         a.ext_g = ext_g.p;
         a.alpha = alpha.p;
         a.beta = beta.p;
@@ -342,10 +345,16 @@ struct Net {
         const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
                                                     a.tile, a.more_cap);
         int64_t launched = 0;
+        trace_launch.clear();
+        if (trace) trace_buf.reserve(4 * (size_t)std::max<int64_t>(sched_off[nl], 1));
         for (int64_t k = 0; k < nl; ++k) {
             const int64_t grid = sched_off[k + 1] - sched_off[k];
             if (grid == 0) continue;
             a.active = active.p + sched_off[k];
+            if (trace) {
+                a.trace = trace_buf.p + 4 * sched_off[k];
+                trace_launch.resize(sched_off[k + 1], k);
+            }
             a.kappa0 = (int32_t)(k * plan.p.tile);
             if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
             HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, dense, stream));
@@ -665,6 +674,38 @@ int mc_reset_timing(void* net) {
         Net* N = as_net(net);
         N->kernel_ms = N->run_ms = 0.0;
         N->launches = 0;
+    });
+}
+
+int mc_set_trace(void* net, int enable) {
+    return guarded([&] { as_net(net)->trace = enable != 0; });
+}
+
+int mc_get_trace(void* net, int64_t* out, int64_t cap, int64_t* n_records, int64_t* clock_khz) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        const int64_t m = (int64_t)N->trace_launch.size();
+        if (n_records) *n_records = m;
+        if (clock_khz) {
+            int khz = 0;
+            HIPC(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, N->device));
+            *clock_khz = khz;
+        }
+        if (!out || cap <= 0 || m == 0) return;
+        std::vector<int64_t> raw(4 * (size_t)m);
+        HIPC(hipStreamSynchronize(N->stream));
+        HIPC(hipMemcpy(raw.data(), N->trace_buf.p, raw.size() * sizeof(int64_t),
+                       hipMemcpyDeviceToHost));
+        const std::vector<int32_t>& list = N->active_list;
+        for (int64_t r = 0; r < std::min(cap, m); ++r) {
+            int64_t* o = out + 6 * r;
+            o[0] = N->trace_launch[r];
+            o[1] = list[r];
+            o[2] = raw[4 * r];
+            o[3] = raw[4 * r + 1];
+            o[4] = raw[4 * r + 2];
+            o[5] = raw[4 * r + 3] & 0xffffffff;
+        }
     });
 }
 

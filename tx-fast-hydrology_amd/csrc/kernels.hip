@@ -55,7 +55,8 @@ __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
 //   FR  [SLOTS][3]     f64  the lane's forcing rows rb .. rb + 2 of the current chunk
 //   TAB [table_cap]    int4 step-table window {row_lo, row_hi, frac}
 //   XE  [ext_cap][tile] f64 external inputs of this launch
-//   XM  [more_cap]     u32  overflow upstream codes (5th and later upstream reaches)
+//   XM  [4 + more_cap] u32  overflow upstreams (5th and later) as resolved LDS byte addresses,
+//                           bit 0 set for external inputs; group 0 is all zero-slot addresses
 // DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
@@ -74,6 +75,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     unsigned* xm = reinterpret_cast<unsigned*>(lds + XM);
 
     const int tid = threadIdx.x;
+    const int64_t t_start = a.trace ? wall_clock64() : 0;
     const int w = a.active[blockIdx.x];
     const int64_t d = (int64_t)w * SLOTS + tid;
     const int T = a.T;
@@ -103,6 +105,8 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int m0 = a.up_more_off[(int64_t)w * SLOTS];
     const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
     const int more = a.up_more_off[d] - m0;
+    const int more_end = a.up_more_off[d + 1] - m0;
+    const int xsid = a.xid[d];
 
     // ---- step-table window of this workgroup -> LDS
     int tw0 = k0 - gmaxw, tw1 = k0 + tile - gminw;
@@ -114,30 +118,39 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int e0 = a.ext_off[w];
     const int ntot = (a.ext_off[w + 1] - e0) * tile;
     for (int base = tid; base < ntot; base += 8 * SLOTS) {
-        int ti[8], eg[8];
-        int64_t at0[8];
+        int ti[8], eg[8], ee[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {   // unconditional (clamped) loads: one wait per batch
             const int idx = min(base + k * SLOTS, ntot - 1);
             const int e = idx / tile;
             ti[k] = k0 + (idx - e * tile);
+            ee[k] = e0 + e;
             eg[k] = a.ext_g[e0 + e];
-            at0[k] = a.ext_at[e0 + e];                    // source's step 0 in its window
         }
         double v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < 8; ++k) {   // consecutive lanes read consecutive steps of a stream
             const int t = ti[k] - eg[k];
             const bool ok = t >= 0 && t < T;
-            v[k] = a.O[ok ? at0[k] + (int64_t)t * SLOTS : 0];
+            v[k] = a.XS[ok ? (int64_t)ee[k] * T + t : 0];
             v[k] = ok ? v[k] : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             if (base + k * SLOTS < ntot) xe[base + k * SLOTS] = v[k];
     }
-    // ---- overflow upstream codes of this workgroup -> LDS
-    for (int idx = tid; idx < nm; idx += SLOTS) xm[idx] = a.up_more[m0 + idx];
+    // ---- overflow upstream codes of this workgroup -> LDS byte addresses (bit 0: external)
+    for (int idx = tid; idx < nm + kUpGroup; idx += SLOTS) {
+        unsigned ent = XB + (unsigned)SLOTS * 16;         // zero group / padding: the zero slot
+        if (idx >= kUpGroup) {
+            const unsigned code = a.up_more[m0 + idx - kUpGroup];
+            ent = (code & kExtBit) ? ((XE + (code & 0x7fffu) * (unsigned)tile * 8) | 1u)
+                                   : XB + code * 16;
+        }
+        xm[idx] = ent;
+    }
+    const int ngrp = live ? (more_end - more) / kUpGroup : 0;       // this lane's groups
+    const unsigned gofs = XM + (unsigned)(kUpGroup + more) * 4;       // its first group
 
     double op = from_out ? o_ld : st_o;
     double ip = from_out ? i_ld : st_i;
@@ -160,7 +173,8 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         uinc[u] = ext ? 16u : 0u;
     }
     const bool any3 = __any(cnt > 2);                   // wave-uniform
-    const bool any5 = __any(cnt > kUpInline);
+    int ngw = 0;                                        // overflow groups of the wave
+    while (__any(ngw < ngrp)) ++ngw;
     const unsigned own = XB + (unsigned)tid * 16;
 
     // forcing rows of the first chunk
@@ -170,8 +184,12 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     double f1 = a.F[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
     double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
     __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
+    const int64_t t_loop = a.trace ? wall_clock64() : 0;
 
     const int wend = gmaxw + T;                         // end of this workgroup's window
+    // feeds another cluster: step t also goes to XS[xsid][t] (address at tick k: xs0 + k)
+    const bool xsrc = live && xsid >= 0;
+    const int64_t xs0 = xsrc ? (int64_t)xsid * T - Gr : 0;
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         // this chunk's forcing rows -> the lane's LDS slots (private: no barrier needed)
@@ -230,14 +248,22 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                     I = I + lds_f64(lds, m[2] + rd);
                     I = I + lds_f64(lds, m[3] + rd);
                 }
-                if (any5) {
-                    for (int u = kUpInline; u < cnt; ++u) {
-                        const unsigned code = xm[more + u - kUpInline];
-                        const unsigned at = (code & kExtBit)
-                                                ? XE + ((code & 0x7fffu) * tile + c + i) * 8u
-                                                : XB + code * 16 + rd;
-                        I = I + lds_f64(lds, at);
-                    }
+                // overflow upstreams, one group of kUpGroup per 16-byte LDS read; lanes past
+                // their own list read the zero group
+                const unsigned sx = 8u * (unsigned)(c + i);   // external-input column of tick i
+                for (int g = 0; g < ngw; ++g) {
+                    const uint4 e = *reinterpret_cast<const uint4*>(
+                        lds + (g < ngrp ? gofs + 16u * g : XM));
+                    const unsigned a0 = (e.x & ~1u) + ((e.x & 1u) ? sx : rd);
+                    const unsigned a1 = (e.y & ~1u) + ((e.y & 1u) ? sx : rd);
+                    const unsigned a2 = (e.z & ~1u) + ((e.z & 1u) ? sx : rd);
+                    const unsigned a3 = (e.w & ~1u) + ((e.w & 1u) ? sx : rd);
+                    const double v0 = lds_f64(lds, a0), v1 = lds_f64(lds, a1);
+                    const double v2 = lds_f64(lds, a2), v3 = lds_f64(lds, a3);
+                    I = I + v0;
+                    I = I + v1;
+                    I = I + v2;
+                    I = I + v3;
                 }
                 const double ov = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[j]);
                 // inactive ticks write garbage that no active reach reads (its consumer is
@@ -253,6 +279,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                 double* irow = inwin ? a.I + row : a.dummy + SLOTS;
                 orow[tid] = routed ? ov : 0.0;
                 irow[tid] = I;
+                if (xsrc && act) a.XS[xs0 + k] = ov;
                 __syncthreads();
             }
         }
@@ -261,6 +288,13 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         f0 = g0;
         f1 = g1;
         f2 = g2;
+    }
+    if (a.trace && tid == 0) {
+        int64_t* rec = a.trace + 4 * (int64_t)blockIdx.x;
+        rec[0] = t_start;
+        rec[1] = t_loop;
+        rec[2] = wall_clock64();
+        rec[3] = (int64_t)__smid() | ((int64_t)w << 32);
     }
 }
 
@@ -305,12 +339,6 @@ __global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __r
     }
 }
 
-__global__ void ext_index(const int64_t* __restrict__ jbase, const int64_t* __restrict__ ext_src,
-                          int64_t n_ext, int64_t* __restrict__ ext_at) {
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n_ext;
-         e += (int64_t)gridDim.x * blockDim.x)
-        ext_at[e] = jbase[ext_src[e]];
-}
 
 __global__ void final_state(const double* __restrict__ O, const double* __restrict__ I,
                             double* __restrict__ st_o, double* __restrict__ st_i,
@@ -402,14 +430,10 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
 
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
                                const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
-                               const int64_t* ext_src, int64_t n_ext, int64_t* ext_at,
                                hipStream_t s) {
     if (n > 0)
         hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
                            slots, n, jbase);
-    if (n_ext > 0)
-        hipLaunchKernelGGL(ext_index, grid_for(n_ext, 256), 256, 0, s, jbase, ext_src, n_ext,
-                           ext_at);
     return hipGetLastError();
 }
 

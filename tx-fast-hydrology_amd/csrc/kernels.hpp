@@ -4,7 +4,9 @@
 // Output layout ("workgroup windows").  Workgroup w owns the ticks [gmin[w], gmax[w] + T) of the
 // space-time schedule; its outputs are stored tick-major inside that window:
 //     O[wbase[w] + (tick - gmin[w]) * SLOTS + lane]
-// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  Step t of the reach in
+// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  A reach that feeds a
+// reach of another cluster (an "external input" of the consumer's workgroup) also writes its
+// outflow to a step-contiguous stream XS[e][t], which the consumer reads coalesced.  Step t of the reach in
 // slot d = w * SLOTS + lane lives at tick G[d] + t, i.e. at  jbase[j] + t * SLOTS  for its caller
 // index j (jbase is computed per horizon by launch_window_index).
 #pragma once
@@ -30,7 +32,7 @@ struct WaveArgs {
     const int32_t* up_more_off;   // [nslots + 1]
     const uint16_t* up_more;
     const int32_t* ext_off;       // [nwg + 1]
-    const int64_t* ext_at;        // per external input: window index of its source's step 0
+    const int32_t* xid;           // [nslots] external input fed by the slot's reach, -1 if none
     const int32_t* ext_g;         // G of the consuming reach
     const double* alpha;          // [nslots]
     const double* beta;
@@ -45,7 +47,9 @@ struct WaveArgs {
     const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
     double* O;                    // workgroup windows (see above)
     double* I;
+    double* XS;                   // external-input streams [n_ext][T]: step t of each source
     double* dummy;                // >= 2 * 1024 doubles: target of out-of-window ticks
+    int64_t* trace;               // optional launch trace, 4 words per workgroup (NULL = off)
     int64_t nslots;
     int32_t n_rows;
     int32_t T;
@@ -53,13 +57,13 @@ struct WaveArgs {
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
-    int32_t more_cap;             // LDS words reserved for overflow upstream codes
+    int32_t more_cap;             // LDS words reserved for overflow upstream addresses (+ a zero group)
 };
 
 inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile,
                                   int more_cap) {
     return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)table_cap +
-           8 * (size_t)ext_cap * tile + 4 * (size_t)more_cap;
+           8 * (size_t)ext_cap * tile + 4 * ((size_t)more_cap + 4);
 }
 
 // dense: the step table has a kChunk-step window spanning more than 3 forcing rows
@@ -75,10 +79,9 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 // F[r][d] = fp[r][slot_reach[d]]  (forcing table to slot order; 0 for padding slots)
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, hipStream_t s);
-// jbase[j] = window index of step 0 of caller reach j;  ext_at[e] = jbase[ext_src[e]]
+// jbase[j] = window index of step 0 of caller reach j
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
                                const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
-                               const int64_t* ext_src, int64_t n_ext, int64_t* ext_at,
                                hipStream_t s);
 // state after the last step: st[d] = step T-1 of slot d
 hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,

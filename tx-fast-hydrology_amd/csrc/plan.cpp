@@ -318,7 +318,10 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (size_t k = 0; k < codes.size() && k < (size_t)kUpInline; ++k)
             packed |= (uint64_t)codes[k] << (16 * k);
         P.up4[d] = packed;
+        // overflow list padded to whole groups of kUpGroup with the zero-slot code: the kernel
+        // reads it one group at a time (adding +0.0 to the running sum is exact)
         for (size_t k = kUpInline; k < codes.size(); ++k) P.up_more.push_back(codes[k]);
+        while (P.up_more.size() % kUpGroup) P.up_more.push_back((uint16_t)C);
         P.up_more_off[d + 1] = (int32_t)P.up_more.size();
     }
     for (int32_t w = 0; w < P.nwg; ++w) {
@@ -328,6 +331,13 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             P.ext_src.push_back(pr.first);
             P.ext_g.push_back(pr.second);
         }
+    }
+    // each reach has one downstream reach, so it feeds at most one external input
+    P.xid.assign(P.nslots, -1);
+    for (size_t e = 0; e < P.ext_src.size(); ++e) {
+        const int64_t d = P.pos[P.ext_src[e]];
+        if (P.xid[d] != -1) return "internal: reach feeds two external inputs";
+        P.xid[d] = (int32_t)e;
     }
     return std::string();
 }

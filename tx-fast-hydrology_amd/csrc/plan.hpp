@@ -40,6 +40,7 @@ constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 
 // workgroup-local slot of the upstream reach.
 constexpr uint16_t kExtBit = 0x8000;
 constexpr int kUpInline = 4;  // upstream codes kept in registers; more go to an overflow list
+constexpr int kUpGroup = 4;   // overflow lists are padded to whole groups (one 16-byte LDS read)
 
 enum SlotFlags : uint8_t {
     kSlotPad = 0,        // unused thread slot
@@ -70,8 +71,9 @@ struct Plan {
     std::vector<uint8_t> flags;
     std::vector<uint8_t> up_cnt;
     std::vector<uint64_t> up4;         // first kUpInline codes, 16 bits each
-    std::vector<int32_t> up_more_off;  // overflow list offset (codes kUpInline..)
-    std::vector<uint16_t> up_more;
+    std::vector<int32_t> up_more_off;  // overflow list offset (codes kUpInline..), per-lane lists
+    std::vector<uint16_t> up_more;     // padded to kUpGroup with the zero-slot code (= slots)
+    std::vector<int32_t> xid;          // external input this reach feeds (index into ext_*), -1
 
     // per workgroup
     std::vector<int32_t> wg_gmin, wg_gmax;  // G range of the workgroup's real reaches

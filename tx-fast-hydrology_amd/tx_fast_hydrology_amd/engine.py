@@ -204,6 +204,19 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
+    def set_trace(self, enable: bool):
+        nat.check(nat.lib().mc_set_trace(self._h, 1 if enable else 0))
+
+    def trace(self) -> tuple:
+        """Launch trace of the last run: (records [m, 6] int64, clock_khz); see mcroute.h."""
+        m = ctypes.c_int64()
+        khz = ctypes.c_int64()
+        nat.check(nat.lib().mc_get_trace(self._h, None, 0, ctypes.byref(m), ctypes.byref(khz)))
+        out = np.zeros((m.value, 6), dtype=np.int64)
+        nat.check(nat.lib().mc_get_trace(self._h, out.ctypes.data_as(ctypes.c_void_p), m.value,
+                                         ctypes.byref(m), ctypes.byref(khz)))
+        return out, khz.value
+
     def close(self):
         if getattr(self, "_h", None):
             nat.lib().mc_net_destroy(self._h)
