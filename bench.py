@@ -145,7 +145,8 @@ def main():
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                "kernel": "wavefront_det", "launches_per_step": tm["launches"] / args.timing_runs,
+                "kernel": "wavefront_flow" if net.mode()[1] == "dataflow" else "wavefront_det",
+                "launches_per_step": tm["launches"] / args.timing_runs,
                 "avg_launch_us": round(launch_ms * 1e3, 3),
                 "kernel_ms_per_step": round(tm["kernel_ms"] / args.timing_runs, 4)}
 

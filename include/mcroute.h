@@ -144,11 +144,19 @@ int mc_set_timing(void* net, int enable);
 int mc_get_timing(void* net, double* kernel_ms, int64_t* launches, double* run_ms);
 int mc_reset_timing(void* net);
 
-/* Launch trace of the last mc_run (off by default; diagnostic).  One record of 6 int64 per
- * workgroup per launch: {launch, workgroup, t_start, t_loop, t_end, hw_id}; times are ticks of
- * the device's constant wall clock (clock_khz), t_loop is the end of the launch prologue, hw_id
- * is the XCC/SE/CU id of the workgroup's first wave.  n_records receives the record count;
- * at most `cap` records are copied to `out` (which may be NULL). */
+/* Execution path of mc_run / mc_step.  mode 0 (default): one resident dataflow launch for the
+ * whole horizon when the network fits the device at once, else launches of `tile` ticks;
+ * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit).
+ * last_path: 1 or 2 = the path the last run took (0 before any run). */
+int mc_set_mode(void* net, int mode);
+int mc_get_mode(void* net, int* mode, int* last_path);
+
+/* Launch trace of the last mc_run (off by default; diagnostic).  One record of 8 int64 per
+ * workgroup per launch: {launch, workgroup, t_start, t_loop, t_end, hw_id, c_loop, c_end}.
+ * t_* are ticks of the device's constant wall clock (clock_khz); t_loop is the end of the launch
+ * prologue; hw_id is the XCC/SE/CU id of the workgroup's first wave; c_loop / c_end are its
+ * shader-clock counter at the start / end of the tick loop.  n_records receives the record
+ * count; at most `cap` records are copied to `out` (which may be NULL). */
 int mc_set_trace(void* net, int enable);
 int mc_get_trace(void* net, int64_t* out, int64_t cap, int64_t* n_records, int64_t* clock_khz);
 

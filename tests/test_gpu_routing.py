@@ -3,6 +3,10 @@
 Every discharge comparison is BIT-EXACT (np.array_equal on float64): the kernel keeps the
 reference's association, FMA contraction is off, and inflows are summed in the reference's
 finalisation order.  The north-star tolerance (1e-6 relative) is therefore not needed here.
+
+Every test runs twice: with the multi-launch path forced ("launches", kernels.hip) and in the
+default mode ("auto"), which routes the whole horizon as one resident dataflow launch
+(flow.hip) whenever the network fits the device.
 """
 import hashlib
 
@@ -13,6 +17,18 @@ from oracle import oracle as orc
 from tx_fast_hydrology_amd import engine, synthetic
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["launches", "auto"])
+def exec_mode(request, monkeypatch):
+    orig = engine.RoutingNet.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.set_mode(request.param)
+
+    monkeypatch.setattr(engine.RoutingNet, "__init__", init)
+    return request.param
 
 
 def _model(endnodes, K, X, dt, o0=None, seed=0):
@@ -189,9 +205,11 @@ def test_session_rejects_unaligned_tile():
         engine.RoutingNet(np.array([0]), np.array([0]), np.array([0]), tile=5)
 
 
-def test_texas_scale_bitexact_vs_oracle():
+@pytest.mark.parametrize("slots", [256, 448])
+def test_texas_scale_bitexact_vs_oracle(exec_mode, slots):
     """Full Texas-size network (190k reaches, depth ~1500), 24 h @ 300 s: every output of every
-    step bit-identical to the serial oracle."""
+    step bit-identical to the serial oracle.  At 448 slots the network fits one resident
+    dataflow launch (auto mode takes it); at 256 it does not (auto falls back to launches)."""
     end = synthetic.texas(seed=0)
     n = end.size
     K, X, o0 = synthetic.model_arrays(n, seed=0)
@@ -201,8 +219,10 @@ def test_texas_scale_bitexact_vs_oracle():
     xp = xp.astype(float)
     x = xp[0] + 300e9 * np.arange(1, 289)
     want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
-    net = _net(end, indeg, heads, coef, o0, i0)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots)
     got_o, got_i = net.simulate(x, xp, fp)
+    flow = exec_mode != "launches" and slots == 448
+    assert net.mode()[1] == ("dataflow" if flow else "launches")
     assert np.array_equal(got_o, want_o)
     assert np.array_equal(got_i, want_i)
 
@@ -224,3 +244,61 @@ def test_steady_state_mass_balance():
     outlets = np.flatnonzero(end == np.arange(n))
     for r in outlets:
         np.testing.assert_allclose(o[r], q[root == r].sum(), rtol=1e-10)
+
+
+# ---------------------------------------------------------------- dataflow path specifics
+def _flow_case(n=6000, seed=11, basins=5, depth=400):
+    end = synthetic.river_network(n, basins, depth, np.random.default_rng(seed))
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=seed)
+    indeg, heads, coef, _, i0 = _model(end, K, X, 300.0, o0=o0)
+    xp, fp = synthetic.forcing(n, rows=9, seed=seed)
+    return end, indeg, heads, coef, o0, i0, xp.astype(float), fp
+
+
+def test_dataflow_forced_back_to_back_runs_and_mode_switches():
+    """Dataflow forced: consecutive runs (granule epochs advance), then alternating paths on one
+    session continuing the state -- all bit-exact against the oracle's continued simulation."""
+    end, indeg, heads, coef, o0, i0, xp, fp = _flow_case()
+    n = end.size
+    net = _net(end, indeg, heads, coef, o0, i0, slots=128, tile=16)
+    net.set_mode("dataflow")
+    net.load_forcing(xp, fp)
+    o_s, i_s = o0.copy(), i0.copy()
+    t_next = xp[0]
+    for r, mode in enumerate(["dataflow", "dataflow", "launches", "dataflow", "auto"]):
+        net.set_mode(mode)
+        T = 40 + 7 * r
+        x = t_next + 300e9 * np.arange(1, T + 1)
+        t_next = x[-1]
+        want_o, want_i, o_s, i_s = orc.simulate(np.arange(n), end, indeg, *coef, o_s, i_s, x, xp,
+                                                 fp)
+        net.run(x)
+        got_o, got_i = net.fetch_outputs()
+        assert net.mode()[1] == ("launches" if mode == "launches" else "dataflow"), mode
+        assert np.array_equal(got_o, want_o), (r, mode)
+        assert np.array_equal(got_i, want_i), (r, mode)
+
+
+def test_dataflow_single_step_api():
+    end, indeg, heads, coef, o0, i0, xp, fp = _flow_case(n=3000, seed=5)
+    net = _net(end, indeg, heads, coef, o0, i0)
+    net.set_mode("dataflow")
+    q = np.random.default_rng(1).uniform(0, 2, end.size)
+    i_n, o_n = net.step(q, o0, i0)
+    i_w, o_w = orc.ax_bu(heads, end, *coef, i0, o0, q, indeg)
+    assert net.mode()[1] == "dataflow"
+    assert np.array_equal(o_n, o_w) and np.array_equal(i_n, i_w)
+
+
+def test_dataflow_rejects_what_does_not_fit():
+    from tx_fast_hydrology_amd import _native as nat
+    end, indeg, heads, coef, o0, i0, xp, fp = _flow_case(n=2000, seed=3)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=64, tile=8)     # slack below 2 chunks
+    net.set_mode("dataflow")
+    net.load_forcing(xp, fp)
+    with pytest.raises(nat.RoutingError):
+        net.run(xp[0] + 300e9 * np.arange(1, 11))
+    net.set_mode("auto")
+    net.run(xp[0] + 300e9 * np.arange(1, 11))
+    assert net.mode()[1] == "launches"

@@ -159,7 +159,8 @@ struct Net {
     // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
     // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
     // and the dummy row of out-of-window ticks
-    DBuf<double> O, I, outT, dummy;
+    DBuf<double> O, BS, outT, dummy;
+    DBuf<int64_t> in_off, in_list;   // inflow lists (plan.hpp), caller order
     DBuf<int64_t> wbase, jbase;
     DBuf<double> XS;               // external-input streams [n_ext][T]
     int64_t T_out = 0;
@@ -175,12 +176,26 @@ struct Net {
     double kernel_ms = 0.0, run_ms = 0.0;
     int64_t launches = 0;
     std::vector<hipEvent_t> events;
+    // dataflow kernel (flow.hip): mode 0 = automatic, 1 = multi-launch only, 2 = dataflow only
+    int mode = 0;
+    int last_path = 0;             // 1 multi-launch, 2 dataflow (path of the last run)
+    int cu_count = 0;
+    DBuf<int32_t> all_wg;          // every workgroup, in plan order (the dataflow grid)
+    DBuf<uint32_t> XG;             // granules [n_ext][T][4 words]
+    size_t xg_words = 0;
+    uint32_t epoch = 0;
+    DBuf<int32_t> status;
+    int32_t* status_host = nullptr;  // pinned mirror, valid after a sync
+    bool status_pending = false;
+
     // launch trace (mc_set_trace)
     bool trace = false;
     DBuf<int64_t> trace_buf;
     std::vector<int64_t> trace_launch;   // launch index of each traced workgroup record
+    std::vector<int32_t> trace_wg;       // workgroup of each record
 
     ~Net() {
+        if (status_host) (void)hipHostFree(status_host);
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
     }
@@ -211,6 +226,10 @@ struct Net {
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
         xid.upload(plan.xid.data(), plan.xid.size(), stream);
+        in_off.upload(plan.in_off.data(), plan.in_off.size(), stream);
+        in_list.upload(plan.in_list.data(), plan.in_list.size(), stream);
+        in_list.reserve(1);
+        BS.reserve(2 * (size_t)std::max<int64_t>(plan.nslots, 1));
         wg_gmin.upload(plan.wg_gmin.data(), plan.wg_gmin.size(), stream);
         wg_gmax.upload(plan.wg_gmax.data(), plan.wg_gmax.size(), stream);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
@@ -219,7 +238,52 @@ struct Net {
         }
         stage.reserve(std::max<int64_t>(plan.n, 1));
         dummy.reserve(2 * 1024);
+        HIPC(hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device));
+        {
+            std::vector<int32_t> ids(std::max<int32_t>(plan.nwg, 1));
+            for (size_t w = 0; w < ids.size(); ++w) ids[w] = (int32_t)w;
+            all_wg.upload(ids.data(), ids.size(), stream);
+        }
+        status.reserve(1);
+        HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
+        HIPC(hipHostMalloc(reinterpret_cast<void**>(&status_host), sizeof(int32_t),
+                           hipHostMallocDefault));
+        *status_host = 0;
+        sync();
+    }
+
+    // Wait for the stream; report a dataflow run whose waits gave up.
+    void sync() {
         HIPC(hipStreamSynchronize(stream));
+        if (status_pending) {
+            status_pending = false;
+            if (*status_host != 0) {
+                *status_host = 0;
+                HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
+                throw Fail(MC_E_HIP, "dataflow kernel: a wait for upstream results gave up "
+                                     "(outputs of the last run are invalid)");
+            }
+        }
+    }
+
+    // Can the whole horizon run as one dataflow launch?  Every workgroup must be resident.
+    bool flow_fits(int64_t T, bool dense, size_t& lds) {
+        if (mode == 1) return false;
+        const int S = plan.p.slots;
+        const size_t xg = plan.ext_src.size() * (size_t)T * 16;
+        lds = mcr::flow_lds_bytes(S, (int)T, plan.max_ext_wg, more_cap);
+        bool ok = (S == 64 || S == 128 || S == 192 || S == 256 || S == 384 || S == 448) &&
+                  plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
+                  T <= mcr::kFlowMaxT && xg < (size_t(1) << 31) && lds <= 160 * 1024;
+        if (ok) {
+            int bpc = 0;
+            HIPC(mcr::flow_occupancy(S, dense, lds, &bpc));
+            ok = (int64_t)bpc * cu_count >= plan.nwg;
+        }
+        if (mode == 2 && !ok)
+            throw Fail(MC_E_STATE, "dataflow mode requested but this network/horizon does not fit "
+                                   "one resident launch");
+        return ok;
     }
 
     // caller-order host array -> slot-order device array
@@ -234,7 +298,7 @@ struct Net {
         if (n == 0) return;
         HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, stream));
         HIPC(hipMemcpyAsync(host, stage.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
-        HIPC(hipStreamSynchronize(stream));
+        sync();
     }
 
     void set_coeffs(const double* a, const double* b, const double* c, const double* g) {
@@ -243,16 +307,16 @@ struct Net {
         to_slots(b, beta);
         to_slots(c, chi);
         to_slots(g, gamma);
-        HIPC(hipStreamSynchronize(stream));  // `stage` is reused by the next call
+        sync();  // `stage` is reused by the next call
         coeffs_set = true;
     }
 
     void set_state(const double* o, const double* i) {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
         to_slots(o, st_o);
-        HIPC(hipStreamSynchronize(stream));
+        sync();
         to_slots(i, st_i);
-        HIPC(hipStreamSynchronize(stream));
+        sync();
     }
 
     // Per-horizon layout: active workgroups of every launch and the output windows.
@@ -269,12 +333,11 @@ struct Net {
         }
         wbase.upload(wb.data(), wb.size(), stream);
         O.reserve((size_t)total);
-        I.reserve((size_t)total);
         jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
         XS.reserve(std::max<size_t>(plan.ext_src.size() * (size_t)T, 1));
         HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, wbase.p, plan.p.slots, plan.n,
                                       jbase.p, stream));
-        HIPC(hipStreamSynchronize(stream));
+        sync();
         sched_T = T;
     }
 
@@ -304,7 +367,8 @@ struct Net {
             dense = last - tabh[t].x + 1 > 3;
         }
         stab.upload(tabh.data(), tabh.size(), stream);
-        HIPC(hipStreamSynchronize(stream));  // the host table is freed when the caller returns
+        sync();  // the host table is freed when the caller returns
+        last_path = 0;
         ensure_schedule(T);
         const int64_t nl = (int64_t)sched_off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
@@ -333,26 +397,62 @@ struct Net {
         a.wg_gmax = wg_gmax.p;
         a.wbase = wbase.p;
         a.O = O.p;
-        a.I = I.p;
+        a.BS = BS.p;
         a.dummy = dummy.p;
         a.nslots = plan.nslots;
         a.n_rows = (int32_t)rows;
         a.T = (int32_t)T;
         a.tile = plan.p.tile;
-        a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
         a.ext_cap = plan.max_ext_wg;
         a.more_cap = more_cap;
-        const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
-                                                    a.tile, a.more_cap);
         int64_t launched = 0;
         trace_launch.clear();
-        if (trace) trace_buf.reserve(4 * (size_t)std::max<int64_t>(sched_off[nl], 1));
-        for (int64_t k = 0; k < nl; ++k) {
+        trace_wg.clear();
+        size_t flds = 0;
+        if (flow_fits(T, dense, flds)) {
+            // ---- one dataflow launch for the whole horizon (flow.hip)
+            const size_t words = plan.ext_src.size() * (size_t)T * 4;
+            if (words > xg_words || epoch == 0xffffffffu) {
+                XG.reserve(std::max<size_t>(words, 4));
+                HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(words, 4) * 4, stream));
+                xg_words = std::max(xg_words, words);
+                epoch = 0;                 // granules of earlier runs can never match again
+            }
+            ++epoch;
+            a.XG = XG.p;
+            a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
+            a.epoch = epoch;
+            a.status = status.p;
+            a.table_cap = (int32_t)T;
+            a.active = all_wg.p;
+            if (trace) {
+                trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int32_t>(plan.nwg, 1));
+                a.trace = trace_buf.p;
+                trace_launch.assign(plan.nwg, 0);
+                for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
+            }
+            if (timing) HIPC(hipEventRecord(events[0], stream));
+            HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, flds, dense, stream));
+            if (timing) HIPC(hipEventRecord(events[1], stream));
+            HIPC(hipMemcpyAsync(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                stream));
+            status_pending = true;
+            launched = 1;
+            last_path = 2;
+        }
+        a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
+        const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
+                                                    a.tile, a.more_cap);
+        if (launched == 0 && trace) {
+            trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(sched_off[nl], 1));
+            trace_wg = active_list;
+        }
+        for (int64_t k = 0; k < nl && last_path != 2; ++k) {
             const int64_t grid = sched_off[k + 1] - sched_off[k];
             if (grid == 0) continue;
             a.active = active.p + sched_off[k];
             if (trace) {
-                a.trace = trace_buf.p + 4 * sched_off[k];
+                a.trace = trace_buf.p + mcr::kTraceWords * sched_off[k];
                 trace_launch.resize(sched_off[k + 1], k);
             }
             a.kappa0 = (int32_t)(k * plan.p.tile);
@@ -360,8 +460,10 @@ struct Net {
             HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, dense, stream));
             if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
             ++launched;
+            last_path = 1;
         }
-        HIPC(mcr::launch_final_state(O.p, I.p, st_o.p, st_i.p, jbase.p, slot_reach.p,
+        HIPC(mcr::launch_final_state(O.p, st_o.p, st_i.p, jbase.p, slot_reach.p, in_off.p,
+                                     in_list.p,
                                      plan.nslots, plan.p.slots, T, stream));
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
@@ -393,7 +495,7 @@ struct Net {
         tmp.upload(fp, (size_t)rows * n, stream);
         HIPC(mcr::launch_forcing_to_slots(tmp.p, F.p, slot_reach.p, n, plan.nslots, rows,
                                           stream));
-        HIPC(hipStreamSynchronize(stream));
+        sync();
     }
 
     void run(int64_t T, const double* x) {
@@ -429,7 +531,7 @@ struct Net {
             from_slots(st_o, o_out);
             from_slots(st_i, i_out);
         }
-        HIPC(hipStreamSynchronize(stream));
+        sync();
     }
 
     void fetch(int64_t t0, int64_t t1, double* oo, double* io) {
@@ -440,16 +542,18 @@ struct Net {
         if (n == 0 || k == 0) return;
         outT.reserve((size_t)n * k);
         if (oo) {
-            HIPC(mcr::launch_gather_steps(O.p, jbase.p, plan.p.slots, outT.p, n, t0, t1, stream));
+            HIPC(mcr::launch_gather_steps(O.p, jbase.p, in_off.p, in_list.p, false,
+                                          plan.p.slots, outT.p, n, t0, t1, stream));
             HIPC(hipMemcpyAsync(oo, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
-            HIPC(hipStreamSynchronize(stream));
+            sync();
         }
         if (io) {
-            HIPC(mcr::launch_gather_steps(I.p, jbase.p, plan.p.slots, outT.p, n, t0, t1, stream));
+            HIPC(mcr::launch_gather_steps(O.p, jbase.p, in_off.p, in_list.p, true,
+                                          plan.p.slots, outT.p, n, t0, t1, stream));
             HIPC(hipMemcpyAsync(io, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
-            HIPC(hipStreamSynchronize(stream));
+            sync();
         }
     }
 
@@ -462,10 +566,10 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_gather_series(k == 0 ? O.p : I.p, jbase.p, plan.p.slots, outT.p, n,
-                                           T_out, stream));
+            HIPC(mcr::launch_gather_series(O.p, jbase.p, in_off.p, in_list.p, k == 1,
+                                           plan.p.slots, outT.p, n, T_out, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
-            HIPC(hipStreamSynchronize(stream));
+            sync();
         }
     }
 };
@@ -594,7 +698,7 @@ int mc_net_get_info(const void* net, mc_plan_info* info) {
 int mc_net_set_stream(void* net, void* s) {
     return guarded([&] {
         Net* N = as_net(net);
-        HIPC(hipStreamSynchronize(N->stream));
+        N->sync();
         N->stream = s ? static_cast<hipStream_t>(s) : N->own;
     });
 }
@@ -653,7 +757,7 @@ int mc_simulate(void* net, int64_t T, const double* x, int64_t n_rows, const dou
 }
 
 int mc_synchronize(void* net) {
-    return guarded([&] { HIPC(hipStreamSynchronize(as_net(net)->stream)); });
+    return guarded([&] { as_net(net)->sync(); });
 }
 
 int mc_set_timing(void* net, int enable) {
@@ -677,6 +781,21 @@ int mc_reset_timing(void* net) {
     });
 }
 
+int mc_set_mode(void* net, int mode) {
+    return guarded([&] {
+        REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
+        as_net(net)->mode = mode;
+    });
+}
+
+int mc_get_mode(void* net, int* mode, int* last_path) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        if (mode) *mode = N->mode;
+        if (last_path) *last_path = N->last_path;
+    });
+}
+
 int mc_set_trace(void* net, int enable) {
     return guarded([&] { as_net(net)->trace = enable != 0; });
 }
@@ -692,19 +811,23 @@ int mc_get_trace(void* net, int64_t* out, int64_t cap, int64_t* n_records, int64
             *clock_khz = khz;
         }
         if (!out || cap <= 0 || m == 0) return;
-        std::vector<int64_t> raw(4 * (size_t)m);
-        HIPC(hipStreamSynchronize(N->stream));
+        const int W = mcr::kTraceWords;
+        std::vector<int64_t> raw(W * (size_t)m);
+        N->sync();
         HIPC(hipMemcpy(raw.data(), N->trace_buf.p, raw.size() * sizeof(int64_t),
                        hipMemcpyDeviceToHost));
-        const std::vector<int32_t>& list = N->active_list;
+        const std::vector<int32_t>& list = N->trace_wg;
         for (int64_t r = 0; r < std::min(cap, m); ++r) {
-            int64_t* o = out + 6 * r;
+            int64_t* o = out + 8 * r;
+            const int64_t* q = raw.data() + W * r;
             o[0] = N->trace_launch[r];
             o[1] = list[r];
-            o[2] = raw[4 * r];
-            o[3] = raw[4 * r + 1];
-            o[4] = raw[4 * r + 2];
-            o[5] = raw[4 * r + 3] & 0xffffffff;
+            o[2] = q[0];
+            o[3] = q[1];
+            o[4] = q[2];
+            o[5] = q[3];
+            o[6] = q[4];
+            o[7] = q[5];
         }
     });
 }

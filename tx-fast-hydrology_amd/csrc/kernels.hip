@@ -16,39 +16,33 @@
 //   q = (1 - frac) * f[ix-1] + frac * f[ix]   (or a row copy at the ends)  nutils.py:23-33
 #include "kernels.hpp"
 #include "plan.hpp"
+#include "device_common.hpp"
 
 #pragma clang fp contract(off)
+
+// Diagnostic builds only (scripts/exp_variants.sh): each MCR_EXP_* switch removes one part of the
+// tick to measure its cost.  Results of such a build are wrong by construction.
+#ifndef MCR_EXP_NO_STORES
+#define MCR_EXP_NO_STORES 0
+#endif
+#ifndef MCR_EXP_NO_OVERFLOW
+#define MCR_EXP_NO_OVERFLOW 0
+#endif
+#ifndef MCR_EXP_NO_BARRIER
+#define MCR_EXP_NO_BARRIER 0
+#endif
+#ifndef MCR_EXP_NO_Q
+#define MCR_EXP_NO_Q 0
+#endif
 
 namespace mcr {
 
 namespace {
 
-// Forcing rows a lane needs for the chunk starting at tick kc: [rb, rb + nr).  Rows are
-// non-decreasing in t (step times are increasing), so the first step's row_lo and the last
-// step's max(row_lo, row_hi) bound them.  nr = 0 when the lane has no step in the chunk.
-__device__ __forceinline__ void chunk_rows(const int4* tab, int tw0, int kc, int G, int T,
-                                           int& rb, int& nr) {
-    int ta = kc - G, tb = kc + kChunk - 1 - G;
-    if (tb < 0 || ta >= T) {
-        rb = 0;
-        nr = 0;
-        return;
-    }
-    ta = ta < 0 ? 0 : ta;
-    tb = tb >= T ? T - 1 : tb;
-    const int4 ea = tab[ta - tw0];
-    const int4 eb = tab[tb - tw0];
-    rb = ea.x;
-    nr = (eb.y > eb.x ? eb.y : eb.x) - rb + 1;
-}
-
-__device__ __forceinline__ int clamp_row(int r, int n_rows) { return r < n_rows ? r : n_rows - 1; }
-
+using dev::chunk_rows;
+using dev::clamp_row;
+using dev::lds_f64;
 constexpr int kHalf = kChunk;  // ticks whose lateral inflow is formed in one burst
-
-__device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
-    return *reinterpret_cast<const double*>(lds + byte);
-}
 
 // LDS layout of one workgroup (bytes):
 //   XB  [SLOTS + 1][2] f64  outflow of each slot at tick parity 0/1; slot SLOTS stays 0.0
@@ -91,13 +85,11 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int t_first = k0 - Gr;                        // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
     const int G = live ? Gr : (1 << 29);                // never active when not live
-    const bool from_out = real && t_first >= 1 && t_first <= T;
+    // the workgroup ran in the previous launch: its lanes' state is in the boundary buffer
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
+    const bool from_bs = k0 > gminw;
     const int64_t wb = a.wbase[w];
-    // previous step = this lane's output at tick k0 - 1 (inside its window when from_out)
-    const int64_t at_prev = from_out ? wb + (int64_t)(k0 - 1 - gminw) * SLOTS + tid : 0;
-    const double o_ld = a.O[at_prev];
-    const double i_ld = a.I[at_prev];
+    const double2 bs = reinterpret_cast<const double2*>(a.BS)[from_bs ? d : 0];
     const double st_o = a.st_o[d], st_i = a.st_i[d];
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
     const int cnt = live ? a.up_cnt[d] : 0;
@@ -152,8 +144,8 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int ngrp = live ? (more_end - more) / kUpGroup : 0;       // this lane's groups
     const unsigned gofs = XM + (unsigned)(kUpGroup + more) * 4;       // its first group
 
-    double op = from_out ? o_ld : st_o;
-    double ip = from_out ? i_ld : st_i;
+    double op = from_bs ? bs.x : st_o;
+    double ip = from_bs ? bs.y : st_i;
     // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
     xbp[tid * 2 + ((k0 - 1) & 1)] = op;
     if (tid < 2) xbp[SLOTS * 2 + tid] = 0.0;            // zero slot for unused upstream codes
@@ -175,6 +167,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const bool any3 = __any(cnt > 2);                   // wave-uniform
     int ngw = 0;                                        // overflow groups of the wave
     while (__any(ngw < ngrp)) ++ngw;
+    if (MCR_EXP_NO_OVERFLOW) ngw = 0;
     const unsigned own = XB + (unsigned)tid * 16;
 
     // forcing rows of the first chunk
@@ -185,6 +178,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
     __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
+    const int64_t c_loop = a.trace ? clock64() : 0;
 
     const int wend = gmaxw + T;                         // end of this workgroup's window
     // feeds another cluster: step t also goes to XS[xsid][t] (address at tick k: xs0 + k)
@@ -228,7 +222,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                 }
                 const double fr = __hiloint2double(e.w, e.z);
                 const double qi = (1.0 - fr) * flo + fr * fhi;
-                qv[j] = e.y < 0 ? flo : qi;
+                qv[j] = MCR_EXP_NO_Q ? 0.0 : (e.y < 0 ? flo : qi);
             }
             if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
 #pragma unroll
@@ -276,11 +270,11 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                 const bool inwin = k >= gminw && k < wend;
                 const int64_t row = inwin ? wb + (int64_t)(k - gminw) * SLOTS : 0;
                 double* orow = inwin ? a.O + row : a.dummy;
-                double* irow = inwin ? a.I + row : a.dummy + SLOTS;
-                orow[tid] = routed ? ov : 0.0;
-                irow[tid] = I;
-                if (xsrc && act) a.XS[xs0 + k] = ov;
-                __syncthreads();
+                if (!MCR_EXP_NO_STORES) {
+                    orow[tid] = routed ? ov : 0.0;
+                    if (xsrc && act) a.XS[xs0 + k] = ov;
+                }
+                if (!MCR_EXP_NO_BARRIER) __syncthreads();
             }
         }
         rb = rbn;
@@ -289,12 +283,17 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         f1 = g1;
         f2 = g2;
     }
+    // state for the next launch of this workgroup (lanes that did not run keep theirs)
+    reinterpret_cast<double2*>(a.BS)[d] = make_double2(op, ip);
     if (a.trace && tid == 0) {
-        int64_t* rec = a.trace + 4 * (int64_t)blockIdx.x;
+        const int64_t c_end = clock64();
+        int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
         rec[0] = t_start;
         rec[1] = t_loop;
         rec[2] = wall_clock64();
-        rec[3] = (int64_t)__smid() | ((int64_t)w << 32);
+        rec[3] = (int64_t)__smid();
+        rec[4] = c_loop;
+        rec[5] = c_end;
     }
 }
 
@@ -340,43 +339,59 @@ __global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __r
 }
 
 
-__global__ void final_state(const double* __restrict__ O, const double* __restrict__ I,
-                            double* __restrict__ st_o, double* __restrict__ st_i,
-                            const int64_t* __restrict__ jbase,
-                            const int64_t* __restrict__ slot_reach, int64_t nslots, int slots,
+// inflow of caller reach j at step t: ((0 + o[u1][t]) + o[u2][t]) + ...  (reference order)
+__device__ __forceinline__ double inflow_at(const double* __restrict__ O,
+                                            const int64_t* __restrict__ jbase,
+                                            const int64_t* __restrict__ in_off,
+                                            const int64_t* __restrict__ in_list, int64_t j,
+                                            int64_t t, int slots) {
+    double s = 0.0;
+    for (int64_t k = in_off[j]; k < in_off[j + 1]; ++k) s = s + O[jbase[in_list[k]] + t * slots];
+    return s;
+}
+
+__global__ void final_state(const double* __restrict__ O, double* __restrict__ st_o,
+                            double* __restrict__ st_i, const int64_t* __restrict__ jbase,
+                            const int64_t* __restrict__ slot_reach,
+                            const int64_t* __restrict__ in_off,
+                            const int64_t* __restrict__ in_list, int64_t nslots, int slots,
                             int64_t T) {
     for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < nslots;
          d += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = slot_reach[d];
         if (j >= 0) {
-            const int64_t at = jbase[j] + (T - 1) * slots;
-            st_o[d] = O[at];
-            st_i[d] = I[at];
+            st_o[d] = O[jbase[j] + (T - 1) * slots];
+            st_i[d] = inflow_at(O, jbase, in_off, in_list, j, T - 1, slots);
         }
     }
 }
 
 // out[t - t0][j]: consecutive threads take consecutive j (coalesced writes, gathered reads)
-__global__ void gather_steps(const double* __restrict__ S, const int64_t* __restrict__ jbase,
-                             int slots, double* __restrict__ out, int64_t n, int64_t t0,
-                             int64_t t1) {
+__global__ void gather_steps(const double* __restrict__ O, const int64_t* __restrict__ jbase,
+                             const int64_t* __restrict__ in_off,
+                             const int64_t* __restrict__ in_list, bool inflow, int slots,
+                             double* __restrict__ out, int64_t n, int64_t t0, int64_t t1) {
     const int64_t total = n * (t1 - t0);
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = x / n;
         const int64_t j = x - t * n;
-        out[x] = S[jbase[j] + (t0 + t) * slots];
+        out[x] = inflow ? inflow_at(O, jbase, in_off, in_list, j, t0 + t, slots)
+                        : O[jbase[j] + (t0 + t) * slots];
     }
 }
 
-__global__ void gather_series(const double* __restrict__ S, const int64_t* __restrict__ jbase,
-                              int slots, double* __restrict__ out, int64_t n, int64_t T) {
+__global__ void gather_series(const double* __restrict__ O, const int64_t* __restrict__ jbase,
+                              const int64_t* __restrict__ in_off,
+                              const int64_t* __restrict__ in_list, bool inflow, int slots,
+                              double* __restrict__ out, int64_t n, int64_t T) {
     const int64_t total = n * T;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = x / T;
         const int64_t t = x - j * T;
-        out[x] = S[jbase[j] + t * slots];
+        out[x] = inflow ? inflow_at(O, jbase, in_off, in_list, j, t, slots)
+                        : O[jbase[j] + t * slots];
     }
 }
 
@@ -392,11 +407,10 @@ inline int grid_for(int64_t work, int block) {
 template <bool DENSE>
 hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, size_t lds, hipStream_t s) {
     switch (slots) {
-        case 64: hipLaunchKernelGGL((wavefront_det<64, DENSE>), grid, 64, lds, s, a); break;
-        case 128: hipLaunchKernelGGL((wavefront_det<128, DENSE>), grid, 128, lds, s, a); break;
-        case 256: hipLaunchKernelGGL((wavefront_det<256, DENSE>), grid, 256, lds, s, a); break;
-        case 512: hipLaunchKernelGGL((wavefront_det<512, DENSE>), grid, 512, lds, s, a); break;
-        case 1024: hipLaunchKernelGGL((wavefront_det<1024, DENSE>), grid, 1024, lds, s, a); break;
+#define MCR_CASE(S) \
+    case S: hipLaunchKernelGGL((wavefront_det<S, DENSE>), grid, S, lds, s, a); break;
+        MCR_SLOT_LIST(MCR_CASE)
+#undef MCR_CASE
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -437,27 +451,30 @@ hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32
     return hipGetLastError();
 }
 
-hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,
-                              const int64_t* jbase, const int64_t* slot_reach, int64_t nslots,
-                              int slots, int64_t T, hipStream_t s) {
-    hipLaunchKernelGGL(final_state, grid_for(nslots, 256), 256, 0, s, O, I, st_o, st_i, jbase,
-                       slot_reach, nslots, slots, T);
+hipError_t launch_final_state(const double* O, double* st_o, double* st_i, const int64_t* jbase,
+                              const int64_t* slot_reach, const int64_t* in_off,
+                              const int64_t* in_list, int64_t nslots, int slots, int64_t T,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(final_state, grid_for(nslots, 256), 256, 0, s, O, st_o, st_i, jbase,
+                       slot_reach, in_off, in_list, nslots, slots, T);
     return hipGetLastError();
 }
 
-hipError_t launch_gather_steps(const double* S, const int64_t* jbase, int slots, double* out,
+hipError_t launch_gather_steps(const double* O, const int64_t* jbase, const int64_t* in_off,
+                               const int64_t* in_list, bool inflow, int slots, double* out,
                                int64_t n, int64_t t0, int64_t t1, hipStream_t s) {
     if (n <= 0 || t1 <= t0) return hipSuccess;
-    hipLaunchKernelGGL(gather_steps, grid_for(n * (t1 - t0), 256), 256, 0, s, S, jbase, slots,
-                       out, n, t0, t1);
+    hipLaunchKernelGGL(gather_steps, grid_for(n * (t1 - t0), 256), 256, 0, s, O, jbase, in_off,
+                       in_list, inflow, slots, out, n, t0, t1);
     return hipGetLastError();
 }
 
-hipError_t launch_gather_series(const double* S, const int64_t* jbase, int slots, double* out,
+hipError_t launch_gather_series(const double* O, const int64_t* jbase, const int64_t* in_off,
+                                const int64_t* in_list, bool inflow, int slots, double* out,
                                 int64_t n, int64_t T, hipStream_t s) {
     if (n <= 0 || T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_series, grid_for(n * T, 256), 256, 0, s, S, jbase, slots, out, n,
-                       T);
+    hipLaunchKernelGGL(gather_series, grid_for(n * T, 256), 256, 0, s, O, jbase, in_off, in_list,
+                       inflow, slots, out, n, T);
     return hipGetLastError();
 }
 

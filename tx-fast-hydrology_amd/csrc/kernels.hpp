@@ -4,7 +4,9 @@
 // Output layout ("workgroup windows").  Workgroup w owns the ticks [gmin[w], gmax[w] + T) of the
 // space-time schedule; its outputs are stored tick-major inside that window:
 //     O[wbase[w] + (tick - gmin[w]) * SLOTS + lane]
-// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  A reach that feeds a
+// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  Inflows are not stored:
+// i[j][t] = ((0 + o[u1][t]) + o[u2][t]) + ... over j's inflow list (plan.hpp) is recomputed
+// bit-exactly wherever it is needed (fetches, final state).  A reach that feeds a
 // reach of another cluster (an "external input" of the consumer's workgroup) also writes its
 // outflow to a step-contiguous stream XS[e][t], which the consumer reads coalesced.  Step t of the reach in
 // slot d = w * SLOTS + lane lives at tick G[d] + t, i.e. at  jbase[j] + t * SLOTS  for its caller
@@ -17,9 +19,23 @@
 
 namespace mcr {
 
+// Workgroup sizes (plan slots) the kernels are instantiated for.
+#define MCR_SLOT_LIST(X) X(64) X(128) X(192) X(256) X(384) X(448) X(512) X(1024)
+
 // Ticks whose lateral inflow is formed in one burst (and whose forcing rows are prefetched
 // together).  Launch lengths (`tile`) are multiples of it.
 constexpr int kChunk = 8;
+
+// Dataflow kernel (flow.hip): external inputs per workgroup it supports, longest step table it
+// keeps in LDS, minimum cross-cluster slack (the helper stages the next chunk, so producers must
+// be more than one chunk ahead of it).
+constexpr int kFlowMaxExt = 128;
+constexpr int kFlowMaxT = 1024;
+constexpr int kFlowMinSlack = 2 * kChunk;
+
+// launch trace record of one workgroup: wall clock at start / loop start / end, hw id, shader
+// clock at loop start / end
+constexpr int kTraceWords = 6;
 
 // Everything the wavefront kernel reads, by value.  Per-slot arrays are in device-slot order
 // (plan.hpp).
@@ -45,11 +61,16 @@ struct WaveArgs {
     const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
     const int32_t* wg_gmax;
     const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
-    double* O;                    // workgroup windows (see above)
-    double* I;
+    double* O;                    // workgroup windows of outflows (see above)
+    double* BS;                   // [nslots][2] {o, i} of each slot at the end of a launch
     double* XS;                   // external-input streams [n_ext][T]: step t of each source
-    double* dummy;                // >= 2 * 1024 doubles: target of out-of-window ticks
-    int64_t* trace;               // optional launch trace, 4 words per workgroup (NULL = off)
+    double* dummy;                // >= 2 * 1024 doubles: cells of out-of-window ticks
+    int64_t* trace;               // optional launch trace, kTraceWords per workgroup (NULL = off)
+    // dataflow kernel (flow.hip) only
+    uint32_t* XG;                 // external-input granules [n_ext][T] x {lo, epoch, hi, epoch}
+    uint32_t xg_bytes;            // size of XG in bytes (< 2^31)
+    uint32_t epoch;               // tag of this run's granules (never 0)
+    int32_t* status;              // set to 1 when a wait gave up
     int64_t nslots;
     int32_t n_rows;
     int32_t T;
@@ -65,6 +86,17 @@ inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int til
     return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)table_cap +
            8 * (size_t)ext_cap * tile + 4 * ((size_t)more_cap + 4);
 }
+
+inline size_t flow_lds_bytes(int slots, int T, int ext_cap, int more_cap) {
+    return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)T +
+           2 * (size_t)ext_cap * kChunk * 8 + 4 * ((size_t)more_cap + 4) + 4 * kFlowMaxExt;
+}
+
+// One launch for the whole horizon; grid = every workgroup (all must be co-resident).
+hipError_t launch_flow(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
+                       hipStream_t s);
+// Resident workgroups per CU of the dataflow kernel at this LDS size.
+hipError_t flow_occupancy(int slots, bool dense, size_t lds_bytes, int* blocks_per_cu);
 
 // dense: the step table has a kChunk-step window spanning more than 3 forcing rows
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
@@ -83,15 +115,20 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
                                const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
                                hipStream_t s);
-// state after the last step: st[d] = step T-1 of slot d
-hipError_t launch_final_state(const double* O, const double* I, double* st_o, double* st_i,
-                              const int64_t* jbase, const int64_t* slot_reach, int64_t nslots,
-                              int slots, int64_t T, hipStream_t s);
-// out[t - t0][j] = S[jbase[j] + t * slots]  for t in [t0, t1)   (step-major, caller order)
-hipError_t launch_gather_steps(const double* S, const int64_t* jbase, int slots, double* out,
+// state after the last step: st[d] = step T-1 of slot d (inflow recomputed from O)
+hipError_t launch_final_state(const double* O, double* st_o, double* st_i, const int64_t* jbase,
+                              const int64_t* slot_reach, const int64_t* in_off,
+                              const int64_t* in_list, int64_t nslots, int slots, int64_t T,
+                              hipStream_t s);
+// Output gathers (caller order).  inflow = false: out = O[jbase[j] + t * slots];  inflow = true:
+// out = the inflow of reach j at step t, summed from O over its inflow list.
+// step-major out[t - t0][j] for t in [t0, t1)
+hipError_t launch_gather_steps(const double* O, const int64_t* jbase, const int64_t* in_off,
+                               const int64_t* in_list, bool inflow, int slots, double* out,
                                int64_t n, int64_t t0, int64_t t1, hipStream_t s);
-// out[j][t] = S[jbase[j] + t * slots]  for t in [0, T)   (reach-major, caller order)
-hipError_t launch_gather_series(const double* S, const int64_t* jbase, int slots, double* out,
+// reach-major out[j][t] for t in [0, T)
+hipError_t launch_gather_series(const double* O, const int64_t* jbase, const int64_t* in_off,
+                                const int64_t* in_list, bool inflow, int slots, double* out,
                                 int64_t n, int64_t T, hipStream_t s);
 
 }  // namespace mcr

@@ -91,6 +91,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (int64_t s : order)  // rank order -> each list sorted by rank
             if (endnodes[s] != s) up_list[fill[endnodes[s]]++] = s;
     }
+    P.in_off = up_off;   // kept: inflows are recomputed from outflows on the device
+    P.in_list = up_list;
     for (int64_t s : order) {
         const int64_t e = endnodes[s];
         if (e != s && P.rank[e] >= 0 && P.rank[e] < P.rank[s]) {

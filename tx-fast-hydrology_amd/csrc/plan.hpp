@@ -64,6 +64,9 @@ struct Plan {
 
     // replay of the reference walk (original reach order)
     std::vector<int64_t> rank;     // -1 if never processed
+    // inflow lists: routed upstream reaches of each reach in finalisation (rank) order, i.e.
+    // i[j] = ((0 + o[in_list[in_off[j]]]) + ...) exactly as the reference accumulates it
+    std::vector<int64_t> in_off, in_list;
 
     // per device slot d in [0, nslots)
     std::vector<int64_t> slot_reach;   // original reach index, -1 for padding

@@ -204,15 +204,29 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
+    MODES = {"auto": 0, "launches": 1, "dataflow": 2}
+
+    def set_mode(self, mode: str):
+        """Execution path: "auto" (default), "launches" or "dataflow" (see mcroute.h)."""
+        nat.check(nat.lib().mc_set_mode(self._h, self.MODES[mode]))
+
+    def mode(self) -> tuple:
+        """(requested mode, path of the last run: "launches" / "dataflow" / None)."""
+        m = ctypes.c_int()
+        p = ctypes.c_int()
+        nat.check(nat.lib().mc_get_mode(self._h, ctypes.byref(m), ctypes.byref(p)))
+        names = {v: k for k, v in self.MODES.items()}
+        return names[m.value], {1: "launches", 2: "dataflow"}.get(p.value)
+
     def set_trace(self, enable: bool):
         nat.check(nat.lib().mc_set_trace(self._h, 1 if enable else 0))
 
     def trace(self) -> tuple:
-        """Launch trace of the last run: (records [m, 6] int64, clock_khz); see mcroute.h."""
+        """Launch trace of the last run: (records [m, 8] int64, clock_khz); see mcroute.h."""
         m = ctypes.c_int64()
         khz = ctypes.c_int64()
         nat.check(nat.lib().mc_get_trace(self._h, None, 0, ctypes.byref(m), ctypes.byref(khz)))
-        out = np.zeros((m.value, 6), dtype=np.int64)
+        out = np.zeros((m.value, 8), dtype=np.int64)
         nat.check(nat.lib().mc_get_trace(self._h, out.ctypes.data_as(ctypes.c_void_p), m.value,
                                          ctypes.byref(m), ctypes.byref(khz)))
         return out, khz.value
