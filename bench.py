@@ -44,12 +44,29 @@ def parse():
     ap.add_argument("--depth", type=int, default=1500)
     ap.add_argument("--T", type=int, default=288)
     ap.add_argument("--dt", type=float, default=300.0)
-    ap.add_argument("--slots", type=int, default=0)
+    # 448 lanes + the helper wave: the whole Texas network is one resident dataflow launch
+    ap.add_argument("--slots", type=int, default=448)
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-runs", type=int, default=3)
     return ap.parse_args()
+
+
+def measured_traffic(info, n, T):
+    """HBM bytes per launch of the routing kernel measured with rocprofv3 PMC counters for this
+    exact workload (scripts/hbm_traffic.py -> profiles/*_hbm_traffic.json), newest first."""
+    import glob
+    want = {"slots": info["slots"], "tile": info["tile"], "n": n, "T": T}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
+        try:
+            rec = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if rec.get("workload") == want:
+            rec["file"] = os.path.relpath(f, ROOT)
+            return rec
+    return None
 
 
 def build_workload(args, rank=0):
@@ -143,8 +160,11 @@ def main():
     launch_ms = tm["kernel_ms"] / max(tm["launches"], 1)
     bytes_per_launch = BYTES_PER_UNIT * n * args.T * args.timing_runs / max(tm["launches"], 1)
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+    traffic = measured_traffic(info, n, args.T)
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                "traffic_source": traffic["file"] if traffic else None,
                 "kernel": "wavefront_flow" if net.mode()[1] == "dataflow" else "wavefront_det",
                 "launches_per_step": tm["launches"] / args.timing_runs,
                 "avg_launch_us": round(launch_ms * 1e3, 3),

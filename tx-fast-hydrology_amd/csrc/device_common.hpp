@@ -27,7 +27,10 @@ __device__ __forceinline__ void chunk_rows(const int4* tab, int tw0, int kc, int
     nr = (eb.y > eb.x ? eb.y : eb.x) - rb + 1;
 }
 
-__device__ __forceinline__ int clamp_row(int r, int n_rows) { return r < n_rows ? r : n_rows - 1; }
+// forcing row index clamped into [0, n_rows): rows of inactive ticks may be arbitrary
+__device__ __forceinline__ int clamp_row(int r, int n_rows) {
+    return r < 0 ? 0 : (r < n_rows ? r : n_rows - 1);
+}
 
 __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
     return *reinterpret_cast<const double*>(lds + byte);
