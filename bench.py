@@ -44,8 +44,11 @@ def parse():
     ap.add_argument("--depth", type=int, default=1500)
     ap.add_argument("--T", type=int, default=288)
     ap.add_argument("--dt", type=float, default=300.0)
-    # 448 lanes + the helper wave: the whole Texas network is one resident dataflow launch
-    ap.add_argument("--slots", type=int, default=448)
+    # 0 = per workload: 448 lanes + the helper wave make the deterministic Texas network one
+    # resident dataflow launch; ensembles run the multi-launch path at 256
+    ap.add_argument("--slots", type=int, default=0)
+    ap.add_argument("--members", type=int, default=1,
+                    help="ensemble members (BASELINE configs[2]: 64); 1 = deterministic")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -87,19 +90,23 @@ def build_workload(args, rank=0):
     beta = (dt + 2 * K * X) / (2 * K * (1 - X) + dt)
     chi = (2 * K * (1 - X) - dt) / (2 * K * (1 - X) + dt)
     gamma = dt / (K * (1 - X) + dt / 2)
-    i0 = np.zeros(n)
-    np.add.at(i0, end, o0)                                      # muskingum.py:416-417
     rows = int(np.ceil(args.T * dt / 3600.0)) + 1
     xp_ns, fp = synthetic.forcing(n, rows=rows, seed=1 + rank)
     xp = xp_ns.astype(float)
     x = xp[0] + dt * 1e9 * np.arange(1, args.T + 1)
+    E = args.members
+    if E > 1:
+        o0, fp = synthetic.ensemble(o0, fp, E, seed=5 + 7 * rank)
+    i0 = np.zeros(o0.shape)
+    np.add.at(i0, end, o0)                                      # muskingum.py:416-417
 
-    net = engine.RoutingNet(end, indeg, heads, slots=args.slots, tile=args.tile)
+    slots = args.slots or (448 if E == 1 else 256)
+    net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=args.tile, members=E)
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
     w = SimpleNamespace(n=n, start=start, end=end, indeg=indeg, alpha=alpha, beta=beta, chi=chi,
-                        gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt)
+                        gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt, E=E)
     return net, w
 
 
@@ -146,7 +153,8 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    units = float(n) * args.T * args.steps * world
+    E = wl.E
+    units = float(n) * E * args.T * args.steps * world
     value = units / elapsed
 
     # ---- roofline of the dominant kernel (HIP events around every wavefront launch) --------
@@ -158,9 +166,11 @@ def main():
     tm = net.timing()
     net.set_timing(False)
     launch_ms = tm["kernel_ms"] / max(tm["launches"], 1)
-    bytes_per_launch = BYTES_PER_UNIT * n * args.T * args.timing_runs / max(tm["launches"], 1)
+    # 72 B per reach·timestep deterministic, 40 + 32/E per reach·member·timestep
+    per_unit = BYTES_PER_UNIT if E == 1 else 40.0 + 32.0 / E
+    bytes_per_launch = per_unit * n * E * args.T * args.timing_runs / max(tm["launches"], 1)
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-    traffic = measured_traffic(info, n, args.T)
+    traffic = measured_traffic(info, n, args.T) if E == 1 else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
@@ -172,7 +182,27 @@ def main():
 
     # ---- CPU baseline (serial transliteration of the reference loop, rank 0 at N=1) --------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and E > 1:
+        # E independent member runs over the host cores the box gives this job (OpenMP)
+        cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+        ms = min(E, cores)
+        o_s = np.ascontiguousarray(wl.o0[:, :ms])
+        i_s = np.ascontiguousarray(wl.i0[:, :ms])
+        fps = np.ascontiguousarray(wl.fp[:, :, :ms])
+        reps, t_cpu = 0, 0.0
+        while t_cpu < args.cpu_seconds or reps == 0:
+            c0 = time.perf_counter()
+            o_s, i_s = orc.simulate_members(wl.start, wl.end, wl.indeg, wl.alpha, wl.beta,
+                                            wl.chi, wl.gamma, o_s, i_s, x, wl.xp, fps,
+                                            threads=cores)
+            t_cpu += time.perf_counter() - c0
+            reps += 1
+        cpu = {"value": float(n) * ms * args.T * reps / t_cpu,
+               "unit": "reach·member·timesteps/s", "cores": cores, "kind": "port",
+               "sample": f"{reps} x full 24 h horizon (T={args.T}) of {ms} members on the same "
+                         f"{n}-reach network, C member loop (-O3 -ffp-contract=off, OpenMP "
+                         f"over members), {t_cpu:.1f} s"}
+    elif rank == 0 and world == 1 and not args.no_cpu:
         o_s, i_s = wl.o0.copy(), wl.i0.copy()
         reps, t_cpu = 0, 0.0
         while t_cpu < args.cpu_seconds or reps == 0:
@@ -190,7 +220,7 @@ def main():
         line = {
             "metric": METRIC,
             "value": value,
-            "unit": "reach·timesteps/s",
+            "unit": "reach·timesteps/s" if E == 1 else "reach·member·timesteps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -200,8 +230,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "texas-det (BASELINE configs[1]): full-Texas synthetic "
-                                   "network, deterministic, 24 h @ 300 s",
+            "config": {"workload": ("texas-det (BASELINE configs[1]): full-Texas synthetic "
+                                    "network, deterministic, 24 h @ 300 s") if E == 1 else
+                                   (f"texas-ens{E} (BASELINE configs[2]): full-Texas synthetic "
+                                    f"network, {E}-member ensemble forecast, 24 h @ 300 s"),
+                       "members": E,
                        "n_reaches": n, "outlets": int((wl.end == wl.start).sum()),
                        "max_height": info["max_height"], "T": args.T, "dt_s": wl.dt,
                        "forcing_rows": wl.rows, "parallelism": f"replicas x{world}",

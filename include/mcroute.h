@@ -105,6 +105,16 @@ int mc_net_destroy(void* net);
 int mc_net_get_info(const void* net, mc_plan_info* info);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the session's own. */
 int mc_net_set_stream(void* net, void* hip_stream);
+/* Ensemble members (default 1).  With E > 1 every per-reach array passed to or returned by
+ * mc_set_state, mc_get_state, mc_step (o/i/q) is [n][E] (member innermost), the forcing of
+ * mc_load_forcing / mc_simulate is [n_rows][n][E], mc_fetch_outputs returns [t][n][E] and
+ * mc_fetch_series [n][T][E].  Members share topology and coefficients (each member
+ * is an independent deterministic run with its own forcing and initial state).  Setting the
+ * member count zeroes the state and drops loaded forcing and outputs.  Ensembles always run the
+ * multi-launch path. */
+int mc_net_set_members(void* net, int64_t members);
+int mc_net_get_members(const void* net, int64_t* members);
+
 
 /* Coefficients alpha, beta, chi, gamma (muskingum.py:332-360), caller order. */
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,

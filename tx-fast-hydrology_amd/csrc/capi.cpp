@@ -176,6 +176,11 @@ struct Net {
     double kernel_ms = 0.0, run_ms = 0.0;
     int64_t launches = 0;
     std::vector<hipEvent_t> events;
+    // ensemble members (mc_net_set_members): per-member arrays are member-major on the device
+    int64_t E = 1;
+    int64_t Otot = 0;              // output cells of one member (window sizes summed)
+    int64_t sched_E = 0;
+
     // dataflow kernel (flow.hip): mode 0 = automatic, 1 = multi-launch only, 2 = dataflow only
     int mode = 0;
     int last_path = 0;             // 1 multi-launch, 2 dataflow (path of the last run)
@@ -237,7 +242,7 @@ struct Net {
             HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
         }
         stage.reserve(std::max<int64_t>(plan.n, 1));
-        dummy.reserve(2 * 1024);
+        dummy.reserve(mcr::kDummyPerMember);
         HIPC(hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device));
         {
             std::vector<int32_t> ids(std::max<int32_t>(plan.nwg, 1));
@@ -286,18 +291,39 @@ struct Net {
         return ok;
     }
 
-    // caller-order host array -> slot-order device array
-    void to_slots(const double* host, DBuf<double>& dst) {
+    // caller-order host array [n][m] -> member-major slot-order device array [m][nslots]
+    void to_slots(const double* host, DBuf<double>& dst, int64_t m = 1) {
         const int64_t n = plan.n;
         if (n == 0) return;
-        HIPC(hipMemcpyAsync(stage.p, host, n * sizeof(double), hipMemcpyHostToDevice, stream));
-        HIPC(mcr::launch_scatter_to_slots(stage.p, dst.p, slot_reach.p, plan.nslots, stream));
+        stage.reserve((size_t)(n * m));
+        HIPC(hipMemcpyAsync(stage.p, host, n * m * sizeof(double), hipMemcpyHostToDevice,
+                            stream));
+        HIPC(mcr::launch_scatter_to_slots(stage.p, dst.p, slot_reach.p, plan.nslots, m, stream));
     }
-    void from_slots(const DBuf<double>& src, double* host) {
+    void from_slots(const DBuf<double>& src, double* host, int64_t m = 1) {
         const int64_t n = plan.n;
         if (n == 0) return;
-        HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, stream));
-        HIPC(hipMemcpyAsync(host, stage.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+        stage.reserve((size_t)(n * m));
+        HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, plan.nslots, m, stream));
+        HIPC(hipMemcpyAsync(host, stage.p, n * m * sizeof(double), hipMemcpyDeviceToHost,
+                            stream));
+        sync();
+    }
+
+    void set_members(int64_t m) {
+        REQUIRE(m >= 1 && m <= 65535, "members must be in [1, 65535]");
+        sync();
+        E = m;
+        const size_t ns = (size_t)std::max<int64_t>(plan.nslots, 1);
+        for (DBuf<double>* b : {&st_o, &st_i}) {
+            b->reserve(ns * m);
+            HIPC(hipMemsetAsync(b->p, 0, ns * m * sizeof(double), stream));
+        }
+        BS.reserve(2 * ns * m);
+        dummy.reserve(mcr::kDummyPerMember * m);
+        n_rows = 0;                    // forcing and outputs are per member: load again
+        T_out = 0;
+        sched_T = -1;
         sync();
     }
 
@@ -313,15 +339,15 @@ struct Net {
 
     void set_state(const double* o, const double* i) {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
-        to_slots(o, st_o);
+        to_slots(o, st_o, E);
         sync();
-        to_slots(i, st_i);
+        to_slots(i, st_i, E);
         sync();
     }
 
     // Per-horizon layout: active workgroups of every launch and the output windows.
     void ensure_schedule(int64_t T) {
-        if (sched_T == T) return;
+        if (sched_T == T && sched_E == E) return;
         std::vector<int32_t>& list = active_list;
         mcr::active_schedule(plan, T, list, sched_off);
         active.upload(list.data(), list.size(), stream);
@@ -332,13 +358,15 @@ struct Net {
             total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * plan.p.slots;
         }
         wbase.upload(wb.data(), wb.size(), stream);
-        O.reserve((size_t)total);
+        Otot = total;
+        O.reserve((size_t)(total * E));
         jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
-        XS.reserve(std::max<size_t>(plan.ext_src.size() * (size_t)T, 1));
+        XS.reserve(std::max<size_t>(plan.ext_src.size() * (size_t)T * E, 1));
         HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, wbase.p, plan.p.slots, plan.n,
                                       jbase.p, stream));
         sync();
         sched_T = T;
+        sched_E = E;
     }
 
     void ensure_events(size_t k) {
@@ -405,11 +433,17 @@ struct Net {
         a.tile = plan.p.tile;
         a.ext_cap = plan.max_ext_wg;
         a.more_cap = more_cap;
+        a.mF = rows * plan.nslots;
+        a.mO = Otot;
+        a.mX = (int64_t)plan.ext_src.size() * T;
+        a.mS = plan.nslots;
         int64_t launched = 0;
         trace_launch.clear();
         trace_wg.clear();
         size_t flds = 0;
-        if (flow_fits(T, dense, flds)) {
+        if (E > 1 && mode == 2)
+            throw Fail(MC_E_STATE, "dataflow mode routes one member; ensembles use launches");
+        if (E == 1 && flow_fits(T, dense, flds)) {
             // ---- one dataflow launch for the whole horizon (flow.hip)
             const size_t words = plan.ext_src.size() * (size_t)T * 4;
             if (words > xg_words || epoch == 0xffffffffu) {
@@ -457,14 +491,14 @@ struct Net {
             }
             a.kappa0 = (int32_t)(k * plan.p.tile);
             if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, dense, stream));
+            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, dense, (int)E, stream));
             if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
             ++launched;
             last_path = 1;
         }
-        HIPC(mcr::launch_final_state(O.p, st_o.p, st_i.p, jbase.p, slot_reach.p, in_off.p,
-                                     in_list.p,
-                                     plan.nslots, plan.p.slots, T, stream));
+        HIPC(mcr::launch_final_state(O.p, Otot, st_o.p, st_i.p, jbase.p, slot_reach.p,
+                                     in_off.p, in_list.p, plan.nslots, plan.p.slots, T, E,
+                                     stream));
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
             HIPC(hipEventSynchronize(events[2 * nl + 1]));
@@ -489,11 +523,11 @@ struct Net {
         const int64_t n = plan.n;
         xp.assign(xps, xps + rows);
         n_rows = rows;
-        F.reserve((size_t)rows * plan.nslots);
+        F.reserve((size_t)(rows * plan.nslots * E));
         if (n == 0) return;
         DBuf<double> tmp;
-        tmp.upload(fp, (size_t)rows * n, stream);
-        HIPC(mcr::launch_forcing_to_slots(tmp.p, F.p, slot_reach.p, n, plan.nslots, rows,
+        tmp.upload(fp, (size_t)(rows * n * E), stream);
+        HIPC(mcr::launch_forcing_to_slots(tmp.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
                                           stream));
         sync();
     }
@@ -524,12 +558,12 @@ struct Net {
     void step(const double* q, double* i_out, double* o_out) {
         REQUIRE(plan.n == 0 || (q && i_out && o_out), "q/outputs must not be NULL");
         const int64_t n = plan.n;
-        Fstep.reserve(std::max<int64_t>(plan.nslots, 1));
-        if (n) to_slots(q, Fstep);
+        Fstep.reserve((size_t)(std::max<int64_t>(plan.nslots, 1) * E));
+        if (n) to_slots(q, Fstep, E);
         run_tables(1, Fstep.p, 1, std::vector<int4>(1, step_entry(0, -1, 0.0)));
         if (n) {  // the new state is the output of the step
-            from_slots(st_o, o_out);
-            from_slots(st_i, i_out);
+            from_slots(st_o, o_out, E);
+            from_slots(st_i, i_out, E);
         }
         sync();
     }
@@ -540,18 +574,13 @@ struct Net {
         const int64_t n = plan.n;
         const int64_t k = t1 - t0;
         if (n == 0 || k == 0) return;
-        outT.reserve((size_t)n * k);
-        if (oo) {
-            HIPC(mcr::launch_gather_steps(O.p, jbase.p, in_off.p, in_list.p, false,
-                                          plan.p.slots, outT.p, n, t0, t1, stream));
-            HIPC(hipMemcpyAsync(oo, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
-                                stream));
-            sync();
-        }
-        if (io) {
-            HIPC(mcr::launch_gather_steps(O.p, jbase.p, in_off.p, in_list.p, true,
-                                          plan.p.slots, outT.p, n, t0, t1, stream));
-            HIPC(hipMemcpyAsync(io, outT.p, n * k * sizeof(double), hipMemcpyDeviceToHost,
+        outT.reserve((size_t)(n * k * E));
+        for (int c = 0; c < 2; ++c) {
+            double* dst = c == 0 ? oo : io;
+            if (!dst) continue;
+            HIPC(mcr::launch_gather_steps(O.p, Otot, jbase.p, in_off.p, in_list.p, c == 1,
+                                          plan.p.slots, outT.p, n, t0, t1, E, stream));
+            HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             sync();
         }
@@ -561,13 +590,13 @@ struct Net {
         REQUIRE(T_out > 0, "no outputs: call mc_run first");
         const int64_t n = plan.n;
         if (n == 0) return;
-        outT.reserve((size_t)n * T_out);
-        const size_t bytes = (size_t)n * T_out * sizeof(double);
+        outT.reserve((size_t)(n * T_out * E));
+        const size_t bytes = (size_t)(n * T_out * E) * sizeof(double);
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_gather_series(O.p, jbase.p, in_off.p, in_list.p, k == 1,
-                                           plan.p.slots, outT.p, n, T_out, stream));
+            HIPC(mcr::launch_gather_series(O.p, Otot, jbase.p, in_off.p, in_list.p, k == 1,
+                                           plan.p.slots, outT.p, n, T_out, E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             sync();
         }
@@ -703,6 +732,17 @@ int mc_net_set_stream(void* net, void* s) {
     });
 }
 
+int mc_net_set_members(void* net, int64_t members) {
+    return guarded([&] { as_net(net)->set_members(members); });
+}
+
+int mc_net_get_members(const void* net, int64_t* members) {
+    return guarded([&] {
+        REQUIRE(net && members, "null argument");
+        *members = static_cast<const Net*>(net)->E;
+    });
+}
+
 int mc_set_coeffs(void* net, const double* a, const double* b, const double* c,
                   const double* g) {
     return guarded([&] { as_net(net)->set_coeffs(a, b, c, g); });
@@ -716,8 +756,8 @@ int mc_get_state(void* net, double* o, double* i) {
     return guarded([&] {
         Net* N = as_net(net);
         REQUIRE(N->plan.n == 0 || (o && i), "state arrays must not be NULL");
-        N->from_slots(N->st_o, o);
-        N->from_slots(N->st_i, i);
+        N->from_slots(N->st_o, o, N->E);
+        N->from_slots(N->st_i, i, N->E);
     });
 }
 

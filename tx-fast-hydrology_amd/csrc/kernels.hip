@@ -55,7 +55,8 @@ constexpr int kHalf = kChunk;  // ticks whose lateral inflow is formed in one bu
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
 template <int SLOTS, bool DENSE>
-__global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
+__global__ __launch_bounds__(SLOTS) __attribute__((amdgpu_waves_per_eu(4)))
+void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tile = a.tile;
     constexpr unsigned XB = 0;
@@ -71,6 +72,13 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int tid = threadIdx.x;
     const int64_t t_start = a.trace ? wall_clock64() : 0;
     const int w = a.active[blockIdx.x];
+    // ensemble member of this workgroup instance: member-major arrays (uniform bases)
+    const int64_t mem = blockIdx.y;
+    const double* Fm = a.F + mem * a.mF;
+    double* Om = a.O + mem * a.mO;
+    double* XSm = a.XS + mem * a.mX;
+    double2* BSm = reinterpret_cast<double2*>(a.BS) + mem * a.mS;
+    double* dum = a.dummy + mem * kDummyPerMember;
     const int64_t d = (int64_t)w * SLOTS + tid;
     const int T = a.T;
     const int k0 = a.kappa0;
@@ -89,8 +97,8 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
     const bool from_bs = k0 > gminw;
     const int64_t wb = a.wbase[w];
-    const double2 bs = reinterpret_cast<const double2*>(a.BS)[from_bs ? d : 0];
-    const double st_o = a.st_o[d], st_i = a.st_i[d];
+    const double2 bs = BSm[from_bs ? d : 0];
+    const double st_o = a.st_o[mem * a.mS + d], st_i = a.st_i[mem * a.mS + d];
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
     const int cnt = live ? a.up_cnt[d] : 0;
     const uint64_t up4 = a.up4[d];
@@ -124,7 +132,7 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         for (int k = 0; k < 8; ++k) {   // consecutive lanes read consecutive steps of a stream
             const int t = ti[k] - eg[k];
             const bool ok = t >= 0 && t < T;
-            v[k] = a.XS[ok ? (int64_t)ee[k] * T + t : 0];
+            v[k] = XSm[ok ? (int64_t)ee[k] * T + t : 0];
             v[k] = ok ? v[k] : 0.0;
         }
 #pragma unroll
@@ -173,9 +181,9 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
     // forcing rows of the first chunk
     int rb, nr;
     chunk_rows(tab, tw0, k0, G, T, rb, nr);
-    double f0 = a.F[(int64_t)clamp_row(rb, nrow) * ns + d];
-    double f1 = a.F[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
-    double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
+    double f0 = Fm[(int64_t)clamp_row(rb, nrow) * ns + d];
+    double f1 = Fm[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
+    double f2 = Fm[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
     __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
@@ -196,9 +204,9 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
         int rbn, nrn;
         chunk_rows(tab, tw0, kc + kChunk, G, c + kChunk < tile ? T : 0, rbn, nrn);
-        const double g0 = a.F[(int64_t)clamp_row(rbn, nrow) * ns + d];
-        const double g1 = a.F[(int64_t)clamp_row(rbn + 1, nrow) * ns + d];
-        const double g2 = a.F[(int64_t)clamp_row(rbn + 2, nrow) * ns + d];
+        const double g0 = Fm[(int64_t)clamp_row(rbn, nrow) * ns + d];
+        const double g1 = Fm[(int64_t)clamp_row(rbn + 1, nrow) * ns + d];
+        const double g2 = Fm[(int64_t)clamp_row(rbn + 2, nrow) * ns + d];
         // per-chunk LDS cursors: upstream value of tick i at m[u] + 8 * ((i + 1) & 1)
         unsigned m[kUpInline];
 #pragma unroll
@@ -214,8 +222,8 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                 const int4 e = *reinterpret_cast<const int4*>(lds + tp + 16u * (h + j));
                 double flo, fhi;
                 if (DENSE && slow) {
-                    flo = a.F[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + d];
-                    fhi = a.F[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + d];
+                    flo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + d];
+                    fhi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + d];
                 } else {
                     flo = lds_f64(lds, frp + 8u * (unsigned)e.x);
                     fhi = lds_f64(lds, frp + 8u * (unsigned)e.y);
@@ -269,10 +277,10 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
                 const int k = kc + i;
                 const bool inwin = k >= gminw && k < wend;
                 const int64_t row = inwin ? wb + (int64_t)(k - gminw) * SLOTS : 0;
-                double* orow = inwin ? a.O + row : a.dummy;
+                double* orow = inwin ? Om + row : dum;
                 if (!MCR_EXP_NO_STORES) {
                     orow[tid] = routed ? ov : 0.0;
-                    if (xsrc && act) a.XS[xs0 + k] = ov;
+                    if (xsrc && act) XSm[xs0 + k] = ov;
                 }
                 if (!MCR_EXP_NO_BARRIER) __syncthreads();
             }
@@ -284,8 +292,8 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
         f2 = g2;
     }
     // state for the next launch of this workgroup (lanes that did not run keep theirs)
-    reinterpret_cast<double2*>(a.BS)[d] = make_double2(op, ip);
-    if (a.trace && tid == 0) {
+    BSm[d] = make_double2(op, ip);
+    if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
         rec[0] = t_start;
@@ -298,31 +306,42 @@ __global__ __launch_bounds__(SLOTS) void wavefront_det(WaveArgs a) {
 }
 
 __global__ void scatter_to_slots(const double* __restrict__ src, double* __restrict__ dst,
-                                 const int64_t* __restrict__ slot_reach, int64_t nslots) {
-    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < nslots;
-         d += (int64_t)gridDim.x * blockDim.x) {
+                                 const int64_t* __restrict__ slot_reach, int64_t nslots,
+                                 int64_t E) {
+    const int64_t total = nslots * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = x / nslots;
+        const int64_t d = x - e * nslots;
         const int64_t j = slot_reach[d];
-        dst[d] = j >= 0 ? src[j] : 0.0;
+        dst[x] = j >= 0 ? src[j * E + e] : 0.0;
     }
 }
 
 __global__ void gather_from_slots(const double* __restrict__ src, double* __restrict__ dst,
-                                  const int64_t* __restrict__ pos, int64_t n) {
-    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
-         j += (int64_t)gridDim.x * blockDim.x)
-        dst[j] = src[pos[j]];
+                                  const int64_t* __restrict__ pos, int64_t n, int64_t nslots,
+                                  int64_t E) {
+    const int64_t total = n * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = x / E;
+        const int64_t e = x - j * E;
+        dst[x] = src[e * nslots + pos[j]];
+    }
 }
 
 __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restrict__ F,
                                  const int64_t* __restrict__ slot_reach, int64_t n,
-                                 int64_t nslots, int64_t n_rows) {
-    const int64_t total = nslots * n_rows;
+                                 int64_t nslots, int64_t n_rows, int64_t E) {
+    const int64_t total = nslots * n_rows * E;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = x / nslots;
-        const int64_t d = x - r * nslots;
+        const int64_t er = x / nslots;                  // e * n_rows + r
+        const int64_t d = x - er * nslots;
+        const int64_t e = er / n_rows;
+        const int64_t r = er - e * n_rows;
         const int64_t j = slot_reach[d];
-        F[x] = j >= 0 ? fp[r * n + j] : 0.0;
+        F[x] = j >= 0 ? fp[(r * n + j) * E + e] : 0.0;
     }
 }
 
@@ -350,48 +369,61 @@ __device__ __forceinline__ double inflow_at(const double* __restrict__ O,
     return s;
 }
 
-__global__ void final_state(const double* __restrict__ O, double* __restrict__ st_o,
+__global__ void final_state(const double* __restrict__ O, int64_t mO, double* __restrict__ st_o,
                             double* __restrict__ st_i, const int64_t* __restrict__ jbase,
                             const int64_t* __restrict__ slot_reach,
                             const int64_t* __restrict__ in_off,
                             const int64_t* __restrict__ in_list, int64_t nslots, int slots,
-                            int64_t T) {
-    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < nslots;
-         d += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t j = slot_reach[d];
+                            int64_t T, int64_t E) {
+    const int64_t total = nslots * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = x / nslots;
+        const int64_t j = slot_reach[x - e * nslots];
         if (j >= 0) {
-            st_o[d] = O[jbase[j] + (T - 1) * slots];
-            st_i[d] = inflow_at(O, jbase, in_off, in_list, j, T - 1, slots);
+            const double* Oe = O + e * mO;
+            st_o[x] = Oe[jbase[j] + (T - 1) * slots];
+            st_i[x] = inflow_at(Oe, jbase, in_off, in_list, j, T - 1, slots);
         }
     }
 }
 
-// out[t - t0][j]: consecutive threads take consecutive j (coalesced writes, gathered reads)
-__global__ void gather_steps(const double* __restrict__ O, const int64_t* __restrict__ jbase,
+// out[t - t0][j][e]: consecutive threads take consecutive (j, e) (coalesced writes)
+__global__ void gather_steps(const double* __restrict__ O, int64_t mO,
+                             const int64_t* __restrict__ jbase,
                              const int64_t* __restrict__ in_off,
                              const int64_t* __restrict__ in_list, bool inflow, int slots,
-                             double* __restrict__ out, int64_t n, int64_t t0, int64_t t1) {
-    const int64_t total = n * (t1 - t0);
+                             double* __restrict__ out, int64_t n, int64_t t0, int64_t t1,
+                             int64_t E) {
+    const int64_t total = n * (t1 - t0) * E;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = x / n;
-        const int64_t j = x - t * n;
-        out[x] = inflow ? inflow_at(O, jbase, in_off, in_list, j, t0 + t, slots)
-                        : O[jbase[j] + (t0 + t) * slots];
+        const int64_t tj = x / E;
+        const int64_t e = x - tj * E;
+        const int64_t t = tj / n;
+        const int64_t j = tj - t * n;
+        const double* Oe = O + e * mO;
+        out[x] = inflow ? inflow_at(Oe, jbase, in_off, in_list, j, t0 + t, slots)
+                        : Oe[jbase[j] + (t0 + t) * slots];
     }
 }
 
-__global__ void gather_series(const double* __restrict__ O, const int64_t* __restrict__ jbase,
+// out[j][t][e]
+__global__ void gather_series(const double* __restrict__ O, int64_t mO,
+                              const int64_t* __restrict__ jbase,
                               const int64_t* __restrict__ in_off,
                               const int64_t* __restrict__ in_list, bool inflow, int slots,
-                              double* __restrict__ out, int64_t n, int64_t T) {
-    const int64_t total = n * T;
+                              double* __restrict__ out, int64_t n, int64_t T, int64_t E) {
+    const int64_t total = n * T * E;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t j = x / T;
-        const int64_t t = x - j * T;
-        out[x] = inflow ? inflow_at(O, jbase, in_off, in_list, j, t, slots)
-                        : O[jbase[j] + t * slots];
+        const int64_t jt = x / E;
+        const int64_t e = x - jt * E;
+        const int64_t j = jt / T;
+        const int64_t t = jt - j * T;
+        const double* Oe = O + e * mO;
+        out[x] = inflow ? inflow_at(Oe, jbase, in_off, in_list, j, t, slots)
+                        : Oe[jbase[j] + t * slots];
     }
 }
 
@@ -405,10 +437,12 @@ inline int grid_for(int64_t work, int block) {
 }  // namespace
 
 template <bool DENSE>
-hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, size_t lds, hipStream_t s) {
+hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, size_t lds, int members,
+                              hipStream_t s) {
+    const dim3 g(grid, members);
     switch (slots) {
 #define MCR_CASE(S) \
-    case S: hipLaunchKernelGGL((wavefront_det<S, DENSE>), grid, S, lds, s, a); break;
+    case S: hipLaunchKernelGGL((wavefront_det<S, DENSE>), g, S, lds, s, a); break;
         MCR_SLOT_LIST(MCR_CASE)
 #undef MCR_CASE
         default: return hipErrorInvalidValue;
@@ -417,28 +451,30 @@ hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, size_t lds
 }
 
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds, bool dense,
-                            hipStream_t s) {
-    return dense ? launch_wavefront_t<true>(a, grid, slots, lds, s)
-                 : launch_wavefront_t<false>(a, grid, slots, lds, s);
+                            int members, hipStream_t s) {
+    return dense ? launch_wavefront_t<true>(a, grid, slots, lds, members, s)
+                 : launch_wavefront_t<false>(a, grid, slots, lds, members, s);
 }
 
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,
-                                   int64_t nslots, hipStream_t s) {
-    hipLaunchKernelGGL(scatter_to_slots, grid_for(nslots, 256), 256, 0, s, src, dst, slot_reach,
-                       nslots);
+                                   int64_t nslots, int64_t E, hipStream_t s) {
+    hipLaunchKernelGGL(scatter_to_slots, grid_for(nslots * E, 256), 256, 0, s, src, dst,
+                       slot_reach, nslots, E);
     return hipGetLastError();
 }
 
 hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_t* pos,
-                                    int64_t n, hipStream_t s) {
-    hipLaunchKernelGGL(gather_from_slots, grid_for(n, 256), 256, 0, s, src, dst, pos, n);
+                                    int64_t n, int64_t nslots, int64_t E, hipStream_t s) {
+    hipLaunchKernelGGL(gather_from_slots, grid_for(n * E, 256), 256, 0, s, src, dst, pos, n,
+                       nslots, E);
     return hipGetLastError();
 }
 
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
-                                   int64_t n, int64_t nslots, int64_t n_rows, hipStream_t s) {
-    hipLaunchKernelGGL(forcing_to_slots, grid_for(nslots * n_rows, 256), 256, 0, s, fp, F,
-                       slot_reach, n, nslots, n_rows);
+                                   int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
+                                   hipStream_t s) {
+    hipLaunchKernelGGL(forcing_to_slots, grid_for(nslots * n_rows * E, 256), 256, 0, s, fp, F,
+                       slot_reach, n, nslots, n_rows, E);
     return hipGetLastError();
 }
 
@@ -451,30 +487,32 @@ hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32
     return hipGetLastError();
 }
 
-hipError_t launch_final_state(const double* O, double* st_o, double* st_i, const int64_t* jbase,
-                              const int64_t* slot_reach, const int64_t* in_off,
-                              const int64_t* in_list, int64_t nslots, int slots, int64_t T,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(final_state, grid_for(nslots, 256), 256, 0, s, O, st_o, st_i, jbase,
-                       slot_reach, in_off, in_list, nslots, slots, T);
+hipError_t launch_final_state(const double* O, int64_t mO, double* st_o, double* st_i,
+                              const int64_t* jbase, const int64_t* slot_reach,
+                              const int64_t* in_off, const int64_t* in_list, int64_t nslots,
+                              int slots, int64_t T, int64_t E, hipStream_t s) {
+    hipLaunchKernelGGL(final_state, grid_for(nslots * E, 256), 256, 0, s, O, mO, st_o, st_i,
+                       jbase, slot_reach, in_off, in_list, nslots, slots, T, E);
     return hipGetLastError();
 }
 
-hipError_t launch_gather_steps(const double* O, const int64_t* jbase, const int64_t* in_off,
-                               const int64_t* in_list, bool inflow, int slots, double* out,
-                               int64_t n, int64_t t0, int64_t t1, hipStream_t s) {
+hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase,
+                               const int64_t* in_off, const int64_t* in_list, bool inflow,
+                               int slots, double* out, int64_t n, int64_t t0, int64_t t1,
+                               int64_t E, hipStream_t s) {
     if (n <= 0 || t1 <= t0) return hipSuccess;
-    hipLaunchKernelGGL(gather_steps, grid_for(n * (t1 - t0), 256), 256, 0, s, O, jbase, in_off,
-                       in_list, inflow, slots, out, n, t0, t1);
+    hipLaunchKernelGGL(gather_steps, grid_for(n * (t1 - t0) * E, 256), 256, 0, s, O, mO, jbase,
+                       in_off, in_list, inflow, slots, out, n, t0, t1, E);
     return hipGetLastError();
 }
 
-hipError_t launch_gather_series(const double* O, const int64_t* jbase, const int64_t* in_off,
-                                const int64_t* in_list, bool inflow, int slots, double* out,
-                                int64_t n, int64_t T, hipStream_t s) {
+hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbase,
+                                const int64_t* in_off, const int64_t* in_list, bool inflow,
+                                int slots, double* out, int64_t n, int64_t T, int64_t E,
+                                hipStream_t s) {
     if (n <= 0 || T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_series, grid_for(n * T, 256), 256, 0, s, O, jbase, in_off, in_list,
-                       inflow, slots, out, n, T);
+    hipLaunchKernelGGL(gather_series, grid_for(n * T * E, 256), 256, 0, s, O, mO, jbase, in_off,
+                       in_list, inflow, slots, out, n, T, E);
     return hipGetLastError();
 }
 

@@ -26,6 +26,9 @@ namespace mcr {
 // together).  Launch lengths (`tile`) are multiples of it.
 constexpr int kChunk = 8;
 
+// doubles of the out-of-window dummy row per ensemble member (>= 2 * largest slots)
+constexpr int64_t kDummyPerMember = 2048;
+
 // Dataflow kernel (flow.hip): external inputs per workgroup it supports, longest step table it
 // keeps in LDS, minimum cross-cluster slack (the helper stages the next chunk, so producers must
 // be more than one chunk ahead of it).
@@ -63,6 +66,9 @@ struct WaveArgs {
     const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
     double* O;                    // workgroup windows of outflows (see above)
     double* BS;                   // [nslots][2] {o, i} of each slot at the end of a launch
+    // ensemble members (grid y; multi-launch kernel): element strides between members of the
+    // member-major arrays F, O, XS and of st_o / st_i / BS (in slots)
+    int64_t mF, mO, mX, mS;
     double* XS;                   // external-input streams [n_ext][T]: step t of each source
     double* dummy;                // >= 2 * 1024 doubles: cells of out-of-window ticks
     int64_t* trace;               // optional launch trace, kTraceWords per workgroup (NULL = off)
@@ -98,37 +104,44 @@ hipError_t launch_flow(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
 // Resident workgroups per CU of the dataflow kernel at this LDS size.
 hipError_t flow_occupancy(int slots, bool dense, size_t lds_bytes, int* blocks_per_cu);
 
-// dense: the step table has a kChunk-step window spanning more than 3 forcing rows
+// dense: the step table has a kChunk-step window spanning more than 3 forcing rows.
+// members: ensemble members (grid y); member strides are in `a`.
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
-                            hipStream_t s);
+                            int members, hipStream_t s);
 
-// st[d] = src[slot_reach[d]] for real slots (caller order -> slot order)
+// Layout conversions between the caller (reach order, member innermost: [n][E]) and the device
+// (slot order, member-major: [E][nslots]).  E = 1 is the deterministic case.
+// dst[e][d] = src[slot_reach[d]][e]  (0 for padding slots)
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,
-                                   int64_t nslots, hipStream_t s);
-// dst[j] = src[pos[j]] (slot order -> caller order)
+                                   int64_t nslots, int64_t E, hipStream_t s);
+// dst[j][e] = src[e][pos[j]]
 hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_t* pos,
-                                    int64_t n, hipStream_t s);
-// F[r][d] = fp[r][slot_reach[d]]  (forcing table to slot order; 0 for padding slots)
+                                    int64_t n, int64_t nslots, int64_t E, hipStream_t s);
+// F[e][r][d] = fp[r][slot_reach[d]][e]  (forcing table to slot order; 0 for padding slots)
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
-                                   int64_t n, int64_t nslots, int64_t n_rows, hipStream_t s);
+                                   int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
+                                   hipStream_t s);
 // jbase[j] = window index of step 0 of caller reach j
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
                                const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
                                hipStream_t s);
-// state after the last step: st[d] = step T-1 of slot d (inflow recomputed from O)
-hipError_t launch_final_state(const double* O, double* st_o, double* st_i, const int64_t* jbase,
-                              const int64_t* slot_reach, const int64_t* in_off,
-                              const int64_t* in_list, int64_t nslots, int slots, int64_t T,
-                              hipStream_t s);
-// Output gathers (caller order).  inflow = false: out = O[jbase[j] + t * slots];  inflow = true:
-// out = the inflow of reach j at step t, summed from O over its inflow list.
-// step-major out[t - t0][j] for t in [t0, t1)
-hipError_t launch_gather_steps(const double* O, const int64_t* jbase, const int64_t* in_off,
-                               const int64_t* in_list, bool inflow, int slots, double* out,
-                               int64_t n, int64_t t0, int64_t t1, hipStream_t s);
-// reach-major out[j][t] for t in [0, T)
-hipError_t launch_gather_series(const double* O, const int64_t* jbase, const int64_t* in_off,
-                                const int64_t* in_list, bool inflow, int slots, double* out,
-                                int64_t n, int64_t T, hipStream_t s);
+// state after the last step: st[e][d] = step T-1 of slot d of member e (inflow recomputed
+// from O); member e's windows start at O + e * mO
+hipError_t launch_final_state(const double* O, int64_t mO, double* st_o, double* st_i,
+                              const int64_t* jbase, const int64_t* slot_reach,
+                              const int64_t* in_off, const int64_t* in_list, int64_t nslots,
+                              int slots, int64_t T, int64_t E, hipStream_t s);
+// Output gathers (caller order, member innermost).  inflow = false: outflow O; true: the inflow
+// of reach j, summed from O over its inflow list.
+// step-major out[t - t0][j][e] for t in [t0, t1)
+hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase,
+                               const int64_t* in_off, const int64_t* in_list, bool inflow,
+                               int slots, double* out, int64_t n, int64_t t0, int64_t t1,
+                               int64_t E, hipStream_t s);
+// reach-major out[j][t][e] for t in [0, T)
+hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbase,
+                                const int64_t* in_off, const int64_t* in_list, bool inflow,
+                                int slots, double* out, int64_t n, int64_t T, int64_t E,
+                                hipStream_t s);
 
 }  // namespace mcr

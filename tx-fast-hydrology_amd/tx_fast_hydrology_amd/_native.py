@@ -88,6 +88,8 @@ SIGNATURES = {
     "mc_get_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "mc_reset_timing": (_i32, [_vp]),
+    "mc_net_set_members": (_i32, [_vp, _i64]),
+    "mc_net_get_members": (_i32, [_vp, ctypes.POINTER(ctypes.c_int64)]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_get_mode": (_i32, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),

@@ -92,9 +92,13 @@ class Plan:
 
 
 class RoutingNet:
-    """Device-resident routing session for one network (one HIP device, one stream)."""
+    """Device-resident routing session for one network (one HIP device, one stream).
 
-    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0):
+    With ``members`` = E > 1 the session routes an ensemble: per-reach arrays are [n, E]
+    (member innermost), forcing [n_rows, n, E], step-major outputs [T, n, E] (mcroute.h).
+    """
+
+    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, members=1):
         L = nat.lib()
         end = i64(endnodes)
         deg = i64(indegree)
@@ -108,6 +112,18 @@ class RoutingNet:
                                   ctypes.byref(p), ctypes.byref(h)))
         self._h = h
         self.T = 0
+        self.E = 1
+        if members != 1:
+            self.set_members(members)
+
+    def set_members(self, members: int):
+        """Number of ensemble members (zeroes the state, drops forcing and outputs)."""
+        nat.check(nat.lib().mc_net_set_members(self._h, int(members)))
+        self.E = int(members)
+        self.T = 0
+
+    def _shape(self, *lead):
+        return (*lead, self.n) if self.E == 1 else (*lead, self.n, self.E)
 
     # -- configuration -------------------------------------------------------------------
     @property
@@ -128,13 +144,13 @@ class RoutingNet:
 
     def set_state(self, o_t_next, i_t_next):
         o, i = f64(o_t_next), f64(i_t_next)
-        if o.size != self.n or i.size != self.n:
-            raise ValueError("state arrays must have n entries")
+        if o.size != self.n * self.E or i.size != self.n * self.E:
+            raise ValueError(f"state arrays must be {self._shape()}")
         nat.check(nat.lib().mc_set_state(self._h, ptr(o), ptr(i)))
 
     def get_state(self):
-        o = np.empty(self.n)
-        i = np.empty(self.n)
+        o = np.empty(self._shape())
+        i = np.empty(self._shape())
         nat.check(nat.lib().mc_get_state(self._h, ptr(o), ptr(i)))
         return o, i
 
@@ -142,22 +158,22 @@ class RoutingNet:
     def step(self, q_t_next, o_t_prev=None, i_t_prev=None):
         """One timestep; returns fresh (i_t_next, o_t_next) like nutils._ax_bu."""
         q = f64(q_t_next)
-        if q.size != self.n:
-            raise ValueError("q must have n entries")
+        if q.size != self.n * self.E:
+            raise ValueError(f"q must be {self._shape()}")
         o = None if o_t_prev is None else f64(o_t_prev)
         i = None if i_t_prev is None else f64(i_t_prev)
         if (o is None) != (i is None):
             raise ValueError("pass both o_t_prev and i_t_prev, or neither")
-        i_out = np.empty(self.n)
-        o_out = np.empty(self.n)
+        i_out = np.empty(self._shape())
+        o_out = np.empty(self._shape())
         nat.check(nat.lib().mc_step(self._h, ptr(o), ptr(i), ptr(q), ptr(i_out), ptr(o_out)))
         return i_out, o_out
 
     def load_forcing(self, xp, fp):
         xp = f64(xp)
         fp = f64(fp)
-        if fp.ndim != 2 or fp.shape != (xp.size, self.n):
-            raise ValueError(f"forcing must be [{xp.size}][{self.n}], got {fp.shape}")
+        if fp.shape != self._shape(xp.size):
+            raise ValueError(f"forcing must be {self._shape(xp.size)}, got {fp.shape}")
         nat.check(nat.lib().mc_load_forcing(self._h, xp.size, ptr(xp), ptr(fp)))
 
     def run(self, x):
@@ -167,17 +183,18 @@ class RoutingNet:
         self.T = x.size
 
     def fetch_outputs(self, t0=0, t1=None):
-        """Step-major host copies (out_o[t][j], out_i[t][j]) of steps [t0, t1)."""
+        """Step-major host copies (out_o[t][j](e), out_i[t][j](e)) of steps [t0, t1)."""
         t1 = self.T if t1 is None else t1
-        out_o = np.empty((t1 - t0, self.n))
-        out_i = np.empty((t1 - t0, self.n))
+        out_o = np.empty(self._shape(t1 - t0))
+        out_i = np.empty(self._shape(t1 - t0))
         nat.check(nat.lib().mc_fetch_outputs(self._h, t0, t1, ptr(out_o), ptr(out_i)))
         return out_o, out_i
 
     def fetch_series(self):
-        """Reach-major host copies (O[j][t], I[j][t]) of the last run."""
-        O = np.empty((self.n, self.T))
-        I = np.empty((self.n, self.T))
+        """Reach-major host copies (O[j][t](e), I[j][t](e)) of the last run."""
+        shape = (self.n, self.T) if self.E == 1 else (self.n, self.T, self.E)
+        O = np.empty(shape)
+        I = np.empty(shape)
         nat.check(nat.lib().mc_fetch_series(self._h, ptr(O), ptr(I)))
         return O, I
 

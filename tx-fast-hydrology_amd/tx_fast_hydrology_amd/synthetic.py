@@ -140,6 +140,17 @@ def forcing(n, rows=25, seed=1, start="2024-05-01T00:00:00", freq="1h"):
     return idx.asi8.copy(), vals
 
 
+def ensemble(o0, fp, members, seed=5):
+    """Ensemble inputs: member forcing = base x lognormal(0, 0.3) multiplier per
+    (reach, member), constant in time (seed 5); initial state the same way (seed 6).
+    Returns (o0 [n][E], fp [rows][n][E]) in the member-innermost layout of mcroute.h."""
+    n = o0.size
+    m_f = np.random.default_rng(seed).lognormal(0.0, 0.3, (n, members))
+    m_o = np.random.default_rng(seed + 1).lognormal(0.0, 0.3, (n, members))
+    fpe = np.ascontiguousarray(fp[:, :, None] * m_f[None, :, :])
+    return np.ascontiguousarray(o0[:, None] * m_o), fpe
+
+
 def texas(seed=0, n=190_000, n_basins=300, max_depth=1500):
     """Texas-scale synthetic network: ~190k reaches, ~300 outlets."""
     return river_network(n, n_basins, max_depth, np.random.default_rng(seed))
