@@ -117,6 +117,22 @@ int mc_net_get_members(const void* net, int64_t* members);
 
 
 /* Coefficients alpha, beta, chi, gamma (muskingum.py:332-360), caller order. */
+/* _apply_gain (nutils.py:116-134, applied as da.py:124-126) on the session state:
+ * o += 0 + gain for reaches the reference walk processes; i += one-hop sums of those gains in
+ * the reference's finalisation order.  gain: [n] (or [n][E] for an ensemble session). */
+int mc_apply_gain(void* net, const double* gain);
+
+/* Ensemble Kalman analysis on the session's E >= 2 member states: the update of
+ * da.py:110-126 (KalmanFilter.filter) with the forecast covariance replaced by the ensemble
+ * sample covariance, P H^T = X'(HX')^T / (E-1), H P H^T = HX'(HX')^T / (E-1):
+ *     o_e += K (y_e - o_e[gauges]),  K = P H^T (H P H^T + R)^-1,   i_e += one-hop(gain_e)
+ * gauges [m]: reach indices (caller order; H selects their outflow); y [m][E]: observations per
+ * member (identical columns = no perturbation); R [m][m] SPD.  Dense products run on f64 MFMA,
+ * the m x m solve on rocSOLVER.  mc_enkf_gain returns K as [n][m] (diagnostics / tests). */
+int mc_enkf_analysis(void* net, int64_t m, const int64_t* gauges, const double* y,
+                     const double* R);
+int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, double* K_out);
+
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
                   const double* gamma);
 /* State (o_t_next, i_t_next) of the model, caller order. */

@@ -1,0 +1,146 @@
+"""GPU parity of the analysis step.
+
+* `mc_apply_gain` is `_apply_gain` (nutils.py:116-134) applied as da.py:124-126 -> bit-exact vs
+  the oracle, including networks with cycles / unprocessed reaches (golden g8 topologies).
+* The ensemble Kalman analysis has no reference implementation, so parity is by construction
+  ("EnKF known-answer test"): an ensemble whose anomalies have exact sample
+  covariance P must give the reference gain K = P[:, s] (P[s, s] + R)^-1 (da.py:119) and, with
+  identical observations in every member, the reference mean update (da.py:121-126).  Tolerance
+  1e-11 relative (f64 MFMA products + Cholesky vs numpy's inverse).
+* A randomized perturbed-observation analysis is checked against a float64 numpy restatement of
+  the same ensemble formulas.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tx_fast_hydrology_amd import engine, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(end, members=1, slots=0):
+    n = end.size
+    start = np.arange(n)
+    indeg = orc.compute_indegree(start, end)
+    K, X, _ = synthetic.model_arrays(n, seed=n)
+    coef = orc.muskingum_coeffs(K, X, 300.0)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=members)
+    net.set_coeffs(*coef)
+    return net, start, indeg
+
+
+def test_apply_gain_bitexact_golden_topologies(golden):
+    g = golden("g8_ax_bu_edge.npz")
+    rng = np.random.default_rng(0)
+    for name in g["names"]:
+        end, indeg, heads = g[f"{name}_endnodes"], g[f"{name}_indegree"], g[f"{name}_heads"]
+        n = end.size
+        net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16)
+        net.set_coeffs(*(np.full(n, v) for v in (0.1, 0.2, 0.3, 0.4)))
+        o0, i0 = rng.uniform(0, 3, n), rng.uniform(0, 3, n)
+        net.set_state(o0, i0)
+        gain = rng.normal(0, 1, n)
+        net.apply_gain(gain)
+        ig, og = orc.apply_gain(heads, end, gain, indeg)
+        o, i = net.get_state()
+        assert np.array_equal(o, o0 + og), name
+        assert np.array_equal(i, i0 + ig), name
+
+
+def test_apply_gain_ensemble_per_member():
+    end = synthetic.river_network(4000, 5, 150, np.random.default_rng(3))
+    E = 5
+    net, start, indeg = _net(end, members=E)
+    n = end.size
+    rng = np.random.default_rng(1)
+    o0, i0 = rng.uniform(0, 3, (n, E)), rng.uniform(0, 3, (n, E))
+    net.set_state(o0, i0)
+    gain = rng.normal(0, 1, (n, E))
+    net.apply_gain(gain)
+    o, i = net.get_state()
+    for e in range(E):
+        ig, og = orc.apply_gain(start[indeg == 0], end, gain[:, e], indeg)
+        assert np.array_equal(o[:, e], o0[:, e] + og), e
+        assert np.array_equal(i[:, e], i0[:, e] + ig), e
+
+
+def _kat_case(n, m, seed):
+    rng = np.random.default_rng(seed)
+    end = synthetic.river_network(n, 2, 25, rng)
+    n = end.size
+    B = rng.normal(0, 1, (n, n))
+    P = B @ B.T / n + 0.5 * np.eye(n)                       # SPD forecast covariance
+    L = np.linalg.cholesky(P)
+    E = 2 * n
+    Xp = np.sqrt((E - 1) / 2.0) * np.concatenate([L, -L], axis=1)   # exact sample cov = P
+    xbar = rng.uniform(1, 5, n)
+    s = np.sort(rng.choice(n, m, replace=False))
+    R = 1e-2 * np.eye(m) + 1e-3 * np.ones((m, m))
+    return end, P, E, Xp, xbar, s, R
+
+
+def test_enkf_known_answer_gain_and_mean_update():
+    end, P, E, Xp, xbar, s, R = _kat_case(48, 6, 11)
+    n = end.size
+    net, start, indeg = _net(end, members=E)
+    X = xbar[:, None] + Xp
+    i0 = np.random.default_rng(2).uniform(0, 1, (n, E))
+    net.set_state(X, i0)
+    K_ref = P[:, s] @ np.linalg.inv(P[np.ix_(s, s)] + R)             # da.py:119
+    K = net.enkf_gain(s, R)
+    np.testing.assert_allclose(K, K_ref, rtol=0, atol=1e-11 * np.abs(K_ref).max())
+    # identical observations in every member: the mean follows da.py:121-126 exactly
+    y = xbar[s] + np.random.default_rng(4).normal(0, 0.2, s.size)
+    net.enkf_analysis(s, np.repeat(y[:, None], E, axis=1), R)
+    o, i = net.get_state()
+    gain_ref = K_ref @ (y - xbar[s])
+    ig_ref, og_ref = orc.apply_gain(start[indeg == 0], end, gain_ref, indeg)
+    tol = 1e-11 * max(np.abs(gain_ref).max(), 1.0)
+    np.testing.assert_allclose(o.mean(1) - X.mean(1), og_ref, rtol=0, atol=tol)
+    np.testing.assert_allclose(i.mean(1) - i0.mean(1), ig_ref, rtol=0, atol=tol)
+    # anomalies are shrunk but stay centred: the mean of the increments is the mean gain
+
+
+def _numpy_enkf(X, s, Y, R):
+    E = X.shape[1]
+    A = X - X.mean(1, keepdims=True)
+    HA = A[s]
+    C = HA @ HA.T / (E - 1) + R
+    W = np.linalg.solve(C, Y - X[s])
+    return A @ (HA.T @ W) / (E - 1)
+
+
+def test_enkf_perturbed_observations_vs_numpy():
+    end = synthetic.river_network(6000, 6, 200, np.random.default_rng(21))
+    n = end.size
+    E, m = 32, 40
+    net, start, indeg = _net(end, members=E)
+    rng = np.random.default_rng(5)
+    X = rng.uniform(0.5, 5, n)[:, None] * rng.lognormal(0, 0.3, (n, E))
+    I0 = rng.uniform(0, 5, (n, E))
+    net.set_state(X, I0)
+    s = np.sort(rng.choice(n, m, replace=False))
+    R = 1e-2 * np.eye(m)
+    Y = X[s].mean(1, keepdims=True) + 0.3 + rng.normal(0, 0.1, (m, E))
+    net.enkf_analysis(s, Y, R)
+    o, i = net.get_state()
+    G = _numpy_enkf(X, s, Y, R)
+    heads = start[indeg == 0]
+    scale = np.abs(G).max()
+    for e in range(E):
+        ig, og = orc.apply_gain(heads, end, G[:, e], indeg)
+        np.testing.assert_allclose(o[:, e] - X[:, e], og, rtol=0, atol=1e-10 * scale)
+        np.testing.assert_allclose(i[:, e] - I0[:, e], ig, rtol=0, atol=1e-10 * scale * 10)
+
+
+def test_enkf_rejects_single_member_and_bad_R():
+    from tx_fast_hydrology_amd import _native as nat
+    end = synthetic.river_network(500, 1, 30, np.random.default_rng(1))
+    net, start, indeg = _net(end)
+    with pytest.raises(nat.RoutingError):
+        net.enkf_gain(np.array([3, 7]), np.eye(2))
+    net2, _, _ = _net(end, members=4)
+    net2.set_state(np.ones((end.size, 4)), np.ones((end.size, 4)))   # zero spread
+    with pytest.raises(nat.RoutingError):
+        net2.enkf_gain(np.array([3, 7]), -np.eye(2))                 # not SPD

@@ -1,0 +1,227 @@
+// Ensemble analysis kernels (gfx950): the da.py-style Kalman update with the forecast
+// covariance replaced by the ensemble sample covariance.
+//
+//   reference (da.py:110-126, KalmanFilter.filter):  K = P[:, s] (P[s, s] + R)^-1,
+//       gain = K dz,  o += gain,  i += one-hop(gain)  (_apply_gain, nutils.py:116-134)
+//   here, with anomalies A = X - mean(X) over E members and HA = A[s]:
+//       P H^T = A HA^T / (E-1),  H P H^T = HA HA^T / (E-1)
+//       W = (HA HA^T / (E-1) + R)^-1 D,   D = Y - HX  (per-member innovations)
+//       G = A (HA^T W) / (E-1)             (per-member increments, = K D)
+//       o += 0 + G,  i += one-hop(G)       (rank-ordered sums, as _apply_gain)
+// The dense products run on f64 MFMA (v_mfma_f64_16x16x4f64); the m x m SPD solve is rocSOLVER.
+// Device arrays are member-major slot order ([E][nslots]) like the routing session.
+#include "analysis.hpp"
+#include "plan.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace mcr {
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 64;   // C tile per workgroup (4 waves, 32 x 32 each)
+constexpr int kBK = 16;     // K slice staged in LDS
+constexpr int kPad = 1;     // LDS row padding (f64)
+
+// C = alpha op(A) op(B) + beta C, column-major, op = transpose when TA / TB.
+// op(A) is M x K, op(B) is K x N.  beta == 0 never reads C.
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
+                                                  const double* __restrict__ A, int64_t lda,
+                                                  const double* __restrict__ B, int64_t ldb,
+                                                  double beta, double* __restrict__ C,
+                                                  int64_t ldc) {
+    __shared__ double As[kBK][kTile + kPad];   // As[k][i] = op(A)(row0 + i, k0 + k)
+    __shared__ double Bs[kBK][kTile + kPad];   // Bs[k][j] = op(B)(k0 + k, col0 + j)
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t row0 = (int64_t)blockIdx.x * kTile;
+    const int64_t col0 = (int64_t)blockIdx.y * kTile;
+    const int wr = (wave & 1) * 32, wc = (wave >> 1) * 32;
+    f64x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+    for (int64_t k0 = 0; k0 < K; k0 += kBK) {
+#pragma unroll
+        for (int r = 0; r < (kTile * kBK) / 256; ++r) {
+            const int idx = tid + 256 * r;
+            // coalesced along the contiguous dimension of each operand
+            int i, k;
+            if (TA) { k = idx % kBK; i = idx / kBK; } else { i = idx % kTile; k = idx / kTile; }
+            const int64_t gi = row0 + i, gk = k0 + k;
+            double v = 0.0;
+            if (gi < M && gk < K) v = TA ? A[gk + gi * lda] : A[gi + gk * lda];
+            As[k][i] = v;
+            int j;
+            if (TB) { j = idx % kTile; k = idx / kTile; } else { k = idx % kBK; j = idx / kBK; }
+            const int64_t gj = col0 + j, gk2 = k0 + k;
+            double w = 0.0;
+            if (gj < N && gk2 < K) w = TB ? B[gj + gk2 * ldb] : B[gk2 + gj * ldb];
+            Bs[k][j] = w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < kBK; kk += 4) {
+            // f64 16x16x4: A lane l holds A[l & 15][k = l >> 4], B lane l holds B[k = l >> 4][l & 15]
+            const int ka = kk + (lane >> 4);
+            const double a0 = As[ka][wr + (lane & 15)];
+            const double a1 = As[ka][wr + 16 + (lane & 15)];
+            const double b0 = Bs[ka][wc + (lane & 15)];
+            const double b1 = Bs[ka][wc + 16 + (lane & 15)];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // C/D of f64 16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gi = row0 + wr + 16 * i + (lane >> 4) + 4 * r;
+                const int64_t gj = col0 + wc + 16 * j + (lane & 15);
+                if (gi < M && gj < N) {
+                    double* c = C + gi + gj * ldc;
+                    *c = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *c;
+                }
+            }
+}
+
+// xbar[d] = (sum_e X[e][d]) / E ;  A[e][d] = X[e][d] - xbar[d]
+__global__ void mean_anomalies(const double* __restrict__ X, double* __restrict__ A,
+                               int64_t ns, int64_t E) {
+    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < ns;
+         d += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int64_t e = 0; e < E; ++e) s += X[e * ns + d];
+        const double xbar = s / (double)E;
+        for (int64_t e = 0; e < E; ++e) A[e * ns + d] = X[e * ns + d] - xbar;
+    }
+}
+
+// HA[g + e m] = A[e][gslot[g]],  D[g + e m] = Y[g][e] - X[e][gslot[g]]
+__global__ void gauge_gather(const double* __restrict__ A, const double* __restrict__ X,
+                             const int64_t* __restrict__ gslot, const double* __restrict__ Y,
+                             double* __restrict__ HA, double* __restrict__ D, int64_t m,
+                             int64_t ns, int64_t E) {
+    const int64_t total = m * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = x / m;
+        const int64_t g = x - e * m;
+        const int64_t d = gslot[g];
+        HA[x] = A[e * ns + d];
+        if (D) D[x] = Y[g * E + e] - X[e * ns + d];
+    }
+}
+
+// _apply_gain (nutils.py:116-134) per member on slot-order state:
+//   o_gain[j] = 0 + G[j] for reaches the reference walk processes, 0 otherwise;
+//   i_gain[j] = ((0 + o_gain[u1]) + o_gain[u2]) + ...  over j's routed upstreams in rank order;
+//   o += o_gain,  i += i_gain   (da.py:124-126)
+__global__ void apply_gain(const double* __restrict__ G, double* __restrict__ st_o,
+                           double* __restrict__ st_i, const int64_t* __restrict__ slot_reach,
+                           const int64_t* __restrict__ pos, const uint8_t* __restrict__ flags,
+                           const int64_t* __restrict__ in_off,
+                           const int64_t* __restrict__ in_list, int64_t ns, int64_t E) {
+    const int64_t total = ns * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = x / ns;
+        const int64_t d = x - e * ns;
+        const int64_t j = slot_reach[d];
+        if (j < 0) continue;
+        const double* Ge = G + e * ns;
+        const double og = flags[d] == kSlotRouted ? 0.0 + Ge[d] : 0.0;
+        double ig = 0.0;
+        for (int64_t k = in_off[j]; k < in_off[j + 1]; ++k) ig = ig + (0.0 + Ge[pos[in_list[k]]]);
+        st_o[x] = st_o[x] + og;
+        st_i[x] = st_i[x] + ig;
+    }
+}
+
+// Kt[g + j m] (m x n, solved in place) -> K_out[j][g] in caller order: K_out[j * m + g]
+__global__ void gain_to_caller(const double* __restrict__ Kt, double* __restrict__ out,
+                               const int64_t* __restrict__ pos, int64_t m, int64_t n) {
+    const int64_t total = n * m;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = x / m;
+        const int64_t g = x - j * m;
+        out[x] = Kt[g + pos[j] * m];
+    }
+}
+
+inline int grid_for(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > 65536) g = 65536;
+    return (int)g;
+}
+
+}  // namespace
+
+hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha,
+                        const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                        double* C, int64_t ldc, hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if ((M + kTile - 1) / kTile > 0x7fffffff || (N + kTile - 1) / kTile > 65535)
+        return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((M + kTile - 1) / kTile), (unsigned)((N + kTile - 1) / kTile));
+    if (!ta && !tb)
+        hipLaunchKernelGGL((dgemm_mfma<false, false>), grid, 256, 0, s, M, N, K, alpha, A, lda,
+                           B, ldb, beta, C, ldc);
+    else if (!ta && tb)
+        hipLaunchKernelGGL((dgemm_mfma<false, true>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
+                           ldb, beta, C, ldc);
+    else if (ta && !tb)
+        hipLaunchKernelGGL((dgemm_mfma<true, false>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
+                           ldb, beta, C, ldc);
+    else
+        hipLaunchKernelGGL((dgemm_mfma<true, true>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
+                           ldb, beta, C, ldc);
+    return hipGetLastError();
+}
+
+hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(mean_anomalies, grid_for(ns, 256), 256, 0, s, X, A, ns, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_gauge_gather(const double* A, const double* X, const int64_t* gslot,
+                               const double* Y, double* HA, double* D, int64_t m, int64_t ns,
+                               int64_t E, hipStream_t s) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gauge_gather, grid_for(m * E, 256), 256, 0, s, A, X, gslot, Y, HA, D, m,
+                       ns, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i,
+                             const int64_t* slot_reach, const int64_t* pos,
+                             const uint8_t* flags, const int64_t* in_off,
+                             const int64_t* in_list, int64_t ns, int64_t E, hipStream_t s) {
+    hipLaunchKernelGGL(apply_gain, grid_for(ns * E, 256), 256, 0, s, G, st_o, st_i, slot_reach,
+                       pos, flags, in_off, in_list, ns, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_gain_to_caller(const double* Kt, double* out, const int64_t* pos, int64_t m,
+                                 int64_t n, hipStream_t s) {
+    if (n <= 0 || m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gain_to_caller, grid_for(n * m, 256), 256, 0, s, Kt, out, pos, m, n);
+    return hipGetLastError();
+}
+
+}  // namespace mcr

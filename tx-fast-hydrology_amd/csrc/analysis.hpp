@@ -1,0 +1,31 @@
+// Ensemble analysis building blocks (analysis.hip): f64 MFMA GEMM and the element kernels of the
+// ensemble Kalman update.  Matrices are column-major with explicit leading dimensions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mcr {
+
+// C = alpha op(A) op(B) + beta C  (op = transpose when ta / tb; op(A) M x K, op(B) K x N)
+hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha,
+                        const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                        double* C, int64_t ldc, hipStream_t s);
+// ensemble mean over members and anomalies A = X - mean (both [E][ns])
+hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
+                                 hipStream_t s);
+// HA (m x E) = A at the gauge slots; D (m x E) = Y[g][e] - X at the gauge slots (D may be NULL)
+hipError_t launch_gauge_gather(const double* A, const double* X, const int64_t* gslot,
+                               const double* Y, double* HA, double* D, int64_t m, int64_t ns,
+                               int64_t E, hipStream_t s);
+// _apply_gain per member: o += 0 + G (routed reaches), i += rank-ordered one-hop sums
+hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i,
+                             const int64_t* slot_reach, const int64_t* pos,
+                             const uint8_t* flags, const int64_t* in_off,
+                             const int64_t* in_list, int64_t ns, int64_t E, hipStream_t s);
+// Kt (m x nslots, column-major) -> K_out[j][g] in caller reach order
+hipError_t launch_gain_to_caller(const double* Kt, double* out, const int64_t* pos, int64_t m,
+                                 int64_t n, hipStream_t s);
+
+}  // namespace mcr

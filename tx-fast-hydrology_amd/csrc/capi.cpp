@@ -12,6 +12,10 @@
 #include <string>
 #include <vector>
 
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include "analysis.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -181,6 +185,12 @@ struct Net {
     int64_t Otot = 0;              // output cells of one member (window sizes summed)
     int64_t sched_E = 0;
 
+    // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
+    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb;
+    DBuf<int64_t> gslot;
+    DBuf<int32_t> info;
+    rocblas_handle blas = nullptr;
+
     // dataflow kernel (flow.hip): mode 0 = automatic, 1 = multi-launch only, 2 = dataflow only
     int mode = 0;
     int last_path = 0;             // 1 multi-launch, 2 dataflow (path of the last run)
@@ -201,6 +211,7 @@ struct Net {
 
     ~Net() {
         if (status_host) (void)hipHostFree(status_host);
+        if (blas) (void)rocblas_destroy_handle(blas);
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
     }
@@ -307,6 +318,103 @@ struct Net {
         HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, plan.nslots, m, stream));
         HIPC(hipMemcpyAsync(host, stage.p, n * m * sizeof(double), hipMemcpyDeviceToHost,
                             stream));
+        sync();
+    }
+
+    // ---- ensemble analysis ----------------------------------------------
+    void apply_gain(const double* gain) {
+        REQUIRE(plan.n == 0 || gain, "gain must not be NULL");
+        if (plan.n == 0) return;
+        const size_t ns = (size_t)plan.nslots;
+        Gn.reserve(ns * E);
+        to_slots(gain, Gn, E);
+        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, slot_reach.p, pos.p, flags.p,
+                                    in_off.p, in_list.p, plan.nslots, E, stream));
+        sync();
+    }
+
+    rocblas_handle solver() {
+        if (!blas && rocblas_create_handle(&blas) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocblas_create_handle failed");
+        if (rocblas_set_stream(blas, stream) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocblas_set_stream failed");
+        return blas;
+    }
+
+    // C2 = HA HA^T / (E-1) + R factored (Cholesky, lower) from the current member state;
+    // anomalies in An, gauge anomalies in HA, innovations Y - HX in Dn (when y != NULL)
+    void analysis_setup(int64_t m, const int64_t* gauges, const double* y, const double* R) {
+        REQUIRE(E >= 2, "the ensemble analysis needs at least 2 members");
+        REQUIRE(m >= 1 && m < (1ll << 31) && gauges && R, "bad gauge arguments");
+        const int64_t n = plan.n, ns = plan.nslots;
+        std::vector<int64_t> gs(m);
+        for (int64_t g = 0; g < m; ++g) {
+            REQUIRE(gauges[g] >= 0 && gauges[g] < n, "gauge index out of range");
+            gs[g] = plan.pos[gauges[g]];
+        }
+        gslot.upload(gs.data(), gs.size(), stream);
+        An.reserve((size_t)(ns * E));
+        HA.reserve((size_t)(m * E));
+        Dn.reserve((size_t)(m * E));
+        C2.upload(R, (size_t)(m * m), stream);   // symmetric: row-major == column-major
+        if (y) Yb.upload(y, (size_t)(m * E), stream);
+        HIPC(mcr::launch_mean_anomalies(st_o.p, An.p, ns, E, stream));
+        HIPC(mcr::launch_gauge_gather(An.p, st_o.p, gslot.p, y ? Yb.p : nullptr, HA.p,
+                                      y ? Dn.p : nullptr, m, ns, E, stream));
+        const double inv = 1.0 / (double)(E - 1);
+        HIPC(mcr::launch_dgemm(false, true, m, m, E, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
+                               stream));
+        info.reserve(1);
+        if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p, (rocblas_int)m,
+                             info.p) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
+        int32_t ih = 0;
+        HIPC(hipMemcpyAsync(&ih, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        sync();
+        if (ih != 0) throw Fail(MC_E_INVALID, "HPH^T + R is not positive definite");
+    }
+
+    void enkf_analysis(int64_t m, const int64_t* gauges, const double* y, const double* R) {
+        REQUIRE(y, "observations must not be NULL");
+        if (plan.n == 0) return;
+        analysis_setup(m, gauges, y, R);
+        const int64_t ns = plan.nslots;
+        const double inv = 1.0 / (double)(E - 1);
+        // W = C2^-1 D (in place in Dn)
+        if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)m, (rocblas_int)E, C2.p,
+                             (rocblas_int)m, Dn.p, (rocblas_int)m) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+        // Z = HA^T W / (E-1)   (E x E),   G = A Z   (ns x E): the per-member increments K D
+        Zn.reserve((size_t)(E * E));
+        Gn.reserve((size_t)(ns * E));
+        HIPC(mcr::launch_dgemm(true, false, E, E, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, E,
+                               stream));
+        HIPC(mcr::launch_dgemm(false, false, ns, E, E, 1.0, An.p, ns, Zn.p, E, 0.0, Gn.p, ns,
+                               stream));
+        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, slot_reach.p, pos.p, flags.p,
+                                    in_off.p, in_list.p, ns, E, stream));
+        sync();
+    }
+
+    // K = (A HA^T / (E-1)) C2^-1  as [n][m] in caller order
+    void enkf_gain(int64_t m, const int64_t* gauges, const double* R, double* K_out) {
+        REQUIRE(K_out, "K_out must not be NULL");
+        if (plan.n == 0) return;
+        REQUIRE(plan.nslots < (1ll << 31), "network too large for the explicit gain");
+        analysis_setup(m, gauges, nullptr, R);
+        const int64_t ns = plan.nslots;
+        const double inv = 1.0 / (double)(E - 1);
+        Gn.reserve((size_t)(m * ns));               // K^T (m x ns), solved in place
+        HIPC(mcr::launch_dgemm(false, true, m, ns, E, inv, HA.p, m, An.p, ns, 0.0, Gn.p, m,
+                               stream));
+        if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)m, (rocblas_int)ns,
+                             C2.p, (rocblas_int)m, Gn.p, (rocblas_int)m) !=
+            rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+        outT.reserve((size_t)(plan.n * m));
+        HIPC(mcr::launch_gain_to_caller(Gn.p, outT.p, pos.p, m, plan.n, stream));
+        HIPC(hipMemcpyAsync(K_out, outT.p, (size_t)(plan.n * m) * sizeof(double),
+                            hipMemcpyDeviceToHost, stream));
         sync();
     }
 
@@ -741,6 +849,19 @@ int mc_net_get_members(const void* net, int64_t* members) {
         REQUIRE(net && members, "null argument");
         *members = static_cast<const Net*>(net)->E;
     });
+}
+
+int mc_apply_gain(void* net, const double* gain) {
+    return guarded([&] { as_net(net)->apply_gain(gain); });
+}
+
+int mc_enkf_analysis(void* net, int64_t m, const int64_t* gauges, const double* y,
+                     const double* R) {
+    return guarded([&] { as_net(net)->enkf_analysis(m, gauges, y, R); });
+}
+
+int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, double* K_out) {
+    return guarded([&] { as_net(net)->enkf_gain(m, gauges, R, K_out); });
 }
 
 int mc_set_coeffs(void* net, const double* a, const double* b, const double* c,

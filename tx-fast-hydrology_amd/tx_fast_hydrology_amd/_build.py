@@ -51,7 +51,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = LIB_PATH + f".{os.getpid()}.tmp"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
-           "-I", INCLUDE, "-I", SRC_DIR, "-o", tmp] + sources()
+           "-I", INCLUDE, "-I", SRC_DIR, "-o", tmp] + sources() + \
+        ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -90,6 +90,9 @@ SIGNATURES = {
     "mc_reset_timing": (_i32, [_vp]),
     "mc_net_set_members": (_i32, [_vp, _i64]),
     "mc_net_get_members": (_i32, [_vp, ctypes.POINTER(ctypes.c_int64)]),
+    "mc_apply_gain": (_i32, [_vp, _vp]),
+    "mc_enkf_analysis": (_i32, [_vp, _i64, _vp, _vp, _vp]),
+    "mc_enkf_gain": (_i32, [_vp, _i64, _vp, _vp, _vp]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_get_mode": (_i32, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),

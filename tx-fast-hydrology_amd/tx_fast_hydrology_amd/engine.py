@@ -169,6 +169,32 @@ class RoutingNet:
         nat.check(nat.lib().mc_step(self._h, ptr(o), ptr(i), ptr(q), ptr(i_out), ptr(o_out)))
         return i_out, o_out
 
+    # -- ensemble analysis -------------------------------------------------
+    def apply_gain(self, gain):
+        """_apply_gain (nutils.py:116-134) applied to the session state: o += gain, i += one-hop
+        gain (da.py:124-126).  gain: [n] or [n, E]."""
+        g = f64(gain)
+        if g.size != self.n * self.E:
+            raise ValueError(f"gain must be {self._shape()}")
+        nat.check(nat.lib().mc_apply_gain(self._h, ptr(g)))
+
+    def enkf_analysis(self, gauges, y, R):
+        """Ensemble Kalman update of the member states: gauges [m] reach indices, y [m, E]
+        observations per member, R [m, m] observation-error covariance."""
+        gs, yy, RR = i64(gauges), f64(y), f64(R)
+        m = gs.size
+        if yy.shape != (m, self.E) or RR.shape != (m, m):
+            raise ValueError("y must be [m, E] and R [m, m]")
+        nat.check(nat.lib().mc_enkf_analysis(self._h, m, ptr(gs), ptr(yy), ptr(RR)))
+
+    def enkf_gain(self, gauges, R):
+        """Kalman gain of the current ensemble, K = P H^T (H P H^T + R)^-1, as [n, m]."""
+        gs, RR = i64(gauges), f64(R)
+        m = gs.size
+        K = np.empty((self.n, m))
+        nat.check(nat.lib().mc_enkf_gain(self._h, m, ptr(gs), ptr(RR), ptr(K)))
+        return K
+
     def load_forcing(self, xp, fp):
         xp = f64(xp)
         fp = f64(fp)
