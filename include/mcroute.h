@@ -133,6 +133,26 @@ int mc_enkf_analysis(void* net, int64_t m, const int64_t* gauges, const double* 
                      const double* R);
 int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, double* K_out);
 
+/* The analysis in stages, for an ensemble sharded over N ranks (one GPU each, E local members,
+ * Et = N E in all).  Pointers named *_dev are DEVICE buffers owned by the caller, who runs the
+ * collectives between the stages (torch.distributed / RCCL; tx_fast_hydrology_amd/ensemble.py):
+ *   1. mc_ens_gauges: local gauge outflows HX_dev [E][m] and innovations D_dev [E][m] from
+ *      y [m][E] (host);                      -> all-gather both into [Et][m]
+ *   2. mc_ens_pack: local states as reach slices send_dev [N][E][S] (S = mc_ens_slice_size);
+ *                                            -> all-to-all into Xs_dev [Et][S] (this rank's slice)
+ *   3. mc_ens_slice_update: anomalies, C = HA HA^T/(Et-1) + R, W = C^-1 D, Z = HA^T W/(Et-1),
+ *      increments of the slice Gs_dev = A Z [Et][S];    -> all-to-all back into [N][E][S]
+ *   4. mc_ens_unpack_apply: local increments -> _apply_gain on the local members.
+ * With N = 1 the stages are exactly mc_enkf_analysis.  Stages run on the session's stream. */
+int mc_ens_slice_size(const void* net, int64_t nranks, int64_t* S);
+int mc_ens_gauges(void* net, int64_t m, const int64_t* gauges, const double* y, double* HX_dev,
+                  double* D_dev);
+int mc_ens_pack(void* net, int64_t nranks, double* send_dev);
+int mc_ens_slice_update(void* net, int64_t nranks, int64_t m, const double* Xs_dev,
+                        const double* HXall_dev, const double* Dall_dev, const double* R,
+                        double* Gs_dev);
+int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv_dev);
+
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
                   const double* gamma);
 /* State (o_t_next, i_t_next) of the model, caller order. */

@@ -144,3 +144,28 @@ def test_enkf_rejects_single_member_and_bad_R():
     net2.set_state(np.ones((end.size, 4)), np.ones((end.size, 4)))   # zero spread
     with pytest.raises(nat.RoutingError):
         net2.enkf_gain(np.array([3, 7]), -np.eye(2))                 # not SPD
+
+
+def test_staged_driver_single_rank_equals_enkf_analysis():
+    """ensemble.distributed_analysis with one rank runs the mc_ens_* stages on torch device
+    buffers; it must reproduce RoutingNet.enkf_analysis exactly."""
+    import torch
+    from tx_fast_hydrology_amd import ensemble
+    end = synthetic.river_network(5000, 4, 150, np.random.default_rng(8))
+    n = end.size
+    E, m = 16, 30
+    rng = np.random.default_rng(9)
+    X = rng.uniform(0.5, 5, n)[:, None] * rng.lognormal(0, 0.3, (n, E))
+    I0 = rng.uniform(0, 5, (n, E))
+    s = np.sort(rng.choice(n, m, replace=False))
+    R = 2e-2 * np.eye(m)
+    Y = ensemble.perturbed_observations(X[s].mean(1) + 0.2, R, E, rng)
+    a, _, _ = _net(end, members=E)
+    a.set_state(X, I0)
+    a.enkf_analysis(s, Y, R)
+    b, _, _ = _net(end, members=E)
+    b.set_state(X, I0)
+    ensemble.distributed_analysis(b, s, Y, R, device=torch.device("cuda", 0))
+    oa, ia = a.get_state()
+    ob, ib = b.get_state()
+    assert np.array_equal(oa, ob) and np.array_equal(ia, ib)

@@ -125,6 +125,51 @@ __global__ void gauge_gather(const double* __restrict__ A, const double* __restr
     }
 }
 
+// HX[e m + g] = X[e][gslot[g]],  D[e m + g] = Y[g][e] - HX  (local members)
+__global__ void gauge_values(const double* __restrict__ X, const int64_t* __restrict__ gslot,
+                             const double* __restrict__ Y, double* __restrict__ HX,
+                             double* __restrict__ D, int64_t m, int64_t ns, int64_t E) {
+    const int64_t total = m * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = x / m;
+        const int64_t g = x - e * m;
+        const double v = X[e * ns + gslot[g]];
+        HX[x] = v;
+        D[x] = Y[g * E + e] - v;
+    }
+}
+
+// member-major state [E][ns] -> reach slices for every rank: out[(r E + e) S + k] = X[e][r S + k]
+__global__ void pack_slices(const double* __restrict__ X, double* __restrict__ out, int64_t ns,
+                            int64_t E, int64_t S, int64_t N) {
+    const int64_t total = N * E * S;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t re = x / S;
+        const int64_t k = x - re * S;
+        const int64_t r = re / E;
+        const int64_t e = re - r * E;
+        const int64_t d = r * S + k;
+        out[x] = d < ns ? X[e * ns + d] : 0.0;
+    }
+}
+
+// inverse: G[e][r S + k] = in[(r E + e) S + k]
+__global__ void unpack_slices(const double* __restrict__ in, double* __restrict__ G, int64_t ns,
+                              int64_t E, int64_t S, int64_t N) {
+    const int64_t total = N * E * S;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t re = x / S;
+        const int64_t k = x - re * S;
+        const int64_t r = re / E;
+        const int64_t e = re - r * E;
+        const int64_t d = r * S + k;
+        if (d < ns) G[e * ns + d] = in[x];
+    }
+}
+
 // _apply_gain (nutils.py:116-134) per member on slot-order state:
 //   o_gain[j] = 0 + G[j] for reaches the reference walk processes, 0 otherwise;
 //   i_gain[j] = ((0 + o_gain[u1]) + o_gain[u2]) + ...  over j's routed upstreams in rank order;
@@ -205,6 +250,27 @@ hipError_t launch_gauge_gather(const double* A, const double* X, const int64_t* 
     if (m <= 0) return hipSuccess;
     hipLaunchKernelGGL(gauge_gather, grid_for(m * E, 256), 256, 0, s, A, X, gslot, Y, HA, D, m,
                        ns, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_gauge_values(const double* X, const int64_t* gslot, const double* Y,
+                               double* HX, double* D, int64_t m, int64_t ns, int64_t E,
+                               hipStream_t s) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gauge_values, grid_for(m * E, 256), 256, 0, s, X, gslot, Y, HX, D, m, ns,
+                       E);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_slices(const double* X, double* out, int64_t ns, int64_t E, int64_t S,
+                              int64_t N, hipStream_t s) {
+    hipLaunchKernelGGL(pack_slices, grid_for(N * E * S, 256), 256, 0, s, X, out, ns, E, S, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_slices(const double* in, double* G, int64_t ns, int64_t E, int64_t S,
+                                int64_t N, hipStream_t s) {
+    hipLaunchKernelGGL(unpack_slices, grid_for(N * E * S, 256), 256, 0, s, in, G, ns, E, S, N);
     return hipGetLastError();
 }
 

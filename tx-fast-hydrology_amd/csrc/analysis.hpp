@@ -19,6 +19,15 @@ hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t
 hipError_t launch_gauge_gather(const double* A, const double* X, const int64_t* gslot,
                                const double* Y, double* HA, double* D, int64_t m, int64_t ns,
                                int64_t E, hipStream_t s);
+// local gauge values HX (m x E, column-major) and innovations D = Y[g][e] - HX
+hipError_t launch_gauge_values(const double* X, const int64_t* gslot, const double* Y,
+                               double* HX, double* D, int64_t m, int64_t ns, int64_t E,
+                               hipStream_t s);
+// member-major [E][ns] <-> per-rank reach slices [N][E][S] (S = ceil(ns / N), zero padded)
+hipError_t launch_pack_slices(const double* X, double* out, int64_t ns, int64_t E, int64_t S,
+                              int64_t N, hipStream_t s);
+hipError_t launch_unpack_slices(const double* in, double* G, int64_t ns, int64_t E, int64_t S,
+                                int64_t N, hipStream_t s);
 // _apply_gain per member: o += 0 + G (routed reaches), i += rank-ordered one-hop sums
 hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i,
                              const int64_t* slot_reach, const int64_t* pos,

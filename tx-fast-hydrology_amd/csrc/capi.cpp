@@ -186,7 +186,7 @@ struct Net {
     int64_t sched_E = 0;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
-    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb;
+    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, XsB, GsB;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
     rocblas_handle blas = nullptr;
@@ -374,26 +374,99 @@ struct Net {
         if (ih != 0) throw Fail(MC_E_INVALID, "HPH^T + R is not positive definite");
     }
 
-    void enkf_analysis(int64_t m, const int64_t* gauges, const double* y, const double* R) {
-        REQUIRE(y, "observations must not be NULL");
-        if (plan.n == 0) return;
-        analysis_setup(m, gauges, y, R);
-        const int64_t ns = plan.nslots;
-        const double inv = 1.0 / (double)(E - 1);
-        // W = C2^-1 D (in place in Dn)
-        if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)m, (rocblas_int)E, C2.p,
-                             (rocblas_int)m, Dn.p, (rocblas_int)m) != rocblas_status_success)
+    // ---- staged ensemble analysis: the member-sharded form (several ranks, one per GPU; the
+    // collectives between the stages run in the caller, ensemble.py) and, with N = 1, the
+    // single-GPU mc_enkf_analysis.  Stage buffers are device pointers owned by the caller.
+    int64_t slice_size(int64_t N) const { return (plan.nslots + N - 1) / N; }
+
+    void upload_gauges(int64_t m, const int64_t* gauges) {
+        REQUIRE(m >= 1 && m < (1ll << 31) && gauges, "bad gauge arguments");
+        std::vector<int64_t> gs(m);
+        for (int64_t g = 0; g < m; ++g) {
+            REQUIRE(gauges[g] >= 0 && gauges[g] < plan.n, "gauge index out of range");
+            gs[g] = plan.pos[gauges[g]];
+        }
+        gslot.upload(gs.data(), gs.size(), stream);
+    }
+
+    // local members: HX [E][m] (gauge outflows), D [E][m] = y[g][e] - HX
+    void ens_gauges(int64_t m, const int64_t* gauges, const double* y, double* HX, double* D) {
+        REQUIRE(y && HX && D, "null argument");
+        upload_gauges(m, gauges);
+        Yb.upload(y, (size_t)(m * E), stream);
+        HIPC(mcr::launch_gauge_values(st_o.p, gslot.p, Yb.p, HX, D, m, plan.nslots, E, stream));
+    }
+
+    // local member states -> reach slices for every rank: send [N][E][S]
+    void ens_pack(int64_t N, double* send) {
+        REQUIRE(N >= 1 && send, "bad pack arguments");
+        HIPC(mcr::launch_pack_slices(st_o.p, send, plan.nslots, E, slice_size(N), N, stream));
+    }
+
+    // this rank's reach slice of ALL members (Xs [Et][S]) + all members' gauge values / innovations
+    // ([Et][m]) -> the slice of the increments G = A Z (Gs [Et][S]);  Et = E * N
+    void ens_slice_update(int64_t N, int64_t m, const double* Xs, const double* HXall,
+                          const double* Dall, const double* R, double* Gs) {
+        REQUIRE(N >= 1 && m >= 1 && Xs && HXall && Dall && R && Gs, "bad update arguments");
+        const int64_t Et = E * N, S = slice_size(N);
+        REQUIRE(Et >= 2, "the ensemble analysis needs at least 2 members");
+        const double inv = 1.0 / (double)(Et - 1);
+        // gauge anomalies HA = HX - mean over members;  C = HA HA^T / (Et-1) + R
+        HA.reserve((size_t)(m * Et));
+        HIPC(mcr::launch_mean_anomalies(HXall, HA.p, m, Et, stream));
+        C2.upload(R, (size_t)(m * m), stream);          // symmetric: row-major == column-major
+        HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
+                               stream));
+        info.reserve(1);
+        if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p, (rocblas_int)m,
+                             info.p) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
+        int32_t ih = 0;
+        HIPC(hipMemcpyAsync(&ih, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        sync();
+        if (ih != 0) throw Fail(MC_E_INVALID, "HPH^T + R is not positive definite");
+        // W = C^-1 D  (every member),  Z = HA^T W / (Et-1)  (Et x Et)
+        Dn.reserve((size_t)(m * Et));
+        HIPC(hipMemcpyAsync(Dn.p, Dall, (size_t)(m * Et) * sizeof(double),
+                            hipMemcpyDeviceToDevice, stream));
+        if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)m, (rocblas_int)Et,
+                             C2.p, (rocblas_int)m, Dn.p, (rocblas_int)m) !=
+            rocblas_status_success)
             throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
-        // Z = HA^T W / (E-1)   (E x E),   G = A Z   (ns x E): the per-member increments K D
-        Zn.reserve((size_t)(E * E));
+        Zn.reserve((size_t)(Et * Et));
+        HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, Et,
+                               stream));
+        // slice anomalies and increments G = A Z  (= K D per member)
+        An.reserve((size_t)(S * Et));
+        HIPC(mcr::launch_mean_anomalies(Xs, An.p, S, Et, stream));
+        HIPC(mcr::launch_dgemm(false, false, S, Et, Et, 1.0, An.p, S, Zn.p, Et, 0.0, Gs, S,
+                               stream));
+    }
+
+    // increments of the local members from every rank's slice (Grecv [N][E][S]) -> _apply_gain
+    void ens_unpack_apply(int64_t N, const double* Grecv) {
+        REQUIRE(N >= 1 && Grecv, "bad unpack arguments");
+        const int64_t ns = plan.nslots;
         Gn.reserve((size_t)(ns * E));
-        HIPC(mcr::launch_dgemm(true, false, E, E, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, E,
-                               stream));
-        HIPC(mcr::launch_dgemm(false, false, ns, E, E, 1.0, An.p, ns, Zn.p, E, 0.0, Gn.p, ns,
-                               stream));
+        HIPC(mcr::launch_unpack_slices(Grecv, Gn.p, ns, E, slice_size(N), N, stream));
         HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, slot_reach.p, pos.p, flags.p,
                                     in_off.p, in_list.p, ns, E, stream));
         sync();
+    }
+
+    void enkf_analysis(int64_t m, const int64_t* gauges, const double* y, const double* R) {
+        REQUIRE(y && R, "observations / R must not be NULL");
+        if (plan.n == 0) return;
+        REQUIRE(E >= 2, "the ensemble analysis needs at least 2 members");
+        const int64_t ns = plan.nslots;
+        HXb.reserve((size_t)(m * E));
+        Db.reserve((size_t)(m * E));
+        XsB.reserve((size_t)(ns * E));
+        GsB.reserve((size_t)(ns * E));
+        ens_gauges(m, gauges, y, HXb.p, Db.p);
+        ens_pack(1, XsB.p);
+        ens_slice_update(1, m, XsB.p, HXb.p, Db.p, R, GsB.p);
+        ens_unpack_apply(1, GsB.p);
     }
 
     // K = (A HA^T / (E-1)) C2^-1  as [n][m] in caller order
@@ -858,6 +931,31 @@ int mc_apply_gain(void* net, const double* gain) {
 int mc_enkf_analysis(void* net, int64_t m, const int64_t* gauges, const double* y,
                      const double* R) {
     return guarded([&] { as_net(net)->enkf_analysis(m, gauges, y, R); });
+}
+
+int mc_ens_slice_size(const void* net, int64_t nranks, int64_t* S) {
+    return guarded([&] {
+        REQUIRE(net && S && nranks >= 1, "bad argument");
+        *S = static_cast<const Net*>(net)->slice_size(nranks);
+    });
+}
+
+int mc_ens_gauges(void* net, int64_t m, const int64_t* gauges, const double* y, double* HX,
+                  double* D) {
+    return guarded([&] { as_net(net)->ens_gauges(m, gauges, y, HX, D); });
+}
+
+int mc_ens_pack(void* net, int64_t nranks, double* send) {
+    return guarded([&] { as_net(net)->ens_pack(nranks, send); });
+}
+
+int mc_ens_slice_update(void* net, int64_t nranks, int64_t m, const double* Xs,
+                        const double* HXall, const double* Dall, const double* R, double* Gs) {
+    return guarded([&] { as_net(net)->ens_slice_update(nranks, m, Xs, HXall, Dall, R, Gs); });
+}
+
+int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv) {
+    return guarded([&] { as_net(net)->ens_unpack_apply(nranks, Grecv); });
 }
 
 int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, double* K_out) {

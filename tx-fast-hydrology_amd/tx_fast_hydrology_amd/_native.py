@@ -93,6 +93,11 @@ SIGNATURES = {
     "mc_apply_gain": (_i32, [_vp, _vp]),
     "mc_enkf_analysis": (_i32, [_vp, _i64, _vp, _vp, _vp]),
     "mc_enkf_gain": (_i32, [_vp, _i64, _vp, _vp, _vp]),
+    "mc_ens_slice_size": (_i32, [_vp, _i64, ctypes.POINTER(ctypes.c_int64)]),
+    "mc_ens_gauges": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "mc_ens_pack": (_i32, [_vp, _i64, _vp]),
+    "mc_ens_slice_update": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "mc_ens_unpack_apply": (_i32, [_vp, _i64, _vp]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_get_mode": (_i32, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),

@@ -195,6 +195,35 @@ class RoutingNet:
         nat.check(nat.lib().mc_enkf_gain(self._h, m, ptr(gs), ptr(RR), ptr(K)))
         return K
 
+    # stages of the member-sharded analysis (mcroute.h; driven by ensemble.py).  Buffers are
+    # device tensors (anything with .data_ptr()) allocated by the caller on the session's stream.
+    def slice_size(self, nranks: int) -> int:
+        S = ctypes.c_int64()
+        nat.check(nat.lib().mc_ens_slice_size(self._h, int(nranks), ctypes.byref(S)))
+        return S.value
+
+    def ens_gauges(self, gauges, y, HX, D):
+        gs, yy = i64(gauges), f64(y)
+        if yy.shape != (gs.size, self.E):
+            raise ValueError("y must be [m, E]")
+        nat.check(nat.lib().mc_ens_gauges(self._h, gs.size, ptr(gs), ptr(yy),
+                                          ctypes.c_void_p(HX.data_ptr()),
+                                          ctypes.c_void_p(D.data_ptr())))
+
+    def ens_pack(self, nranks, send):
+        nat.check(nat.lib().mc_ens_pack(self._h, int(nranks), ctypes.c_void_p(send.data_ptr())))
+
+    def ens_slice_update(self, nranks, m, Xs, HXall, Dall, R, Gs):
+        RR = f64(R)
+        nat.check(nat.lib().mc_ens_slice_update(
+            self._h, int(nranks), int(m), ctypes.c_void_p(Xs.data_ptr()),
+            ctypes.c_void_p(HXall.data_ptr()), ctypes.c_void_p(Dall.data_ptr()), ptr(RR),
+            ctypes.c_void_p(Gs.data_ptr())))
+
+    def ens_unpack_apply(self, nranks, Grecv):
+        nat.check(nat.lib().mc_ens_unpack_apply(self._h, int(nranks),
+                                                ctypes.c_void_p(Grecv.data_ptr())))
+
     def load_forcing(self, xp, fp):
         xp = f64(xp)
         fp = f64(fp)
