@@ -49,6 +49,12 @@ def parse():
     ap.add_argument("--slots", type=int, default=0)
     ap.add_argument("--members", type=int, default=1,
                     help="ensemble members (BASELINE configs[2]: 64); 1 = deterministic")
+    ap.add_argument("--enkf", action="store_true",
+                    help="BASELINE configs[3]: --members is the TOTAL ensemble, sharded over the "
+                         "ranks, with the ensemble Kalman analysis at every step of the first "
+                         "2 h (hourly gauge observations)")
+    ap.add_argument("--gauges", type=int, default=500)
+    ap.add_argument("--obs-hours", type=float, default=2.0)
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -72,7 +78,7 @@ def measured_traffic(info, n, T):
     return None
 
 
-def build_workload(args, rank=0):
+def build_workload(args, rank=0, world=1):
     """Texas-scale synthetic network, coefficients, state and forcing, loaded into a RoutingNet.
     Returns (net, w): w holds the host arrays (w.x = step times of one horizon)."""
     from types import SimpleNamespace
@@ -91,11 +97,36 @@ def build_workload(args, rank=0):
     chi = (2 * K * (1 - X) - dt) / (2 * K * (1 - X) + dt)
     gamma = dt / (K * (1 - X) + dt / 2)
     rows = int(np.ceil(args.T * dt / 3600.0)) + 1
-    xp_ns, fp = synthetic.forcing(n, rows=rows, seed=1 + rank)
+    # replicas route different forcing per rank; the sharded EnKF ensemble is ONE ensemble
+    xp_ns, fp = synthetic.forcing(n, rows=rows, seed=1 if args.enkf else 1 + rank)
     xp = xp_ns.astype(float)
     x = xp[0] + dt * 1e9 * np.arange(1, args.T + 1)
     E = args.members
-    if E > 1:
+    enkf = None
+    if args.enkf:
+        if E % world or E < 2:
+            raise SystemExit("--enkf needs >= 2 members, divisible by the number of ranks")
+        El = E // world
+        o_base = o0
+        o0, fp = synthetic.ensemble(o_base, fp, E, seed=5, cols=slice(rank * El, (rank + 1) * El))
+        # gauges: non-headwater reaches (seed 7); hourly obs for the first 2 h, interpolated at
+        # every model step (da.py:71-81) -> one analysis per step; a "truth" 10 % above the
+        # initial ensemble mean plus N(0, 0.1^2) noise; R = 1e-2 I (app.py:137-139)
+        rng = np.random.default_rng(7)
+        cand = np.flatnonzero(indeg > 0)
+        gauges = np.sort(rng.choice(cand, min(args.gauges, cand.size), replace=False))
+        m = gauges.size
+        m_o = np.random.default_rng(6).lognormal(0.0, 0.3, (n, E))[gauges]
+        truth = 1.1 * (o_base[gauges, None] * m_o).mean(1)
+        R = 1e-2 * np.eye(m)
+        n_an = int(round(args.obs_hours * 3600.0 / dt))
+        obs_rng = np.random.default_rng(1000 + rank)
+        Y = [np.ascontiguousarray(truth[:, None] + rng_k)
+             for rng_k in (np.random.default_rng(100 + k).normal(0, 0.1, (m, 1)) +
+                           obs_rng.normal(0, 0.1, (m, El)) for k in range(n_an))]
+        enkf = SimpleNamespace(gauges=gauges, R=R, Y=Y, n_an=n_an, m=m, E_total=E)
+        E = El
+    elif E > 1:
         o0, fp = synthetic.ensemble(o0, fp, E, seed=5 + 7 * rank)
     i0 = np.zeros(o0.shape)
     np.add.at(i0, end, o0)                                      # muskingum.py:416-417
@@ -106,8 +137,61 @@ def build_workload(args, rank=0):
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
     w = SimpleNamespace(n=n, start=start, end=end, indeg=indeg, alpha=alpha, beta=beta, chi=chi,
-                        gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt, E=E)
+                        gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt, E=E,
+                        enkf=enkf)
     return net, w
+
+
+def workload_name(wl, E):
+    if wl.enkf is not None:
+        ek = wl.enkf
+        return (f"texas-enkf{ek.E_total} (BASELINE configs[3]): full-Texas synthetic network, "
+                f"{ek.E_total}-member ensemble, EnKF analysis at the first {ek.n_an} steps "
+                f"({ek.m} gauges), 24 h @ 300 s")
+    if E == 1:
+        return ("texas-det (BASELINE configs[1]): full-Texas synthetic network, deterministic, "
+                "24 h @ 300 s")
+    return (f"texas-ens{E} (BASELINE configs[2]): full-Texas synthetic network, {E}-member "
+            f"ensemble forecast, 24 h @ 300 s")
+
+
+def cpu_enkf_baseline(args, wl, orc):
+    """Host baseline of the EnKF horizon on a bounded sample: min(E, cores) members through the C
+    member loop (OpenMP) with a NumPy ensemble analysis at the analysis steps."""
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ek = wl.enkf
+    ms = min(wl.E, cores)
+    o = np.ascontiguousarray(wl.o0[:, :ms])
+    i = np.ascontiguousarray(wl.i0[:, :ms])
+    fp = np.ascontiguousarray(wl.fp[:, :, :ms])
+    x = wl.x
+    g = ek.gauges
+    coef = (wl.alpha, wl.beta, wl.chi, wl.gamma)
+    heads = wl.start[wl.indeg == 0]
+    reps, t = 0, 0.0
+    while t < args.cpu_seconds or reps == 0:
+        c0 = time.perf_counter()
+        for k in range(ek.n_an):
+            o, i = orc.simulate_members(wl.start, wl.end, wl.indeg, *coef, o, i, x[k:k + 1],
+                                        wl.xp, fp, threads=cores)
+            A = o - o.mean(1, keepdims=True)
+            HA = A[g]
+            W = np.linalg.solve(HA @ HA.T / (ms - 1) + ek.R, ek.Y[k][:, :ms] - o[g])
+            G = A @ (HA.T @ W) / (ms - 1)
+            for e in range(ms):
+                ig, og = orc.apply_gain(heads, wl.end, np.ascontiguousarray(G[:, e]), wl.indeg)
+                o[:, e] += og
+                i[:, e] += ig
+            o, i = np.ascontiguousarray(o), np.ascontiguousarray(i)
+        o, i = orc.simulate_members(wl.start, wl.end, wl.indeg, *coef, o, i, x[ek.n_an:], wl.xp,
+                                    fp, threads=cores)
+        t += time.perf_counter() - c0
+        reps += 1
+    return {"value": float(wl.n) * ms * args.T * reps / t, "unit": "reach·member·timesteps/s",
+            "cores": cores, "kind": "port",
+            "sample": f"{reps} x full 24 h EnKF horizon (T={args.T}, {ek.n_an} analysis steps) "
+                      f"of {ms} members on the same {wl.n}-reach network: C member loop "
+                      f"(OpenMP) + NumPy ensemble analysis + C _apply_gain, {t:.1f} s"}
 
 
 def main():
@@ -129,8 +213,20 @@ def main():
 
     # ---- workload -------------------------------------------------------------------------
     t_setup = time.time()
-    net, wl = build_workload(args, rank)
+    net, wl = build_workload(args, rank, world)
     n, x = wl.n, wl.x
+    from tx_fast_hydrology_amd import ensemble
+
+    def horizon():
+        """One bench step: a 24-h horizon (with the analysis steps of the EnKF workload)."""
+        if wl.enkf is None:
+            net.run(x)
+            return
+        ek = wl.enkf
+        for k in range(ek.n_an):       # analysis at every model step while obs exist
+            net.run(x[k:k + 1])
+            ensemble.distributed_analysis(net, ek.gauges, ek.Y[k], ek.R)
+        net.run(x[ek.n_an:])
     info = net.info
     setup_s = time.time() - t_setup
 
@@ -142,11 +238,11 @@ def main():
 
     # ---- warmup + timed region -------------------------------------------------------------
     for _ in range(args.warmup):
-        net.run(x)
+        horizon()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        net.run(x)
+        horizon()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -154,14 +250,17 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     E = wl.E
-    units = float(n) * E * args.T * args.steps * world
+    if wl.enkf is not None:            # one ensemble sharded over the ranks (strong scaling)
+        units = float(n) * wl.enkf.E_total * args.T * args.steps
+    else:                              # replicas: every rank routes its own run (weak)
+        units = float(n) * E * args.T * args.steps * world
     value = units / elapsed
 
     # ---- roofline of the dominant kernel (HIP events around every wavefront launch) --------
     net.reset_timing()
     net.set_timing(True)
     for _ in range(args.timing_runs):
-        net.run(x)
+        horizon()
     net.synchronize()
     tm = net.timing()
     net.set_timing(False)
@@ -182,7 +281,9 @@ def main():
 
     # ---- CPU baseline (serial transliteration of the reference loop, rank 0 at N=1) --------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and E > 1:
+    if rank == 0 and world == 1 and not args.no_cpu and wl.enkf is not None:
+        cpu = cpu_enkf_baseline(args, wl, orc)
+    elif rank == 0 and world == 1 and not args.no_cpu and E > 1:
         # E independent member runs over the host cores the box gives this job (OpenMP)
         cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
         ms = min(E, cores)
@@ -220,24 +321,25 @@ def main():
         line = {
             "metric": METRIC,
             "value": value,
-            "unit": "reach·timesteps/s" if E == 1 else "reach·member·timesteps/s",
+            "unit": ("reach·timesteps/s" if E == 1 and wl.enkf is None
+                     else "reach·member·timesteps/s"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if wl.enkf is not None else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": ("texas-det (BASELINE configs[1]): full-Texas synthetic "
-                                    "network, deterministic, 24 h @ 300 s") if E == 1 else
-                                   (f"texas-ens{E} (BASELINE configs[2]): full-Texas synthetic "
-                                    f"network, {E}-member ensemble forecast, 24 h @ 300 s"),
-                       "members": E,
+            "config": {"workload": workload_name(wl, E),
+                       "members": wl.enkf.E_total if wl.enkf is not None else E,
+                       "members_per_gpu": E,
                        "n_reaches": n, "outlets": int((wl.end == wl.start).sum()),
                        "max_height": info["max_height"], "T": args.T, "dt_s": wl.dt,
-                       "forcing_rows": wl.rows, "parallelism": f"replicas x{world}",
+                       "forcing_rows": wl.rows,
+                       "parallelism": (f"members sharded x{world}" if wl.enkf is not None
+                                       else f"replicas x{world}"),
                        "slots": info["slots"], "tile": info["tile"], "nwg": info["nwg"],
                        "schedule_ticks": info["gmax"] + args.T, "setup_s": round(setup_s, 2)},
             "roofline": roofline,

@@ -146,7 +146,7 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, up_more_off, ext_off, ext_g, active, wg_gmin, wg_gmax, xid;
+    DBuf<int32_t> G, up_more_off, ext_off, ext_g, wg_gmin, wg_gmax, xid;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
     DBuf<uint16_t> up_more;
@@ -165,15 +165,24 @@ struct Net {
     // and the dummy row of out-of-window ticks
     DBuf<double> O, BS, outT, dummy;
     DBuf<int64_t> in_off, in_list;   // inflow lists (plan.hpp), caller order
-    DBuf<int64_t> wbase, jbase;
+    // per-horizon schedules (active workgroups per launch, output windows), cached per T
+    struct Sched {
+        int64_t T = -1;
+        std::vector<int64_t> off;      // launch k runs list[off[k] .. off[k+1])
+        std::vector<int32_t> list;
+        DBuf<int32_t> active;
+        DBuf<int64_t> wbase, jbase;    // window base per workgroup, step-0 cell per reach
+        int64_t Otot = 0;              // output cells of one member
+        uint64_t used = 0;
+    };
+    std::vector<std::unique_ptr<Sched>> scheds;
+    Sched* cur = nullptr;              // schedule of the last run (its outputs are in O)
+    uint64_t use_clock = 0;
     DBuf<double> XS;               // external-input streams [n_ext][T]
     int64_t T_out = 0;
     bool coeffs_set = false;
 
     // active-workgroup schedule cache
-    int64_t sched_T = -1;
-    std::vector<int64_t> sched_off;
-    std::vector<int32_t> active_list;
 
     // timing
     bool timing = false;
@@ -182,14 +191,23 @@ struct Net {
     std::vector<hipEvent_t> events;
     // ensemble members (mc_net_set_members): per-member arrays are member-major on the device
     int64_t E = 1;
-    int64_t Otot = 0;              // output cells of one member (window sizes summed)
-    int64_t sched_E = 0;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
     DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, XsB, GsB;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
     rocblas_handle blas = nullptr;
+    int32_t* info_host = nullptr;      // pinned copy of the Cholesky status, checked at sync()
+    bool info_pending = false;
+
+    // pinned staging ring for asynchronous host -> device uploads (no stream sync per call)
+    struct PinSlot {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+    };
+    PinSlot pins[8];
+    int pin_next = 0;
 
     // dataflow kernel (flow.hip): mode 0 = automatic, 1 = multi-launch only, 2 = dataflow only
     int mode = 0;
@@ -212,6 +230,12 @@ struct Net {
     ~Net() {
         if (status_host) (void)hipHostFree(status_host);
         if (blas) (void)rocblas_destroy_handle(blas);
+        if (info_host) (void)hipHostFree(info_host);
+        for (PinSlot& ps : pins) {
+            if (ps.ev) (void)hipEventSynchronize(ps.ev);
+            if (ps.p) (void)hipHostFree(ps.p);
+            if (ps.ev) (void)hipEventDestroy(ps.ev);
+        }
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
     }
@@ -268,9 +292,39 @@ struct Net {
         sync();
     }
 
+    // Copy k elements host -> device without waiting for the stream: the source is staged in a
+    // pinned slot whose previous copy (8 uploads ago) must have completed.
+    template <class T>
+    void upload_async(DBuf<T>& dst, const T* src, size_t k) {
+        dst.reserve(k);
+        if (k == 0) return;
+        PinSlot& ps = pins[pin_next];
+        pin_next = (pin_next + 1) % 8;
+        if (!ps.ev) HIPC(hipEventCreateWithFlags(&ps.ev, hipEventDisableTiming));
+        HIPC(hipEventSynchronize(ps.ev));
+        const size_t bytes = k * sizeof(T);
+        if (ps.cap < bytes) {
+            if (ps.p) HIPC(hipHostFree(ps.p));
+            ps.p = nullptr;
+            HIPC(hipHostMalloc(&ps.p, bytes, hipHostMallocDefault));
+            ps.cap = bytes;
+        }
+        std::memcpy(ps.p, src, bytes);
+        HIPC(hipMemcpyAsync(dst.p, ps.p, bytes, hipMemcpyHostToDevice, stream));
+        HIPC(hipEventRecord(ps.ev, stream));
+    }
+
     // Wait for the stream; report a dataflow run whose waits gave up.
     void sync() {
         HIPC(hipStreamSynchronize(stream));
+        if (info_pending) {
+            info_pending = false;
+            if (*info_host != 0) {
+                *info_host = 0;
+                throw Fail(MC_E_INVALID, "ensemble analysis: HPH^T + R is not positive definite "
+                                         "(the state update was skipped by the solver)");
+            }
+        }
         if (status_pending) {
             status_pending = false;
             if (*status_host != 0) {
@@ -386,14 +440,14 @@ struct Net {
             REQUIRE(gauges[g] >= 0 && gauges[g] < plan.n, "gauge index out of range");
             gs[g] = plan.pos[gauges[g]];
         }
-        gslot.upload(gs.data(), gs.size(), stream);
+        upload_async(gslot, gs.data(), gs.size());
     }
 
     // local members: HX [E][m] (gauge outflows), D [E][m] = y[g][e] - HX
     void ens_gauges(int64_t m, const int64_t* gauges, const double* y, double* HX, double* D) {
         REQUIRE(y && HX && D, "null argument");
         upload_gauges(m, gauges);
-        Yb.upload(y, (size_t)(m * E), stream);
+        upload_async(Yb, y, (size_t)(m * E));
         HIPC(mcr::launch_gauge_values(st_o.p, gslot.p, Yb.p, HX, D, m, plan.nslots, E, stream));
     }
 
@@ -414,17 +468,19 @@ struct Net {
         // gauge anomalies HA = HX - mean over members;  C = HA HA^T / (Et-1) + R
         HA.reserve((size_t)(m * Et));
         HIPC(mcr::launch_mean_anomalies(HXall, HA.p, m, Et, stream));
-        C2.upload(R, (size_t)(m * m), stream);          // symmetric: row-major == column-major
+        upload_async(C2, R, (size_t)(m * m));          // symmetric: row-major == column-major
         HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
                                stream));
         info.reserve(1);
         if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p, (rocblas_int)m,
                              info.p) != rocblas_status_success)
             throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
-        int32_t ih = 0;
-        HIPC(hipMemcpyAsync(&ih, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
-        sync();
-        if (ih != 0) throw Fail(MC_E_INVALID, "HPH^T + R is not positive definite");
+        // status checked at the next sync (a failed factorisation leaves the update unusable)
+        if (!info_host)
+            HIPC(hipHostMalloc(reinterpret_cast<void**>(&info_host), sizeof(int32_t),
+                               hipHostMallocDefault));
+        HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        info_pending = true;
         // W = C^-1 D  (every member),  Z = HA^T W / (Et-1)  (Et x Et)
         Dn.reserve((size_t)(m * Et));
         HIPC(hipMemcpyAsync(Dn.p, Dall, (size_t)(m * Et) * sizeof(double),
@@ -451,7 +507,6 @@ struct Net {
         HIPC(mcr::launch_unpack_slices(Grecv, Gn.p, ns, E, slice_size(N), N, stream));
         HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, slot_reach.p, pos.p, flags.p,
                                     in_off.p, in_list.p, ns, E, stream));
-        sync();
     }
 
     void enkf_analysis(int64_t m, const int64_t* gauges, const double* y, const double* R) {
@@ -504,7 +559,6 @@ struct Net {
         dummy.reserve(mcr::kDummyPerMember * m);
         n_rows = 0;                    // forcing and outputs are per member: load again
         T_out = 0;
-        sched_T = -1;
         sync();
     }
 
@@ -526,28 +580,42 @@ struct Net {
         sync();
     }
 
-    // Per-horizon layout: active workgroups of every launch and the output windows.
+    // Per-horizon layout: active workgroups of every launch and the output windows (cached
+    // for the last few horizon lengths: assimilation alternates 1-step and long runs).
     void ensure_schedule(int64_t T) {
-        if (sched_T == T && sched_E == E) return;
-        std::vector<int32_t>& list = active_list;
-        mcr::active_schedule(plan, T, list, sched_off);
-        active.upload(list.data(), list.size(), stream);
-        std::vector<int64_t> wb(plan.nwg);
-        int64_t total = 0;
-        for (int32_t w = 0; w < plan.nwg; ++w) {
-            wb[w] = total;
-            total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * plan.p.slots;
+        Sched* hit = nullptr;
+        for (auto& sc : scheds)
+            if (sc->T == T) hit = sc.get();
+        if (!hit) {
+            if (scheds.size() >= 4) {
+                auto old = std::min_element(scheds.begin(), scheds.end(),
+                                            [](const auto& a, const auto& b) {
+                                                return a->used < b->used;
+                                            });
+                scheds.erase(old);
+            }
+            scheds.push_back(std::make_unique<Sched>());
+            hit = scheds.back().get();
+            hit->T = T;
+            mcr::active_schedule(plan, T, hit->list, hit->off);
+            hit->active.upload(hit->list.data(), hit->list.size(), stream);
+            std::vector<int64_t> wb(plan.nwg);
+            int64_t total = 0;
+            for (int32_t w = 0; w < plan.nwg; ++w) {
+                wb[w] = total;
+                total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * plan.p.slots;
+            }
+            hit->wbase.upload(wb.data(), wb.size(), stream);
+            hit->Otot = total;
+            hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
+            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, plan.p.slots,
+                                          plan.n, hit->jbase.p, stream));
+            sync();
         }
-        wbase.upload(wb.data(), wb.size(), stream);
-        Otot = total;
-        O.reserve((size_t)(total * E));
-        jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
+        hit->used = ++use_clock;
+        cur = hit;
+        O.reserve((size_t)(cur->Otot * E));
         XS.reserve(std::max<size_t>(plan.ext_src.size() * (size_t)T * E, 1));
-        HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, wbase.p, plan.p.slots, plan.n,
-                                      jbase.p, stream));
-        sync();
-        sched_T = T;
-        sched_E = E;
     }
 
     void ensure_events(size_t k) {
@@ -575,11 +643,10 @@ struct Net {
             const int last = std::max(tabh[t2].x, tabh[t2].y);
             dense = last - tabh[t].x + 1 > 3;
         }
-        stab.upload(tabh.data(), tabh.size(), stream);
-        sync();  // the host table is freed when the caller returns
+        upload_async(stab, tabh.data(), tabh.size());
         last_path = 0;
         ensure_schedule(T);
-        const int64_t nl = (int64_t)sched_off.size() - 1;
+        const int64_t nl = (int64_t)cur->off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
         if (timing) HIPC(hipEventRecord(events[2 * nl], stream));
 
@@ -604,7 +671,7 @@ struct Net {
         a.stab = stab.p;
         a.wg_gmin = wg_gmin.p;
         a.wg_gmax = wg_gmax.p;
-        a.wbase = wbase.p;
+        a.wbase = cur->wbase.p;
         a.O = O.p;
         a.BS = BS.p;
         a.dummy = dummy.p;
@@ -615,7 +682,7 @@ struct Net {
         a.ext_cap = plan.max_ext_wg;
         a.more_cap = more_cap;
         a.mF = rows * plan.nslots;
-        a.mO = Otot;
+        a.mO = cur->Otot;
         a.mX = (int64_t)plan.ext_src.size() * T;
         a.mS = plan.nslots;
         int64_t launched = 0;
@@ -659,16 +726,16 @@ struct Net {
         const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
                                                     a.tile, a.more_cap);
         if (launched == 0 && trace) {
-            trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(sched_off[nl], 1));
-            trace_wg = active_list;
+            trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(cur->off[nl], 1));
+            trace_wg = cur->list;
         }
         for (int64_t k = 0; k < nl && last_path != 2; ++k) {
-            const int64_t grid = sched_off[k + 1] - sched_off[k];
+            const int64_t grid = cur->off[k + 1] - cur->off[k];
             if (grid == 0) continue;
-            a.active = active.p + sched_off[k];
+            a.active = cur->active.p + cur->off[k];
             if (trace) {
-                a.trace = trace_buf.p + mcr::kTraceWords * sched_off[k];
-                trace_launch.resize(sched_off[k + 1], k);
+                a.trace = trace_buf.p + mcr::kTraceWords * cur->off[k];
+                trace_launch.resize(cur->off[k + 1], k);
             }
             a.kappa0 = (int32_t)(k * plan.p.tile);
             if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
@@ -677,8 +744,8 @@ struct Net {
             ++launched;
             last_path = 1;
         }
-        HIPC(mcr::launch_final_state(O.p, Otot, st_o.p, st_i.p, jbase.p, slot_reach.p,
-                                     in_off.p, in_list.p, plan.nslots, plan.p.slots, T, E,
+        HIPC(mcr::launch_final_state(O.p, cur->Otot, st_o.p, st_i.p, cur->jbase.p,
+                                     slot_reach.p, in_off.p, in_list.p, plan.nslots, plan.p.slots, T, E,
                                      stream));
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
@@ -759,8 +826,8 @@ struct Net {
         for (int c = 0; c < 2; ++c) {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_gather_steps(O.p, Otot, jbase.p, in_off.p, in_list.p, c == 1,
-                                          plan.p.slots, outT.p, n, t0, t1, E, stream));
+            HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
+                                          c == 1, plan.p.slots, outT.p, n, t0, t1, E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             sync();
@@ -776,8 +843,8 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_gather_series(O.p, Otot, jbase.p, in_off.p, in_list.p, k == 1,
-                                           plan.p.slots, outT.p, n, T_out, E, stream));
+            HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
+                                           k == 1, plan.p.slots, outT.p, n, T_out, E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             sync();
         }

@@ -140,13 +140,15 @@ def forcing(n, rows=25, seed=1, start="2024-05-01T00:00:00", freq="1h"):
     return idx.asi8.copy(), vals
 
 
-def ensemble(o0, fp, members, seed=5):
+def ensemble(o0, fp, members, seed=5, cols=None):
     """Ensemble inputs: member forcing = base x lognormal(0, 0.3) multiplier per
     (reach, member), constant in time (seed 5); initial state the same way (seed 6).
-    Returns (o0 [n][E], fp [rows][n][E]) in the member-innermost layout of mcroute.h."""
+    Returns (o0 [n][E], fp [rows][n][E]) in the member-innermost layout of mcroute.h; `cols`
+    (a slice of the members) gives one rank's share of the same ensemble."""
     n = o0.size
-    m_f = np.random.default_rng(seed).lognormal(0.0, 0.3, (n, members))
-    m_o = np.random.default_rng(seed + 1).lognormal(0.0, 0.3, (n, members))
+    cols = slice(0, members) if cols is None else cols
+    m_f = np.random.default_rng(seed).lognormal(0.0, 0.3, (n, members))[:, cols]
+    m_o = np.random.default_rng(seed + 1).lognormal(0.0, 0.3, (n, members))[:, cols]
     fpe = np.ascontiguousarray(fp[:, :, None] * m_f[None, :, :])
     return np.ascontiguousarray(o0[:, None] * m_o), fpe
 
