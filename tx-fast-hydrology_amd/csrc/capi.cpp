@@ -163,7 +163,7 @@ struct Net {
     // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
     // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
     // and the dummy row of out-of-window ticks
-    DBuf<double> O, BS, outT, dummy;
+    DBuf<double> O, outT, dummy;
     DBuf<int64_t> in_off, in_list;   // inflow lists (plan.hpp), caller order
     // per-horizon schedules (active workgroups per launch, output windows), cached per T
     struct Sched {
@@ -269,7 +269,6 @@ struct Net {
         in_off.upload(plan.in_off.data(), plan.in_off.size(), stream);
         in_list.upload(plan.in_list.data(), plan.in_list.size(), stream);
         in_list.reserve(1);
-        BS.reserve(2 * (size_t)std::max<int64_t>(plan.nslots, 1));
         wg_gmin.upload(plan.wg_gmin.data(), plan.wg_gmin.size(), stream);
         wg_gmax.upload(plan.wg_gmax.data(), plan.wg_gmax.size(), stream);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
@@ -555,7 +554,6 @@ struct Net {
             b->reserve(ns * m);
             HIPC(hipMemsetAsync(b->p, 0, ns * m * sizeof(double), stream));
         }
-        BS.reserve(2 * ns * m);
         dummy.reserve(mcr::kDummyPerMember * m);
         n_rows = 0;                    // forcing and outputs are per member: load again
         T_out = 0;
@@ -673,7 +671,6 @@ struct Net {
         a.wg_gmax = wg_gmax.p;
         a.wbase = cur->wbase.p;
         a.O = O.p;
-        a.BS = BS.p;
         a.dummy = dummy.p;
         a.nslots = plan.nslots;
         a.n_rows = (int32_t)rows;
@@ -744,9 +741,6 @@ struct Net {
             ++launched;
             last_path = 1;
         }
-        HIPC(mcr::launch_final_state(O.p, cur->Otot, st_o.p, st_i.p, cur->jbase.p,
-                                     slot_reach.p, in_off.p, in_list.p, plan.nslots, plan.p.slots, T, E,
-                                     stream));
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
             HIPC(hipEventSynchronize(events[2 * nl + 1]));

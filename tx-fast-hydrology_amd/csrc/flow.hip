@@ -360,6 +360,8 @@ void wavefront_flow(WaveArgs a) {
         f1 = g1;
         f2 = g2;
     }
+    a.st_o[d] = routed ? op : 0.0;                      // session state after the horizon
+    a.st_i[d] = ip;
     if (a.trace && tid == 0) {
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
         rec[0] = t_start;

@@ -77,7 +77,6 @@ void wavefront_det(WaveArgs a) {
     const double* Fm = a.F + mem * a.mF;
     double* Om = a.O + mem * a.mO;
     double* XSm = a.XS + mem * a.mX;
-    double2* BSm = reinterpret_cast<double2*>(a.BS) + mem * a.mS;
     double* dum = a.dummy + mem * kDummyPerMember;
     const int64_t d = (int64_t)w * SLOTS + tid;
     const int T = a.T;
@@ -93,11 +92,9 @@ void wavefront_det(WaveArgs a) {
     const int t_first = k0 - Gr;                        // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
     const int G = live ? Gr : (1 << 29);                // never active when not live
-    // the workgroup ran in the previous launch: its lanes' state is in the boundary buffer
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
-    const bool from_bs = k0 > gminw;
     const int64_t wb = a.wbase[w];
-    const double2 bs = BSm[from_bs ? d : 0];
+    // the state after the last step this lane ran in an earlier launch (or the initial state)
     const double st_o = a.st_o[mem * a.mS + d], st_i = a.st_i[mem * a.mS + d];
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
     const int cnt = live ? a.up_cnt[d] : 0;
@@ -152,8 +149,8 @@ void wavefront_det(WaveArgs a) {
     const int ngrp = live ? (more_end - more) / kUpGroup : 0;       // this lane's groups
     const unsigned gofs = XM + (unsigned)(kUpGroup + more) * 4;       // its first group
 
-    double op = from_bs ? bs.x : st_o;
-    double ip = from_bs ? bs.y : st_i;
+    double op = st_o;
+    double ip = st_i;
     // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
     xbp[tid * 2 + ((k0 - 1) & 1)] = op;
     if (tid < 2) xbp[SLOTS * 2 + tid] = 0.0;            // zero slot for unused upstream codes
@@ -291,8 +288,11 @@ void wavefront_det(WaveArgs a) {
         f1 = g1;
         f2 = g2;
     }
-    // state for the next launch of this workgroup (lanes that did not run keep theirs)
-    BSm[d] = make_double2(op, ip);
+    // state for the next launch (lanes that did not run keep theirs); never-processed reaches
+    // hold o = 0 as in the reference's fresh o_t_next
+    const int64_t ds = (int64_t)blockIdx.y * a.mS + (int64_t)w * SLOTS + threadIdx.x;
+    a.st_o[ds] = routed ? op : 0.0;
+    a.st_i[ds] = ip;
     if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
@@ -367,25 +367,6 @@ __device__ __forceinline__ double inflow_at(const double* __restrict__ O,
     double s = 0.0;
     for (int64_t k = in_off[j]; k < in_off[j + 1]; ++k) s = s + O[jbase[in_list[k]] + t * slots];
     return s;
-}
-
-__global__ void final_state(const double* __restrict__ O, int64_t mO, double* __restrict__ st_o,
-                            double* __restrict__ st_i, const int64_t* __restrict__ jbase,
-                            const int64_t* __restrict__ slot_reach,
-                            const int64_t* __restrict__ in_off,
-                            const int64_t* __restrict__ in_list, int64_t nslots, int slots,
-                            int64_t T, int64_t E) {
-    const int64_t total = nslots * E;
-    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
-         x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = x / nslots;
-        const int64_t j = slot_reach[x - e * nslots];
-        if (j >= 0) {
-            const double* Oe = O + e * mO;
-            st_o[x] = Oe[jbase[j] + (T - 1) * slots];
-            st_i[x] = inflow_at(Oe, jbase, in_off, in_list, j, T - 1, slots);
-        }
-    }
 }
 
 // out[t - t0][j][e]: consecutive threads take consecutive (j, e) (coalesced writes)
@@ -484,15 +465,6 @@ hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32
     if (n > 0)
         hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
                            slots, n, jbase);
-    return hipGetLastError();
-}
-
-hipError_t launch_final_state(const double* O, int64_t mO, double* st_o, double* st_i,
-                              const int64_t* jbase, const int64_t* slot_reach,
-                              const int64_t* in_off, const int64_t* in_list, int64_t nslots,
-                              int slots, int64_t T, int64_t E, hipStream_t s) {
-    hipLaunchKernelGGL(final_state, grid_for(nslots * E, 256), 256, 0, s, O, mO, st_o, st_i,
-                       jbase, slot_reach, in_off, in_list, nslots, slots, T, E);
     return hipGetLastError();
 }
 

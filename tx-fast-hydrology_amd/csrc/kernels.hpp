@@ -57,17 +57,19 @@ struct WaveArgs {
     const double* beta;
     const double* chi;
     const double* gamma;
-    const double* st_o;           // state at step -1 (o_t_next before the horizon) [nslots]
-    const double* st_i;
+    // routing state {o_t_next, i_t_next} [nslots]: read at a workgroup's first tick of a
+    // launch, written back at its last, so it holds step t_last of the previous launch and the
+    // final state after the horizon (the session state, no separate gather)
+    double* st_o;
+    double* st_i;
     const double* F;              // forcing rows in slot order [n_rows][nslots]
     const int4* stab;             // per step {row_lo, row_hi (-1 = copy row_lo), frac (f64)}
     const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
     const int32_t* wg_gmax;
     const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
     double* O;                    // workgroup windows of outflows (see above)
-    double* BS;                   // [nslots][2] {o, i} of each slot at the end of a launch
     // ensemble members (grid y; multi-launch kernel): element strides between members of the
-    // member-major arrays F, O, XS and of st_o / st_i / BS (in slots)
+    // member-major arrays F, O, XS and of st_o / st_i (in slots)
     int64_t mF, mO, mX, mS;
     double* XS;                   // external-input streams [n_ext][T]: step t of each source
     double* dummy;                // >= 2 * 1024 doubles: cells of out-of-window ticks
@@ -125,12 +127,6 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
                                const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
                                hipStream_t s);
-// state after the last step: st[e][d] = step T-1 of slot d of member e (inflow recomputed
-// from O); member e's windows start at O + e * mO
-hipError_t launch_final_state(const double* O, int64_t mO, double* st_o, double* st_i,
-                              const int64_t* jbase, const int64_t* slot_reach,
-                              const int64_t* in_off, const int64_t* in_list, int64_t nslots,
-                              int slots, int64_t T, int64_t E, hipStream_t s);
 // Output gathers (caller order, member innermost).  inflow = false: outflow O; true: the inflow
 // of reach j, summed from O over its inflow list.
 // step-major out[t - t0][j][e] for t in [t0, t1)
