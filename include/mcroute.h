@@ -57,7 +57,7 @@ typedef struct mc_plan_info {
     int32_t gmax;         /* schedule length without the horizon: ticks = gmax + T */
     int32_t max_height;   /* longest upstream path (network depth - 1) */
     int32_t max_ext_wg;
-    int64_t n_up_more;    /* upstream codes beyond the 4 kept in registers */
+    int64_t n_partial;    /* partial-sum nodes (reaches with more than 4 routed upstreams) */
     int64_t n_ext;        /* cross-cluster inputs over all workgroups */
 } mc_plan_info;
 
@@ -76,11 +76,12 @@ int mc_plan_get_info(const void* plan, mc_plan_info* info);
 /* Any output pointer may be NULL.  rank/pos: [n]; G/slot_reach: [nslots]. */
 int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
                    int64_t* slot_reach);
-/* Schedule links (test / inspection): flags, up_cnt, up4 [nslots]; up_more_off [nslots+1];
- * up_more [n_up_more]; ext_off [nwg+1]; ext_src, ext_g [n_ext].  Any pointer may be NULL. */
+/* Schedule links (test / inspection): flags, up_cnt, up4 [nslots] (at most 4 upstream codes
+ * per slot; flags 3 = partial-sum slot); ext_off [nwg+1]; ext_src, ext_g [n_ext] (ext_src is
+ * the source's output row: its reach index, or n + slot for a partial-sum slot).  Any pointer
+ * may be NULL. */
 int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint64_t* up4,
-                         int32_t* up_more_off, uint16_t* up_more, int32_t* ext_off,
-                         int64_t* ext_src, int32_t* ext_g);
+                         int32_t* ext_off, int64_t* ext_src, int32_t* ext_g);
 /* Launch schedule for a horizon of T steps: launch k covers ticks [k*tile, (k+1)*tile) and
  * runs workgroups list[off[k] .. off[k+1]).  Call with off/list NULL to get the sizes
  * (*n_launch, *n_list); then with arrays of at least n_launch+1 / n_list entries. */

@@ -8,7 +8,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 PKG=tx-fast-hydrology_amd
 OUT=$PKG/tx_fast_hydrology_amd/lib/exp
-VARIANTS="base:-DMCR_EXP_NONE nostores:-DMCR_EXP_NO_STORES=1 nooverflow:-DMCR_EXP_NO_OVERFLOW=1 nobarrier:-DMCR_EXP_NO_BARRIER=1 noq:-DMCR_EXP_NO_Q=1 ${EXTRA_VARIANTS:-}"
+VARIANTS="${VARIANTS:-base:-DMCR_EXP_NONE nostores:-DMCR_EXP_NO_STORES=1 nobarrier:-DMCR_EXP_NO_BARRIER=1 noq:-DMCR_EXP_NO_Q=1} ${EXTRA_VARIANTS:-}"
 if [ "${1:-run}" = build ]; then
   mkdir -p $OUT
   for v in $VARIANTS; do

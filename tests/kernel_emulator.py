@@ -12,7 +12,7 @@ bit-for-bit against the oracle without a GPU:
 """
 import numpy as np
 
-ROUTED, UNROUTED = 1, 2
+ROUTED, UNROUTED, PSUM = 1, 2, 3
 EXT = 0x8000
 
 
@@ -65,11 +65,10 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
     codes = np.zeros((nslots, max(maxc, 1)), np.int64)
     for c in range(min(maxc, 4)):
         codes[:, c] = (ln["up4"] >> np.uint64(16 * c)).astype(np.int64) & 0xFFFF
-    for d in np.flatnonzero(cnt > 4):
-        a = ln["up_more_off"][d]
-        codes[d, 4:cnt[d]] = ln["up_more"][a:a + cnt[d] - 4]
-    O = np.full((n, T), np.nan)
-    I = np.full((n, T), np.nan)
+    # output rows: reaches, then one row per slot for partial-sum nodes (ext_src convention)
+    orow = np.where(real, sr, n + np.arange(nslots))
+    O = np.full((n + nslots, T), np.nan)
+    I = np.full((n + nslots, T), np.nan)
 
     for k in range(len(off) - 1):
         k0 = k * tile
@@ -84,7 +83,7 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
                 ok = (tt >= 0) & (tt < T)
                 xe[e, ok] = Os[ln["ext_src"][e0 + e], tt[ok]]
             g, f = G[d], fl[d]
-            row = sr[d]
+            row = orow[d]
             tf = k0 - g
             live = (f != 0) & (tf < T) & (tf + tile > 0)
             rest = (f != 0) & (tf <= T) & (tf + tile > 0)
@@ -152,9 +151,10 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
                 q = np.where(cp, f_lo, ww0 * f_lo + ww1 * f_hi)
                 o = np.where(f == ROUTED, 0.0 + (((al[d] * Iv + be[d] * ip) + ch[d] * op)
                                                   + ga[d] * q), 0.0)
+                o = np.where(f == PSUM, Iv, o)
                 xb[kk & 1] = np.where(act, o, xb[kk & 1])
                 O[row[act], t[act]] = o[act]
                 I[row[act], t[act]] = Iv[act]
                 op = np.where(act, o, op)
                 ip = np.where(act, Iv, ip)
-    return O, I
+    return O[:n], I[:n]

@@ -39,6 +39,26 @@ def test_emulator_matches_oracle(n, p_chain, slots, tile, T, rows):
     assert np.array_equal(I.T, want_i)
 
 
+@pytest.mark.parametrize("slots,tile", [(64, 1), (64, 8), (128, 16)])
+def test_emulator_partial_sums_high_fan_in(slots, tile):
+    """Reaches with up to 30 routed upstreams read chains of partial-sum slots; the fold must
+    stay bit-identical to the reference's rank-ordered accumulation."""
+    rng = np.random.default_rng(slots + tile)
+    end = synthetic.fan_in_forest(1500, rng)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=5)
+    start, indeg, coef, i0 = _case(end, K, X, 300.0, o0)
+    assert indeg.max() > 8
+    xp, fp = synthetic.forcing(n, rows=4, seed=6)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 41)
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile)
+    assert plan.info["n_partial"] > 0
+    O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
+    assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
+
+
 def test_emulator_river_network_and_golden_edges(golden):
     end = synthetic.river_network(4000, 6, 150, np.random.default_rng(9))
     n = end.size

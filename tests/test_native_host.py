@@ -46,6 +46,7 @@ def _replay_rank(heads, endnodes, indegree):
 
 
 def _check_plan(endnodes, indegree, heads, **kw):
+    """Plan invariants; returns (info, export)."""
     P = Plan(endnodes, indegree, heads, **kw)
     info = P.info
     ex = P.export()
@@ -58,18 +59,31 @@ def _check_plan(endnodes, indegree, heads, **kw):
     G[ex["slot_reach"][ex["slot_reach"] >= 0]] = ex["G"][ex["slot_reach"] >= 0]
     slots = info["slots"]
     tile = info["tile"]
-    wg = ex["pos"] // slots
-    # schedule: consumer runs after producer; same workgroup & unit slack, or slack >= tile
+    # schedule: every consumer runs after its producer
     rank = ex["rank"]
     for u in range(n):
         e = endnodes[u]
-        if rank[u] < 0 or e == u:
-            continue
-        slack = G[e] - G[u]
-        assert slack >= 1
-        assert slack == 1 or slack >= tile, (u, e, slack)
-        if slack == 1 and tile > 1:
-            assert wg[u] == wg[e]
+        if rank[u] >= 0 and e != u:
+            assert G[e] - G[u] >= 1
+    # node level (reaches and partial-sum slots): at most 4 inputs per slot; an input from
+    # the same workgroup has unit slack, one from another workgroup slack >= tile
+    ln = P.export_links()
+    Gs = ex["G"].astype(np.int64)
+    assert (ln["up_cnt"] <= 4).all()
+    assert int((ln["flags"] == 3).sum()) == info["n_partial"]
+    assert (ex["slot_reach"][ln["flags"] == 3] == -1).all()
+    for d in np.flatnonzero(ln["up_cnt"]):
+        w = d // slots
+        for c in range(int(ln["up_cnt"][d])):
+            code = int((ln["up4"][d] >> np.uint64(16 * c)) & np.uint64(0xFFFF))
+            if code & 0x8000:
+                row = int(ln["ext_src"][ln["ext_off"][w] + (code & 0x7FFF)])
+                src = ex["pos"][row] if row < n else row - n
+                assert Gs[d] - Gs[src] >= tile, (d, src)
+                assert ln["ext_g"][ln["ext_off"][w] + (code & 0x7FFF)] == Gs[d]
+            else:
+                src = w * slots + code
+                assert Gs[d] - Gs[src] == 1, (d, src)
     assert info["gmax"] == G.max() if n else True
     return info, ex
 
@@ -83,6 +97,16 @@ def test_plan_invariants_random(slots, tile):
         deg = orc.compute_indegree(np.arange(n), end)
         heads = np.flatnonzero(deg == 0)
         _check_plan(end, deg, heads, slots=slots, tile=tile)
+
+
+@pytest.mark.parametrize("slots,tile", [(64, 1), (64, 8), (128, 16), (256, 32)])
+def test_plan_partial_sums_high_fan_in(slots, tile):
+    rng = np.random.default_rng(slots * 3 + tile)
+    end = synthetic.fan_in_forest(2500, rng)
+    deg = orc.compute_indegree(np.arange(end.size), end)
+    assert deg.max() > 4
+    info, ex = _check_plan(end, deg, np.flatnonzero(deg == 0), slots=slots, tile=tile)
+    assert info["n_partial"] > 0
 
 
 def test_plan_golden_edge_topologies(golden):

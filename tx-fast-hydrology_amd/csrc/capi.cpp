@@ -110,7 +110,7 @@ void fill_info(const mcr::Plan& P, mc_plan_info* info) {
     info->gmax = P.gmax;
     info->max_height = P.max_height;
     info->max_ext_wg = P.max_ext_wg;
-    info->n_up_more = (int64_t)P.up_more.size();
+    info->n_partial = P.n_partial;
     info->n_ext = (int64_t)P.ext_src.size();
 }
 
@@ -146,12 +146,10 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, up_more_off, ext_off, ext_g, wg_gmin, wg_gmax, xid;
+    DBuf<int32_t> G, ext_off, ext_g, wg_gmin, wg_gmax, xid;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
-    DBuf<uint16_t> up_more;
     DBuf<int64_t> slot_reach, pos;
-    int32_t more_cap = 0;          // max overflow upstream codes of one workgroup
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
     // forcing (slot order) and single-step forcing
@@ -254,15 +252,8 @@ struct Net {
         flags.upload(plan.flags.data(), ns, stream);
         up_cnt.upload(plan.up_cnt.data(), ns, stream);
         up4.upload(plan.up4.data(), ns, stream);
-        up_more_off.upload(plan.up_more_off.data(), plan.up_more_off.size(), stream);
-        up_more.upload(plan.up_more.data(), plan.up_more.size(), stream);
         slot_reach.upload(plan.slot_reach.data(), ns, stream);
         ext_off.upload(plan.ext_off.data(), plan.ext_off.size(), stream);
-        for (int32_t w = 0; w < plan.nwg; ++w) {
-            const int64_t a0 = plan.up_more_off[(int64_t)w * plan.p.slots];
-            const int64_t a1 = plan.up_more_off[(int64_t)(w + 1) * plan.p.slots];
-            more_cap = std::max<int32_t>(more_cap, (int32_t)(a1 - a0));
-        }
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
         xid.upload(plan.xid.data(), plan.xid.size(), stream);
@@ -340,7 +331,7 @@ struct Net {
         if (mode == 1) return false;
         const int S = plan.p.slots;
         const size_t xg = plan.ext_src.size() * (size_t)T * 16;
-        lds = mcr::flow_lds_bytes(S, (int)T, plan.max_ext_wg, more_cap);
+        lds = mcr::flow_lds_bytes(S, (int)T, plan.max_ext_wg);
         bool ok = (S == 64 || S == 128 || S == 192 || S == 256 || S == 384 || S == 448) &&
                   plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
                   T <= mcr::kFlowMaxT && xg < (size_t(1) << 31) && lds <= 160 * 1024;
@@ -653,8 +644,6 @@ struct Net {
         a.flags = flags.p;
         a.up_cnt = up_cnt.p;
         a.up4 = up4.p;
-        a.up_more_off = up_more_off.p;
-        a.up_more = up_more.p;
         a.ext_off = ext_off.p;
         a.xid = xid.p;
         a.XS = XS.p;
@@ -677,7 +666,6 @@ struct Net {
         a.T = (int32_t)T;
         a.tile = plan.p.tile;
         a.ext_cap = plan.max_ext_wg;
-        a.more_cap = more_cap;
         a.mF = rows * plan.nslots;
         a.mO = cur->Otot;
         a.mX = (int64_t)plan.ext_src.size() * T;
@@ -721,7 +709,7 @@ struct Net {
         }
         a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
         const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
-                                                    a.tile, a.more_cap);
+                                                    a.tile);
         if (launched == 0 && trace) {
             trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(cur->off[nl], 1));
             trace_wg = cur->list;
@@ -905,8 +893,7 @@ int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
 }
 
 int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint64_t* up4,
-                         int32_t* up_more_off, uint16_t* up_more, int32_t* ext_off,
-                         int64_t* ext_src, int32_t* ext_g) {
+                         int32_t* ext_off, int64_t* ext_src, int32_t* ext_g) {
     return guarded([&] {
         REQUIRE(plan, "null plan");
         const mcr::Plan& P = *static_cast<const mcr::Plan*>(plan);
@@ -916,8 +903,6 @@ int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint
         cp(flags, P.flags);
         cp(up_cnt, P.up_cnt);
         cp(up4, P.up4);
-        cp(up_more_off, P.up_more_off);
-        cp(up_more, P.up_more);
         cp(ext_off, P.ext_off);
         cp(ext_src, P.ext_src);
         cp(ext_g, P.ext_g);

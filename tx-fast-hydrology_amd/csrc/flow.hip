@@ -25,8 +25,8 @@
 #ifndef MCR_EXP_NO_STORES
 #define MCR_EXP_NO_STORES 0
 #endif
-#ifndef MCR_EXP_NO_OVERFLOW
-#define MCR_EXP_NO_OVERFLOW 0
+#ifndef MCR_EXP_PAIR_STORES
+#define MCR_EXP_PAIR_STORES 0
 #endif
 #ifndef MCR_EXP_NO_Q
 #define MCR_EXP_NO_Q 0
@@ -141,7 +141,7 @@ struct Helper {
 
 // LDS layout (bytes): XB [SLOTS + 1][2] f64 | FR [SLOTS][3] f64 | TAB [T] int4 (whole step table)
 //   | XE [2][ext_cap][kChunk] f64 (ring of external inputs, one slot per chunk parity)
-//   | XM [4 + more_cap] u32 (overflow upstream addresses) | EG [kFlowMaxExt] i32 (consumer G)
+//   | EG [kFlowMaxExt] i32 (consumer G)
 template <int SLOTS, bool DENSE>
 __global__ __launch_bounds__(SLOTS + kHelperLanes) __attribute__((amdgpu_waves_per_eu(4)))
 void wavefront_flow(WaveArgs a) {
@@ -152,11 +152,9 @@ void wavefront_flow(WaveArgs a) {
     const int T = a.T;
     const unsigned XE = TAB + (unsigned)a.table_cap * 16;
     const unsigned XSLOT = (unsigned)a.ext_cap * kChunk * 8;
-    const unsigned XM = XE + 2 * XSLOT;
-    const unsigned EG = XM + 4u * (unsigned)(a.more_cap + kUpGroup);
+    const unsigned EG = XE + 2 * XSLOT;
     double* xbp = reinterpret_cast<double*>(lds + XB);
     int4* tab = reinterpret_cast<int4*>(lds + TAB);
-    unsigned* xm = reinterpret_cast<unsigned*>(lds + XM);
 
     const int tid = threadIdx.x;
     const int nthr = SLOTS + kHelperLanes;
@@ -167,20 +165,10 @@ void wavefront_flow(WaveArgs a) {
     const int wend = gmaxw + T;                         // end of its tick window
     const int e0 = a.ext_off[w];
     const int next = a.ext_off[w + 1] - e0;
-    const int m0 = a.up_more_off[(int64_t)w * SLOTS];
-    const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
     const auto xg = __builtin_amdgcn_make_buffer_rsrc(a.XG, (short)0, (int)a.xg_bytes, 0x00020000);
 
-    // ---- shared prologue: step table, overflow addresses, consumer ticks of external inputs
+    // ---- shared prologue: step table, consumer ticks of external inputs
     for (int idx = tid; idx < T; idx += nthr) tab[idx] = a.stab[idx];
-    for (int idx = tid; idx < nm + kUpGroup; idx += nthr) {
-        unsigned ent = XB + (unsigned)SLOTS * 16;
-        if (idx >= kUpGroup) {
-            const unsigned code = a.up_more[m0 + idx - kUpGroup];
-            ent = (code & kExtBit) ? ((XE + (code & 0x7fffu) * kChunk * 8) | 1u) : XB + code * 16;
-        }
-        xm[idx] = ent;
-    }
     for (int idx = tid; idx < next; idx += nthr)
         reinterpret_cast<int*>(lds + EG)[idx] = a.ext_g[e0 + idx];
     if (tid < 2) xbp[SLOTS * 2 + tid] = 0.0;
@@ -229,13 +217,12 @@ void wavefront_flow(WaveArgs a) {
     const int Gr = a.G[d];
     const bool real = fl != kSlotPad;
     const bool routed = fl == kSlotRouted;
+    const bool psum = fl == kSlotSum;                   // partial-sum node: outputs I
     const int G = real ? Gr : (1 << 29);                // padding lanes are never active
     const double st_o = a.st_o[d], st_i = a.st_i[d];
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
     const int cnt = real ? a.up_cnt[d] : 0;
     const uint64_t up4 = a.up4[d];
-    const int more = a.up_more_off[d] - m0;
-    const int more_end = a.up_more_off[d + 1] - m0;
     const int xsid = a.xid[d];
     const int64_t wb = a.wbase[w];
 
@@ -245,8 +232,6 @@ void wavefront_flow(WaveArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();                                    // LDS tables staged
 
-    const int ngrp = real ? (more_end - more) / kUpGroup : 0;
-    const unsigned gofs = XM + (unsigned)(kUpGroup + more) * 4;
     unsigned ubase[kUpInline], uinc[kUpInline];
 #pragma unroll
     for (int u = 0; u < kUpInline; ++u) {
@@ -256,9 +241,6 @@ void wavefront_flow(WaveArgs a) {
         uinc[u] = ext ? 16u : 0u;
     }
     const bool any3 = __any(cnt > 2);
-    int ngw = 0;
-    while (__any(ngw < ngrp)) ++ngw;
-    if (MCR_EXP_NO_OVERFLOW) ngw = 0;
     const unsigned own = XB + (unsigned)tid * 16;
 
     int rb, nr;
@@ -274,6 +256,7 @@ void wavefront_flow(WaveArgs a) {
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
+    double pv = 0.0;                                    // MCR_EXP_PAIR_STORES only
     for (int kc = kb; kc < wend; kc += kChunk) {
         const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
         double* frl = reinterpret_cast<double*>(lds + FR) + tid * 3;
@@ -318,35 +301,35 @@ void wavefront_flow(WaveArgs a) {
             const int k = kc + i;
             const int t = k - G;
             const bool act = (unsigned)t < (unsigned)T;
-            double I = 0.0 + lds_f64(lds, m[0] + rd);
+            double I = lds_f64(lds, m[0] + rd);   // published values are never -0.0
             I = I + lds_f64(lds, m[1] + rd);
             if (any3) {
                 I = I + lds_f64(lds, m[2] + rd);
                 I = I + lds_f64(lds, m[3] + rd);
             }
-            const unsigned sx = sb + 8u * (unsigned)i;
-            for (int g = 0; g < ngw; ++g) {
-                const uint4 e = *reinterpret_cast<const uint4*>(
-                    lds + (g < ngrp ? gofs + 16u * g : XM));
-                const unsigned a0 = (e.x & ~1u) + ((e.x & 1u) ? sx : rd);
-                const unsigned a1 = (e.y & ~1u) + ((e.y & 1u) ? sx : rd);
-                const unsigned a2 = (e.z & ~1u) + ((e.z & 1u) ? sx : rd);
-                const unsigned a3 = (e.w & ~1u) + ((e.w & 1u) ? sx : rd);
-                const double v0 = lds_f64(lds, a0), v1 = lds_f64(lds, a1);
-                const double v2 = lds_f64(lds, a2), v3 = lds_f64(lds, a3);
-                I = I + v0;
-                I = I + v1;
-                I = I + v2;
-                I = I + v3;
-            }
-            const double ov = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[i]);
+            const double rv = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[i]);
+            const double ov = psum ? I : rv;
             *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = ov;
             op = act ? ov : op;
             ip = act ? I : ip;
             const bool inwin = k >= gminw && k < wend;
             const int64_t row = inwin ? wb + (int64_t)(k - gminw) * SLOTS : 0;
             double* orow = inwin ? a.O + row : a.dummy;
-            if (!MCR_EXP_NO_STORES) orow[tid] = routed ? ov : 0.0;
+            if (MCR_EXP_PAIR_STORES) {
+                // timing experiment only: one 16-byte store per lane every second tick
+                const double sv = routed ? ov : 0.0;
+                if (i & 1) {
+                    const int kp = k - 1 >= gminw ? k - 1 : gminw;
+                    const int r0 = (kp - gminw) & ~1;
+                    const bool fits = inwin && r0 + 2 <= wend - gminw;
+                    const int64_t prow = wb + (int64_t)r0 * SLOTS;
+                    double2* pr = reinterpret_cast<double2*>(fits ? a.O + prow : a.dummy);
+                    pr[tid] = make_double2(pv, sv);
+                }
+                pv = sv;
+            } else if (!MCR_EXP_NO_STORES) {
+                orow[tid] = routed ? ov : 0.0;
+            }
             if (xsrc && act) {
                 const uint64_t bits = (uint64_t)__double_as_longlong(ov);
                 const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
@@ -360,7 +343,7 @@ void wavefront_flow(WaveArgs a) {
         f1 = g1;
         f2 = g2;
     }
-    a.st_o[d] = routed ? op : 0.0;                      // session state after the horizon
+    a.st_o[d] = routed || psum ? op : 0.0;              // session state after the horizon
     a.st_i[d] = ip;
     if (a.trace && tid == 0) {
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;

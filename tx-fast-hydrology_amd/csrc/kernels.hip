@@ -25,9 +25,6 @@
 #ifndef MCR_EXP_NO_STORES
 #define MCR_EXP_NO_STORES 0
 #endif
-#ifndef MCR_EXP_NO_OVERFLOW
-#define MCR_EXP_NO_OVERFLOW 0
-#endif
 #ifndef MCR_EXP_NO_BARRIER
 #define MCR_EXP_NO_BARRIER 0
 #endif
@@ -49,8 +46,6 @@ constexpr int kHalf = kChunk;  // ticks whose lateral inflow is formed in one bu
 //   FR  [SLOTS][3]     f64  the lane's forcing rows rb .. rb + 2 of the current chunk
 //   TAB [table_cap]    int4 step-table window {row_lo, row_hi, frac}
 //   XE  [ext_cap][tile] f64 external inputs of this launch
-//   XM  [4 + more_cap] u32  overflow upstreams (5th and later) as resolved LDS byte addresses,
-//                           bit 0 set for external inputs; group 0 is all zero-slot addresses
 // DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
@@ -63,11 +58,9 @@ void wavefront_det(WaveArgs a) {
     constexpr unsigned FR = XB + (SLOTS + 1) * 16;
     constexpr unsigned TAB = FR + SLOTS * 24;
     const unsigned XE = TAB + (unsigned)a.table_cap * 16;
-    const unsigned XM = XE + (unsigned)a.ext_cap * (unsigned)tile * 8;
     double* xbp = reinterpret_cast<double*>(lds + XB);
     int4* tab = reinterpret_cast<int4*>(lds + TAB);
     double* xe = reinterpret_cast<double*>(lds + XE);
-    unsigned* xm = reinterpret_cast<unsigned*>(lds + XM);
 
     const int tid = threadIdx.x;
     const int64_t t_start = a.trace ? wall_clock64() : 0;
@@ -89,6 +82,7 @@ void wavefront_det(WaveArgs a) {
     const int Gr = a.G[d];
     const bool real = fl != kSlotPad;
     const bool routed = fl == kSlotRouted;
+    const bool psum = fl == kSlotSum;                   // partial-sum node: outputs I
     const int t_first = k0 - Gr;                        // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
     const int G = live ? Gr : (1 << 29);                // never active when not live
@@ -99,10 +93,6 @@ void wavefront_det(WaveArgs a) {
     const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
     const int cnt = live ? a.up_cnt[d] : 0;
     const uint64_t up4 = a.up4[d];
-    const int m0 = a.up_more_off[(int64_t)w * SLOTS];
-    const int nm = a.up_more_off[(int64_t)w * SLOTS + SLOTS] - m0;
-    const int more = a.up_more_off[d] - m0;
-    const int more_end = a.up_more_off[d + 1] - m0;
     const int xsid = a.xid[d];
 
     // ---- step-table window of this workgroup -> LDS
@@ -136,19 +126,6 @@ void wavefront_det(WaveArgs a) {
         for (int k = 0; k < 8; ++k)
             if (base + k * SLOTS < ntot) xe[base + k * SLOTS] = v[k];
     }
-    // ---- overflow upstream codes of this workgroup -> LDS byte addresses (bit 0: external)
-    for (int idx = tid; idx < nm + kUpGroup; idx += SLOTS) {
-        unsigned ent = XB + (unsigned)SLOTS * 16;         // zero group / padding: the zero slot
-        if (idx >= kUpGroup) {
-            const unsigned code = a.up_more[m0 + idx - kUpGroup];
-            ent = (code & kExtBit) ? ((XE + (code & 0x7fffu) * (unsigned)tile * 8) | 1u)
-                                   : XB + code * 16;
-        }
-        xm[idx] = ent;
-    }
-    const int ngrp = live ? (more_end - more) / kUpGroup : 0;       // this lane's groups
-    const unsigned gofs = XM + (unsigned)(kUpGroup + more) * 4;       // its first group
-
     double op = st_o;
     double ip = st_i;
     // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
@@ -170,9 +147,6 @@ void wavefront_det(WaveArgs a) {
         uinc[u] = ext ? 16u : 0u;
     }
     const bool any3 = __any(cnt > 2);                   // wave-uniform
-    int ngw = 0;                                        // overflow groups of the wave
-    while (__any(ngw < ngrp)) ++ngw;
-    if (MCR_EXP_NO_OVERFLOW) ngw = 0;
     const unsigned own = XB + (unsigned)tid * 16;
 
     // forcing rows of the first chunk
@@ -240,31 +214,17 @@ void wavefront_det(WaveArgs a) {
                 const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
                 const int t = kc + i - G;
                 const bool act = (unsigned)t < (unsigned)T;
-                // inflow: upstream outflows in reference finalisation order
-                double I = 0.0 + lds_f64(lds, m[0] + rd);
+                // inflow: upstream outflows in reference finalisation order.  Every value a
+                // lane publishes is 0 + (...) or such a sum, never -0.0, so the reference's
+                // leading 0 + is exact without an add
+                double I = lds_f64(lds, m[0] + rd);
                 I = I + lds_f64(lds, m[1] + rd);
                 if (any3) {
                     I = I + lds_f64(lds, m[2] + rd);
                     I = I + lds_f64(lds, m[3] + rd);
                 }
-                // overflow upstreams, one group of kUpGroup per 16-byte LDS read; lanes past
-                // their own list read the zero group
-                const unsigned sx = 8u * (unsigned)(c + i);   // external-input column of tick i
-                for (int g = 0; g < ngw; ++g) {
-                    const uint4 e = *reinterpret_cast<const uint4*>(
-                        lds + (g < ngrp ? gofs + 16u * g : XM));
-                    const unsigned a0 = (e.x & ~1u) + ((e.x & 1u) ? sx : rd);
-                    const unsigned a1 = (e.y & ~1u) + ((e.y & 1u) ? sx : rd);
-                    const unsigned a2 = (e.z & ~1u) + ((e.z & 1u) ? sx : rd);
-                    const unsigned a3 = (e.w & ~1u) + ((e.w & 1u) ? sx : rd);
-                    const double v0 = lds_f64(lds, a0), v1 = lds_f64(lds, a1);
-                    const double v2 = lds_f64(lds, a2), v3 = lds_f64(lds, a3);
-                    I = I + v0;
-                    I = I + v1;
-                    I = I + v2;
-                    I = I + v3;
-                }
-                const double ov = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[j]);
+                const double rv = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[j]);
+                const double ov = psum ? I : rv;
                 // inactive ticks write garbage that no active reach reads (its consumer is
                 // inactive one tick later); never-processed reaches (no consumer) output 0
                 *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = ov;
@@ -291,7 +251,7 @@ void wavefront_det(WaveArgs a) {
     // state for the next launch (lanes that did not run keep theirs); never-processed reaches
     // hold o = 0 as in the reference's fresh o_t_next
     const int64_t ds = (int64_t)blockIdx.y * a.mS + (int64_t)w * SLOTS + threadIdx.x;
-    a.st_o[ds] = routed ? op : 0.0;
+    a.st_o[ds] = routed || psum ? op : 0.0;
     a.st_i[ds] = ip;
     if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();

@@ -48,8 +48,6 @@ struct WaveArgs {
     const uint8_t* flags;         // [nslots]
     const uint8_t* up_cnt;        // [nslots]
     const uint64_t* up4;          // [nslots]
-    const int32_t* up_more_off;   // [nslots + 1]
-    const uint16_t* up_more;
     const int32_t* ext_off;       // [nwg + 1]
     const int32_t* xid;           // [nslots] external input fed by the slot's reach, -1 if none
     const int32_t* ext_g;         // G of the consuming reach
@@ -86,18 +84,16 @@ struct WaveArgs {
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
-    int32_t more_cap;             // LDS words reserved for overflow upstream addresses (+ a zero group)
 };
 
-inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile,
-                                  int more_cap) {
+inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile) {
     return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)table_cap +
-           8 * (size_t)ext_cap * tile + 4 * ((size_t)more_cap + 4);
+           8 * (size_t)ext_cap * tile;
 }
 
-inline size_t flow_lds_bytes(int slots, int T, int ext_cap, int more_cap) {
+inline size_t flow_lds_bytes(int slots, int T, int ext_cap) {
     return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)T +
-           2 * (size_t)ext_cap * kChunk * 8 + 4 * ((size_t)more_cap + 4) + 4 * kFlowMaxExt;
+           2 * (size_t)ext_cap * kChunk * 8 + 4 * kFlowMaxExt;
 }
 
 // One launch for the whole horizon; grid = every workgroup (all must be co-resident).

@@ -102,38 +102,127 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             return m.str();
         }
     }
-    // node order for the compiler: routed reaches in rank order, then the never-processed ones
-    std::vector<int64_t> nodes(order);
-    for (int64_t j = 0; j < n; ++j)
-        if (P.rank[j] < 0) nodes.push_back(j);
-    // consumer of j inside the schedule (-1 if none)
-    auto consumer = [&](int64_t j) -> int64_t {
-        if (P.rank[j] < 0) return -1;
-        const int64_t e = endnodes[j];
-        return e == j ? -1 : e;
-    };
-
-    // ---- 3. heights -----------------------------------------------------------------------
+    // ---- 3. partial-sum nodes and heights -------------------------------------------------
+    // A lane reads at most kUpInline upstream values per tick.  A reach with more routed
+    // upstreams gets a left-deep chain of partial-sum nodes (ids n, n + 1, ...): a node outputs
+    // ((0 + x1) + x2) + ... over at most kUpInline inputs, x1 possibly the previous partial sum.
+    // Every value a lane publishes has the form 0 + (...) and is never -0.0, so 0 + prefix ==
+    // prefix and the chain reproduces the reference's left fold bit for bit.  Where the chain is
+    // cut is chosen per reach by a DP over the inputs' heights, so the deepest upstream enters
+    // the fold as late as the rank order allows (usually no extra level on the critical path).
     std::vector<int32_t> h(n, 0);
-    for (int64_t j : nodes) {
-        int32_t hj = 0;
-        for (int64_t k = up_off[j]; k < up_off[j + 1]; ++k) hj = std::max(hj, h[up_list[k]] + 1);
-        h[j] = hj;
-        P.max_height = std::max(P.max_height, hj);
+    std::vector<int64_t> nodes;                 // topological compile order over all nodes
+    nodes.reserve(n);
+    std::vector<std::vector<int64_t>> vin;      // inputs of partial-sum node n + i
+    std::vector<int64_t> rep_idx(n, -1);        // reaches whose input list was rewritten
+    std::vector<std::vector<int64_t>> reps;
+    {
+        std::vector<int64_t> node_order(order);
+        for (int64_t j = 0; j < n; ++j)
+            if (P.rank[j] < 0) node_order.push_back(j);
+        std::vector<int32_t> best;
+        std::vector<int8_t> cut;
+        std::vector<int64_t> chain;
+        for (int64_t j : node_order) {
+            const int64_t* u = up_list.data() + up_off[j];
+            const int64_t k = up_off[j + 1] - up_off[j];
+            int32_t hj = 0;
+            if (k <= kUpInline) {
+                for (int64_t q = 0; q < k; ++q) hj = std::max(hj, h[u[q]] + 1);
+            } else {
+                // best[p]: height of the value fold(u_1 .. u_p); cut[p]: how many raw inputs
+                // the node of prefix p adds to fold(u_1 .. u_{p - cut[p]}) (0: one node over
+                // u_1 .. u_p, only for p <= kUpInline); fold(u_1) is u_1 itself
+                best.assign(k + 1, 0);
+                cut.assign(k + 1, 0);
+                best[1] = h[u[0]];
+                int32_t pre = h[u[0]];
+                for (int64_t p = 2; p <= k; ++p) {
+                    pre = std::max(pre, h[u[p - 1]]);
+                    if (p <= kUpInline) {
+                        best[p] = pre + 1;
+                        continue;
+                    }
+                    best[p] = INT32_MAX;
+                    for (int s = kUpInline - 1; s >= 1; --s) {
+                        int32_t m = best[p - s];
+                        for (int64_t q = p - s; q < p; ++q) m = std::max(m, h[u[q]]);
+                        if (m + 1 < best[p]) {
+                            best[p] = m + 1;
+                            cut[p] = (int8_t)s;
+                        }
+                    }
+                }
+                chain.clear();                 // prefixes that need a node, the reach first
+                for (int64_t p = k;;) {
+                    chain.push_back(p);
+                    if (cut[p] == 0) break;
+                    p -= cut[p];
+                    if (p == 1) break;
+                }
+                int64_t prev = -1, plen = 1;   // value of the fold built so far (prefix plen)
+                for (auto it = chain.rbegin(); it != chain.rend(); ++it) {
+                    const int64_t p = *it;
+                    const int64_t from = cut[p] == 0 ? 0 : p - cut[p];
+                    std::vector<int64_t> x;
+                    if (from > 0) {
+                        if (from != plen) return "internal: partial-sum chain";
+                        x.push_back(from == 1 ? u[0] : prev);
+                    }
+                    for (int64_t q = from; q < p; ++q) x.push_back(u[q]);
+                    if ((int64_t)x.size() > kUpInline) return "internal: partial-sum fan-in";
+                    int32_t hx = 0;
+                    for (int64_t y : x) hx = std::max(hx, h[y] + 1);
+                    if (p == k) {
+                        hj = hx;
+                        rep_idx[j] = (int64_t)reps.size();
+                        reps.push_back(std::move(x));
+                    } else {
+                        prev = n + (int64_t)vin.size();
+                        vin.push_back(std::move(x));
+                        h.push_back(hx);
+                        nodes.push_back(prev);
+                    }
+                    plen = p;
+                }
+            }
+            h[j] = hj;
+            nodes.push_back(j);
+        }
     }
+    const int64_t V = (int64_t)vin.size();
+    const int64_t N = n + V;
+    P.n_partial = V;
+    // inputs of every node (CSR over [0, N)) and its consumer inside the schedule
+    std::vector<int64_t> gin_off(N + 1, 0), gin_list;
+    gin_list.reserve(up_list.size() + (size_t)V * kUpInline);
+    for (int64_t x = 0; x < N; ++x) {
+        if (x >= n)
+            gin_list.insert(gin_list.end(), vin[x - n].begin(), vin[x - n].end());
+        else if (rep_idx[x] >= 0)
+            gin_list.insert(gin_list.end(), reps[rep_idx[x]].begin(), reps[rep_idx[x]].end());
+        else
+            gin_list.insert(gin_list.end(), up_list.begin() + up_off[x],
+                            up_list.begin() + up_off[x + 1]);
+        gin_off[x + 1] = (int64_t)gin_list.size();
+    }
+    std::vector<int64_t> cons(N, -1);
+    for (int64_t x = 0; x < N; ++x)
+        for (int64_t k = gin_off[x]; k < gin_off[x + 1]; ++k) cons[gin_list[k]] = x;
+    for (int64_t x = 0; x < N; ++x) P.max_height = std::max(P.max_height, h[x]);
 
     // ---- 4. clustering (bottom-up greedy) -------------------------------------------------
     // Each reach starts a cluster that absorbs the clusters of its upstream reaches while the
     // slot and external-input budgets allow.  The deepest upstream is tried first; a shallow
     // upstream whose value can arrive `tile` ticks late without delaying j is cut for free.
-    std::vector<int64_t> cl(n, -1);
+    std::vector<int64_t> cl(N, -1);
     std::vector<Cluster> clusters;
-    std::vector<int32_t> eh(n, 0);          // critical-path estimate (ticks)
-    std::vector<uint8_t> merged(n, 0);      // edge (j -> consumer) is inside a cluster
+    std::vector<int32_t> eh(N, 0);          // critical-path estimate (ticks)
+    std::vector<uint8_t> merged(N, 0);      // edge (j -> consumer) is inside a cluster
     std::vector<std::vector<int64_t>> members;
     std::vector<int64_t> ups;
     for (int64_t j : nodes) {
-        ups.assign(up_list.begin() + up_off[j], up_list.begin() + up_off[j + 1]);
+        ups.assign(gin_list.begin() + gin_off[j], gin_list.begin() + gin_off[j + 1]);
         std::stable_sort(ups.begin(), ups.end(),
                          [&](int64_t a, int64_t b) { return eh[a] > eh[b]; });
         Cluster c;
@@ -195,15 +284,15 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
 
     // ---- 5. schedule: local ALAP skew + cluster offsets -----------------------------------
     // distance to the cluster root: walk nodes in reverse (downstream first)
-    std::vector<int32_t> dist(n, 0);
+    std::vector<int32_t> dist(N, 0);
     for (auto it = nodes.rbegin(); it != nodes.rend(); ++it) {
         const int64_t j = *it;
-        const int64_t e = consumer(j);
+        const int64_t e = cons[j];
         dist[j] = (e >= 0 && merged[j]) ? dist[e] + 1 : 0;
         Cluster& c = clusters[cl[j]];
         c.dmax = std::max(c.dmax, dist[j]);
     }
-    std::vector<int32_t> G(n, 0);
+    std::vector<int32_t> G(N, 0);
     // live clusters in root rank order (roots appear in `nodes` order)
     std::vector<int64_t> live;
     for (int64_t j : nodes)
@@ -214,8 +303,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int64_t off = 0;
         for (int64_t v : members[id]) {
             const int32_t s = c.dmax - dist[v];
-            for (int64_t k = up_off[v]; k < up_off[v + 1]; ++k) {
-                const int64_t u = up_list[k];
+            for (int64_t k = gin_off[v]; k < gin_off[v + 1]; ++k) {
+                const int64_t u = gin_list[k];
                 if (cl[u] != id) off = std::max<int64_t>(off, (int64_t)G[u] + B - s);
             }
         }
@@ -223,7 +312,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         c.off = (int32_t)off;
         for (int64_t v : members[id]) G[v] = c.off + c.dmax - dist[v];
     }
-    for (int64_t j = 0; j < n; ++j) P.gmax = std::max(P.gmax, G[j]);
+    for (int64_t j = 0; j < N; ++j) P.gmax = std::max(P.gmax, G[j]);
 
     // ---- 6. pack clusters into workgroups --------------------------------------------------
     // First fit in order of schedule offset, so a workgroup holds clusters that are active at
@@ -271,8 +360,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     P.flags.assign(P.nslots, kSlotPad);
     P.up_cnt.assign(P.nslots, 0);
     P.up4.assign(P.nslots, 0);
-    P.up_more_off.assign(P.nslots + 1, 0);
     P.pos.assign(n, -1);
+    std::vector<int64_t> npos(N, -1);       // node -> slot
     P.wg_gmin.assign(P.nwg, 0);
     P.wg_gmax.assign(P.nwg, 0);
     for (int32_t w = 0; w < P.nwg; ++w) {
@@ -280,10 +369,16 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         std::stable_sort(v.begin(), v.end(), [&](int64_t a, int64_t b) { return G[a] < G[b]; });
         for (size_t k = 0; k < v.size(); ++k) {
             const int64_t d = (int64_t)w * C + (int64_t)k;
-            P.slot_reach[d] = v[k];
-            P.pos[v[k]] = d;
-            P.G[d] = G[v[k]];
-            P.flags[d] = P.rank[v[k]] >= 0 ? kSlotRouted : kSlotUnrouted;
+            const int64_t x = v[k];
+            npos[x] = d;
+            P.G[d] = G[x];
+            if (x < n) {
+                P.slot_reach[d] = x;
+                P.pos[x] = d;
+                P.flags[d] = P.rank[x] >= 0 ? kSlotRouted : kSlotUnrouted;
+            } else {
+                P.flags[d] = kSlotSum;
+            }
         }
         P.wg_gmin[w] = v.empty() ? 0 : G[v.front()];
         P.wg_gmax[w] = v.empty() ? 0 : G[v.back()];
@@ -292,54 +387,48 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     }
     // upstream codes and external lists
     P.ext_off.assign(P.nwg + 1, 0);
-    std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src slot, consumer G)
-    std::vector<uint16_t> codes;
+    std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src node, consumer G)
+    std::vector<int64_t> node_at(P.nslots, -1);
+    for (int64_t x = 0; x < N; ++x) node_at[npos[x]] = x;
     for (int64_t d = 0; d < P.nslots; ++d) {
-        const int64_t j = P.slot_reach[d];
-        P.up_more_off[d + 1] = P.up_more_off[d];
+        const int64_t j = node_at[d];
         if (j < 0) continue;
         const int32_t w = (int32_t)(d / C);
-        codes.clear();
-        for (int64_t k = up_off[j]; k < up_off[j + 1]; ++k) {
-            const int64_t u = up_list[k];
+        const int64_t k0 = gin_off[j], k1 = gin_off[j + 1];
+        if (k1 - k0 > kUpInline) return "internal: more than kUpInline inputs";
+        P.up_cnt[d] = (uint8_t)(k1 - k0);
+        uint64_t packed = 0;
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t u = gin_list[k];
+            uint16_t code;
             if (cl[u] == cl[j]) {
                 if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";
-                codes.push_back((uint16_t)(P.pos[u] - (int64_t)w * C));
+                code = (uint16_t)(npos[u] - (int64_t)w * C);
             } else {
                 if (G[j] < G[u] + B) return "internal: cross-cluster edge without tile slack";
                 const size_t e = ext[w].size();
                 if (e >= (size_t)hard) return "internal: external-input cap exceeded";
                 ext[w].push_back({u, G[j]});
-                codes.push_back((uint16_t)(kExtBit | e));
+                code = (uint16_t)(kExtBit | e);
                 P.n_cross++;
             }
+            packed |= (uint64_t)code << (16 * (k - k0));
         }
-        if (codes.size() > 255) return "a reach has more than 255 upstream reaches";
-        P.up_cnt[d] = (uint8_t)codes.size();
-        uint64_t packed = 0;
-        for (size_t k = 0; k < codes.size() && k < (size_t)kUpInline; ++k)
-            packed |= (uint64_t)codes[k] << (16 * k);
         P.up4[d] = packed;
-        // overflow list padded to whole groups of kUpGroup with the zero-slot code: the kernel
-        // reads it one group at a time (adding +0.0 to the running sum is exact)
-        for (size_t k = kUpInline; k < codes.size(); ++k) P.up_more.push_back(codes[k]);
-        while (P.up_more.size() % kUpGroup) P.up_more.push_back((uint16_t)C);
-        P.up_more_off[d + 1] = (int32_t)P.up_more.size();
     }
+    // each node has one consumer, so it feeds at most one external input; ext_src names the
+    // source's row of the output arrays: the reach, or n + slot for a partial-sum node
+    P.xid.assign(P.nslots, -1);
     for (int32_t w = 0; w < P.nwg; ++w) {
         P.ext_off[w + 1] = P.ext_off[w] + (int32_t)ext[w].size();
         P.max_ext_wg = std::max(P.max_ext_wg, (int32_t)ext[w].size());
         for (auto& pr : ext[w]) {
-            P.ext_src.push_back(pr.first);
+            const int64_t src = npos[pr.first];
+            if (P.xid[src] != -1) return "internal: node feeds two external inputs";
+            P.xid[src] = (int32_t)P.ext_src.size();
+            P.ext_src.push_back(pr.first < n ? pr.first : n + src);
             P.ext_g.push_back(pr.second);
         }
-    }
-    // each reach has one downstream reach, so it feeds at most one external input
-    P.xid.assign(P.nslots, -1);
-    for (size_t e = 0; e < P.ext_src.size(); ++e) {
-        const int64_t d = P.pos[P.ext_src[e]];
-        if (P.xid[d] != -1) return "internal: reach feeds two external inputs";
-        P.xid[d] = (int32_t)e;
     }
     return std::string();
 }

@@ -7,7 +7,9 @@
 //
 //   * every reach j gets an upstream list sorted by the reference's finalisation rank, so the
 //     inflow sum  i_next[j] = ((0 + o[u1]) + o[u2]) + ...  is formed in exactly the reference's
-//     order (bitwise identical for >= 3-way confluences);
+//     order (bitwise identical for >= 3-way confluences); a reach with more than kUpInline
+//     upstreams reads a chain of partial-sum nodes (extra lanes that output a prefix of the
+//     same left fold), so every lane reads at most kUpInline values per tick;
 //   * reaches are grouped into clusters (connected sub-trees of at most `slots` reaches); a
 //     cluster is swept by one workgroup with a time-skewed wavefront: reach j handles model step
 //     t at global tick  G[j] + t.  Inside a cluster G[j] = G[down(j)] - 1, so every upstream
@@ -39,13 +41,13 @@ constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 
 // upstream code: bit 15 set -> index into the workgroup's external-input list, else the
 // workgroup-local slot of the upstream reach.
 constexpr uint16_t kExtBit = 0x8000;
-constexpr int kUpInline = 4;  // upstream codes kept in registers; more go to an overflow list
-constexpr int kUpGroup = 4;   // overflow lists are padded to whole groups (one 16-byte LDS read)
+constexpr int kUpInline = 4;  // upstream values one lane reads per tick (codes in registers)
 
 enum SlotFlags : uint8_t {
     kSlotPad = 0,        // unused thread slot
     kSlotRouted = 1,     // reach processed by the reference walk: o = 0 + (((a I + b Ip) + c Op) + g q)
     kSlotUnrouted = 2,   // reach never processed (cycle / unreachable): o stays 0, I = sum of inflows
+    kSlotSum = 3,        // partial-sum node: outputs I (a prefix of a reach's inflow fold)
 };
 
 struct Plan {
@@ -57,7 +59,8 @@ struct Plan {
     int64_t n_routed = 0;
     int64_t n_clusters = 0;
     int64_t n_cross = 0;           // cross-cluster edges
-    int32_t max_height = 0;        // longest upstream path (levels - 1)
+    int32_t max_height = 0;        // longest upstream path (levels - 1, partial sums included)
+    int64_t n_partial = 0;         // partial-sum nodes
     int32_t max_ext_wg = 0;
     int32_t ext_hard = 0;          // LDS-derived hard cap of cross-cluster inputs per workgroup
     int32_t max_span = 0;          // max G span inside one workgroup
@@ -69,19 +72,17 @@ struct Plan {
     std::vector<int64_t> in_off, in_list;
 
     // per device slot d in [0, nslots)
-    std::vector<int64_t> slot_reach;   // original reach index, -1 for padding
+    std::vector<int64_t> slot_reach;   // original reach index, -1 for padding / partial sums
     std::vector<int32_t> G;            // tick of model step 0
     std::vector<uint8_t> flags;
     std::vector<uint8_t> up_cnt;
     std::vector<uint64_t> up4;         // first kUpInline codes, 16 bits each
-    std::vector<int32_t> up_more_off;  // overflow list offset (codes kUpInline..), per-lane lists
-    std::vector<uint16_t> up_more;     // padded to kUpGroup with the zero-slot code (= slots)
-    std::vector<int32_t> xid;          // external input this reach feeds (index into ext_*), -1
+    std::vector<int32_t> xid;          // external input this slot feeds (index into ext_*), -1
 
     // per workgroup
     std::vector<int32_t> wg_gmin, wg_gmax;  // G range of the workgroup's real reaches
     std::vector<int32_t> ext_off;           // [nwg + 1]
-    std::vector<int64_t> ext_src;           // caller index of the upstream reach (row of O)
+    std::vector<int64_t> ext_src;           // source row: reach index, or n + slot (partial sum)
     std::vector<int32_t> ext_g;             // G of the consuming reach
 
     // original reach -> device slot

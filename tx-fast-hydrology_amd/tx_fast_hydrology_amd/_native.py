@@ -47,7 +47,7 @@ class PlanInfo(ctypes.Structure):
                 ("nslots", ctypes.c_int64), ("nwg", ctypes.c_int32), ("slots", ctypes.c_int32),
                 ("tile", ctypes.c_int32), ("gmax", ctypes.c_int32),
                 ("max_height", ctypes.c_int32), ("max_ext_wg", ctypes.c_int32),
-                ("n_up_more", ctypes.c_int64), ("n_ext", ctypes.c_int64)]
+                ("n_partial", ctypes.c_int64), ("n_ext", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -64,7 +64,7 @@ SIGNATURES = {
     "mc_plan_create": (_i32, [_i64, _vp, _vp, _vp, _i64, _vp, _pp]),
     "mc_plan_get_info": (_i32, [_vp, ctypes.POINTER(PlanInfo)]),
     "mc_plan_export": (_i32, [_vp, _vp, _vp, _vp, _vp]),
-    "mc_plan_export_links": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mc_plan_export_links": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mc_plan_schedule": (_i32, [_vp, _i64, ctypes.POINTER(ctypes.c_int64),
                                 ctypes.POINTER(ctypes.c_int64), _vp, _vp]),
     "mc_plan_destroy": (_i32, [_vp]),

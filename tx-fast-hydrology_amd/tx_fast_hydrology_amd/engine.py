@@ -57,13 +57,12 @@ class Plan:
         info = self.info
         ns, nwg = info["nslots"], info["nwg"]
         out = dict(flags=np.empty(ns, np.uint8), up_cnt=np.empty(ns, np.uint8),
-                   up4=np.empty(ns, np.uint64), up_more_off=np.empty(ns + 1, np.int32),
-                   up_more=np.empty(info["n_up_more"], np.uint16),
-                   ext_off=np.empty(nwg + 1, np.int32), ext_src=np.empty(info["n_ext"], np.int64),
+                   up4=np.empty(ns, np.uint64), ext_off=np.empty(nwg + 1, np.int32),
+                   ext_src=np.empty(info["n_ext"], np.int64),
                    ext_g=np.empty(info["n_ext"], np.int32))
         nat.check(nat.lib().mc_plan_export_links(
-            self._h, *(ptr(out[k]) for k in ("flags", "up_cnt", "up4", "up_more_off", "up_more",
-                                             "ext_off", "ext_src", "ext_g"))))
+            self._h, *(ptr(out[k]) for k in ("flags", "up_cnt", "up4", "ext_off", "ext_src",
+                                             "ext_g"))))
         return out
 
     def schedule(self, T: int):

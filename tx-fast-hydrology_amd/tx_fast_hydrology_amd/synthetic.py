@@ -33,6 +33,19 @@ def random_forest(n, n_outlets, rng, p_chain=0.0, window=4):
     return _permute(parent, rng)
 
 
+def fan_in_forest(n, rng, hubs=6, max_fan=30):
+    """random_forest plus a few hub reaches of large fan-in (5 .. max_fan upstreams): some
+    headwaters are re-pointed at each hub (a headwater has no upstream, so no cycle forms)."""
+    end = random_forest(n, 2, rng, p_chain=0.9)
+    ids = np.arange(n)
+    for hub in rng.choice(n, size=min(hubs, n), replace=False):
+        deg = np.bincount(end[end != ids], minlength=n)
+        cand = np.flatnonzero((deg == 0) & (ids != hub) & (ids != end[hub]))
+        fan = min(int(rng.integers(5, max_fan + 1)), cand.size)
+        end[rng.choice(cand, size=fan, replace=False)] = hub
+    return end
+
+
 def _permute(parent, rng):
     n = parent.size
     perm = rng.permutation(n)
