@@ -14,6 +14,7 @@ import numpy as np
 
 ROUTED, UNROUTED, PSUM = 1, 2, 3
 EXT = 0x8000
+SELF = 0x7FFF
 
 
 def step_tables(x, xp):
@@ -38,11 +39,16 @@ def step_tables(x, xp):
 
 
 def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
-    """Route len(x) steps exactly as the device does.  Returns (O [n][T], I [n][T], state)."""
+    """Route len(x) steps exactly as the device does.  Returns (O [n][T], I [n][T]).
+
+    A workgroup has `slots` lanes and 2 * slots node slots: lane l owns slot l (low, computed
+    first in a tick) and slot slots + l (high).  A high node may read its lane's low output of
+    the same tick (SELF code); every other in-workgroup code reads the previous tick."""
     info = plan.info
     ex = plan.export()
     ln = plan.export_links()
     C, tile, nslots = info["slots"], info["tile"], info["nslots"]
+    RS = 2 * C
     n = info["n"]
     T = len(x)
     off, wlist = plan.schedule(T)
@@ -56,14 +62,12 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
     al, be, ch, ga = slots(alpha), slots(beta), slots(chi), slots(gamma)
     st_o, st_i = slots(o0), slots(i0)
     F = np.where(real[None, :], np.asarray(fp, float)[:, rowc], 0.0)
-    n_rows = F.shape[0]
     lo, hi, w0, w1 = step_tables(np.asarray(x, float), np.asarray(xp, float))
     G = ex["G"].astype(np.int64)
     fl = ln["flags"]
     cnt = ln["up_cnt"].astype(np.int64)
-    maxc = int(cnt.max()) if cnt.size else 0
-    codes = np.zeros((nslots, max(maxc, 1)), np.int64)
-    for c in range(min(maxc, 4)):
+    codes = np.zeros((nslots, 4), np.int64)
+    for c in range(4):
         codes[:, c] = (ln["up4"] >> np.uint64(16 * c)).astype(np.int64) & 0xFFFF
     # output rows: reaches, then one row per slot for partial-sum nodes (ext_src convention)
     orow = np.where(real, sr, n + np.arange(nslots))
@@ -74,7 +78,7 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
         k0 = k * tile
         Os, Is = O.copy(), I.copy()          # reads see only earlier launches
         for w in wlist[off[k]:off[k + 1]]:
-            d = w * C + np.arange(C)
+            d = w * RS + np.arange(RS)
             e0, e1 = ln["ext_off"][w], ln["ext_off"][w + 1]
             ne = e1 - e0
             xe = np.zeros((max(ne, 1), tile))
@@ -87,74 +91,53 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
             tf = k0 - g
             live = (f != 0) & (tf < T) & (tf + tile > 0)
             rest = (f != 0) & (tf <= T) & (tf + tile > 0)
-            op = np.zeros(C)
-            ip = np.zeros(C)
+            op = np.zeros(RS)
+            ip = np.zeros(RS)
             init = rest & (tf <= 0)
             op[init], ip[init] = st_o[d[init]], st_i[d[init]]
             later = rest & (tf > 0)
             op[later] = Os[row[later], tf[later] - 1]
             ip[later] = Is[row[later], tf[later] - 1]
-            xb = np.full((2, C), np.nan)
-            xb[(k0 - 1) & 1] = op
-            r_lo = np.full(C, -1)
-            r_hi = np.full(C, -1)
-            r_nx = np.full(C, -1)
-            f_lo = np.zeros(C)
-            f_hi = np.zeros(C)
-            f_nx = np.zeros(C)
-            tc = np.clip(tf, 0, T - 1)
-            rn_x = np.where(live, lo[tc], 0)
-            rn_y = np.where(live, hi[tc], -1)
-            wn0 = np.where(live, w0[tc], 0.0)
-            wn1 = np.where(live, w1[tc], 0.0)
+            xb = np.full((2, RS + 1), np.nan)
+            xb[:, RS] = 0.0
+            xb[(k0 - 1) & 1, :RS] = op
             cd = codes[d]
             cn = cnt[d]
             for i in range(tile):
                 kk = k0 + i
                 t = kk - g
-                rx, ry, ww0, ww1 = rn_x.copy(), rn_y.copy(), wn0.copy(), wn1.copy()
                 act = live & (t >= 0) & (t < T)
                 if not act.any():
                     continue
-                pf = act & (t + 1 < T)
-                tn = np.clip(t + 1, 0, T - 1)
-                rn_x = np.where(pf, lo[tn], rn_x)
-                rn_y = np.where(pf, hi[tn], rn_y)
-                wn0 = np.where(pf, w0[tn], wn0)
-                wn1 = np.where(pf, w1[tn], wn1)
+                tc = np.clip(t, 0, T - 1)
+                qlo = F[lo[tc], d]
+                qhi = F[np.maximum(hi[tc], 0), d]
+                q = np.where(hi[tc] < 0, qlo, w0[tc] * qlo + w1[tc] * qhi)
                 prev = xb[(kk - 1) & 1]
-                Iv = np.zeros(C)
-                for c in range(maxc):
-                    m = act & (c < cn)
-                    code = cd[:, c]
-                    isx = (code & EXT) != 0
-                    vi = prev[np.minimum(code, C - 1)]
-                    vx = xe[np.clip(code & 0x7FFF, 0, xe.shape[0] - 1), i]
-                    v = np.where(isx, vx, vi)
-                    Iv = np.where(m, Iv + v, Iv)
-                m1 = act & (rx != r_lo)
-                c_hi = m1 & (rx == r_hi)
-                c_nx = m1 & ~c_hi & (rx == r_nx)
-                c_ld = m1 & ~c_hi & ~c_nx
-                f_lo = np.where(c_hi, f_hi, f_lo)
-                f_lo = np.where(c_nx, f_nx, f_lo)
-                f_lo = np.where(c_ld, F[np.clip(rx, 0, n_rows - 1), d], f_lo)
-                r_lo = np.where(m1, rx, r_lo)
-                cp = ry < 0
-                m2 = act & ~cp & (ry != r_hi)
-                ld = F[np.clip(ry, 0, n_rows - 1), d]
-                f_hi = np.where(m2, np.where(ry == r_nx, f_nx, ld), f_hi)
-                r_hi = np.where(m2, ry, r_hi)
-                m3 = m2 & (r_hi + 1 < n_rows) & (r_nx != r_hi + 1)
-                r_nx = np.where(m3, r_hi + 1, r_nx)
-                f_nx = np.where(m3, F[np.clip(r_nx, 0, n_rows - 1), d], f_nx)
-                q = np.where(cp, f_lo, ww0 * f_lo + ww1 * f_hi)
-                o = np.where(f == ROUTED, 0.0 + (((al[d] * Iv + be[d] * ip) + ch[d] * op)
-                                                  + ga[d] * q), 0.0)
-                o = np.where(f == PSUM, Iv, o)
-                xb[kk & 1] = np.where(act, o, xb[kk & 1])
-                O[row[act], t[act]] = o[act]
-                I[row[act], t[act]] = Iv[act]
-                op = np.where(act, o, op)
-                ip = np.where(act, Iv, ip)
+                cur = xb[kk & 1]
+                for half in (slice(0, C), slice(C, RS)):
+                    Iv = np.zeros(RS)
+                    for c in range(4):
+                        m = act & (c < cn)
+                        m[:half.start] = False
+                        m[half.stop:] = False
+                        code = cd[:, c]
+                        isx = (code & EXT) != 0
+                        self_ = code == SELF
+                        vi = prev[np.minimum(code, RS)]
+                        vs = cur[(np.arange(RS) - C) % RS]
+                        vx = xe[np.clip(code & 0x7FFF, 0, xe.shape[0] - 1), i]
+                        v = np.where(isx, vx, np.where(self_, vs, vi))
+                        Iv = np.where(m, Iv + v, Iv)
+                    o = np.where(f == ROUTED, 0.0 + (((al[d] * Iv + be[d] * ip) + ch[d] * op)
+                                                      + ga[d] * q), 0.0)
+                    o = np.where(f == PSUM, Iv, o)
+                    sel = np.zeros(RS, bool)
+                    sel[half] = True
+                    a_ = act & sel
+                    cur[:RS][a_] = o[a_]
+                    O[row[a_], t[a_]] = o[a_]
+                    I[row[a_], t[a_]] = Iv[a_]
+                    op = np.where(a_, o, op)
+                    ip = np.where(a_, Iv, ip)
     return O[:n], I[:n]

@@ -86,7 +86,7 @@ def _golden_run(g, n_steps=None, **kw):
 
 
 @pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=16), dict(slots=64, tile=48),
-                                dict(slots=1024, tile=64)])
+                                dict(slots=512, tile=64)])
 def test_run_golden_ynet(golden, kw):
     g = golden("g1_ynet.npz")
     o, i = _golden_run(g, **kw)
@@ -119,7 +119,7 @@ def _random_case(n, seed, p_chain, outlets):
 
 @pytest.mark.parametrize("n,p_chain,slots,tile,T", [
     (1, 0.0, 64, 32, 7), (2, 1.0, 64, 16, 3), (300, 0.9, 64, 16, 50), (3000, 0.95, 256, 32, 96),
-    (5000, 0.5, 1024, 16, 40), (2000, 0.99, 128, 64, 1), (800, 0.9, 64, 128, 20),
+    (5000, 0.5, 512, 16, 40), (2000, 0.99, 128, 64, 1), (800, 0.9, 64, 128, 20),
     (6000, 0.98, 512, 48, 333)])
 def test_run_random_vs_oracle(n, p_chain, slots, tile, T):
     end, K, X = _random_case(n, n + T, p_chain, max(1, n // 500))
@@ -135,6 +135,27 @@ def test_run_random_vs_oracle(n, p_chain, slots, tile, T):
     assert np.array_equal(so, fo) and np.array_equal(si, fi)
     O, I = net.fetch_series()
     assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
+
+
+@pytest.mark.parametrize("slots,tile,T", [(64, 16, 40), (128, 32, 97), (448, 16, 64)])
+def test_run_high_fan_in_vs_oracle(slots, tile, T):
+    """Reaches with up to 30 routed upstreams: partial-sum slots and fused lane pairs must keep
+    the rank-ordered inflow fold bit-exact."""
+    rng = np.random.default_rng(slots + T)
+    end = synthetic.fan_in_forest(4000, rng, hubs=12)
+    n = end.size
+    K, X = rng.uniform(1800.0, 7200.0, n), rng.uniform(0.1, 0.4, n)
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=T)
+    xp, fp = synthetic.forcing(n, rows=4, seed=T)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    want_o, want_i, fo, fi = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=tile)
+    assert net.info["n_partial"] > 0 and net.info["n_pairs"] > 0
+    got_o, got_i = net.simulate(x, xp, fp)
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+    so, si = net.get_state()
+    assert np.array_equal(so, fo) and np.array_equal(si, fi)
 
 
 def test_run_continuation_equals_one_long_run():

@@ -112,6 +112,7 @@ void fill_info(const mcr::Plan& P, mc_plan_info* info) {
     info->max_ext_wg = P.max_ext_wg;
     info->n_partial = P.n_partial;
     info->n_ext = (int64_t)P.ext_src.size();
+    info->n_pairs = P.n_pairs;
 }
 
 void check_topology_args(int64_t n, const int64_t* endnodes, const int64_t* indegree,
@@ -422,6 +423,8 @@ struct Net {
     // collectives between the stages run in the caller, ensemble.py) and, with N = 1, the
     // single-GPU mc_enkf_analysis.  Stage buffers are device pointers owned by the caller.
     int64_t slice_size(int64_t N) const { return (plan.nslots + N - 1) / N; }
+    // values per tick row of an output window: the node slots of a workgroup
+    int row_width() const { return 2 * plan.p.slots; }
 
     void upload_gauges(int64_t m, const int64_t* gauges) {
         REQUIRE(m >= 1 && m < (1ll << 31) && gauges, "bad gauge arguments");
@@ -592,12 +595,12 @@ struct Net {
             int64_t total = 0;
             for (int32_t w = 0; w < plan.nwg; ++w) {
                 wb[w] = total;
-                total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * plan.p.slots;
+                total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * row_width();
             }
             hit->wbase.upload(wb.data(), wb.size(), stream);
             hit->Otot = total;
             hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
-            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, plan.p.slots,
+            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, row_width(),
                                           plan.n, hit->jbase.p, stream));
             sync();
         }
@@ -809,7 +812,7 @@ struct Net {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
             HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
-                                          c == 1, plan.p.slots, outT.p, n, t0, t1, E, stream));
+                                          c == 1, row_width(), outT.p, n, t0, t1, E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             sync();
@@ -826,7 +829,7 @@ struct Net {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
             HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
-                                           k == 1, plan.p.slots, outT.p, n, T_out, E, stream));
+                                           k == 1, row_width(), outT.p, n, T_out, E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             sync();
         }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
+#include "plan.hpp"
 
 namespace mcr {
 namespace dev {
@@ -34,6 +35,76 @@ __device__ __forceinline__ int clamp_row(int r, int n_rows) {
 
 __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
     return *reinterpret_cast<const double*>(lds + byte);
+}
+
+// One node slot of a lane: the registers of its reach (or partial sum) for one launch.
+struct Slot {
+    int64_t d;            // node slot
+    int G;                // tick of step 0 (huge when the slot has no work in this launch)
+    bool routed, psum, xsrc;
+    double al, be, ch, ga, op, ip;
+    int cnt;
+    unsigned ubase[kUpInline], uinc[kUpInline];
+    bool self[kUpInline];  // code reads the lane's low output of this tick (fused pair)
+    int64_t xs0;           // XS address of tick 0 when the slot feeds another cluster
+};
+
+// k0 / tile: the ticks this launch covers (the dataflow kernel passes its whole window)
+__device__ __forceinline__ void load_slot(Slot& s, const WaveArgs& a, int64_t d, int64_t mem,
+                                          int k0, int tile, int T) {
+    const uint8_t fl = a.flags[d];
+    const int Gr = a.G[d];
+    const bool real = fl != kSlotPad;
+    const int t_first = k0 - Gr;                        // step at this launch's first tick
+    const bool live = real && (t_first < T) && (t_first + tile > 0);
+    s.d = d;
+    s.G = live ? Gr : (1 << 29);                        // never active when not live
+    s.routed = fl == kSlotRouted;
+    s.psum = fl == kSlotSum;
+    // state after the last step this slot ran in an earlier launch (or the initial state)
+    s.op = a.st_o[mem * a.mS + d];
+    s.ip = a.st_i[mem * a.mS + d];
+    s.al = a.alpha[d];
+    s.be = a.beta[d];
+    s.ch = a.chi[d];
+    s.ga = a.gamma[d];
+    s.cnt = live ? a.up_cnt[d] : 0;
+    const int xsid = a.xid[d];
+    s.xsrc = live && xsid >= 0;
+    s.xs0 = s.xsrc ? (int64_t)xsid * T - Gr : 0;
+}
+
+// input codes -> LDS byte bases; unused codes read the zero slot (adding +0.0 to a sum that
+// started as a published value is exact, so the sum needs no predicate)
+template <int RS>
+__device__ __forceinline__ void decode_codes(Slot& s, uint64_t up4, unsigned XB, unsigned XE,
+                                             unsigned ext_stride) {
+#pragma unroll
+    for (int u = 0; u < kUpInline; ++u) {
+        unsigned code = u < s.cnt ? (unsigned)((up4 >> (16 * u)) & 0xffffu) : (unsigned)RS;
+        s.self[u] = code == kSelfCode;
+        if (s.self[u]) code = RS;
+        const bool ext = (code & kExtBit) != 0;
+        s.ubase[u] = ext ? XE + (code & 0x7fffu) * ext_stride : XB + code * 16;
+        s.uinc[u] = ext ? 16u : 0u;
+    }
+}
+
+// inflow fold in reference finalisation order.  Every value a lane publishes is 0 + (...) or
+// such a sum, never -0.0, so the reference's leading 0 + is exact without an add.  HIGH: the
+// slot may read its lane's low output of this tick (`low`) in place of a code.
+template <bool HIGH>
+__device__ __forceinline__ double fold(const char* lds, const unsigned* m, const bool* self,
+                                       unsigned rd, bool any3, double low) {
+    const double v0 = lds_f64(lds, m[0] + rd), v1 = lds_f64(lds, m[1] + rd);
+    double I = HIGH && self[0] ? low : v0;
+    I = I + (HIGH && self[1] ? low : v1);
+    if (any3) {
+        const double v2 = lds_f64(lds, m[2] + rd), v3 = lds_f64(lds, m[3] + rd);
+        I = I + (HIGH && self[2] ? low : v2);
+        I = I + (HIGH && self[3] ? low : v3);
+    }
+    return I;
 }
 
 }  // namespace dev

@@ -25,9 +25,6 @@
 #ifndef MCR_EXP_NO_STORES
 #define MCR_EXP_NO_STORES 0
 #endif
-#ifndef MCR_EXP_PAIR_STORES
-#define MCR_EXP_PAIR_STORES 0
-#endif
 #ifndef MCR_EXP_NO_Q
 #define MCR_EXP_NO_Q 0
 #endif
@@ -39,6 +36,10 @@ namespace {
 using dev::chunk_rows;
 using dev::clamp_row;
 using dev::lds_f64;
+using dev::Slot;
+using dev::load_slot;
+using dev::decode_codes;
+using dev::fold;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -139,16 +140,19 @@ struct Helper {
     }
 };
 
-// LDS layout (bytes): XB [SLOTS + 1][2] f64 | FR [SLOTS][3] f64 | TAB [T] int4 (whole step table)
+// LDS layout (bytes), RS = 2 * SLOTS node slots (lane l: slots l and SLOTS + l):
+//   XB [RS + 1][2] f64 | FR [RS][3] f64 | TAB [T] int4 (whole step table)
 //   | XE [2][ext_cap][kChunk] f64 (ring of external inputs, one slot per chunk parity)
 //   | EG [kFlowMaxExt] i32 (consumer G)
+// Each tick a lane routes its low slot, then its high slot (fused pairs: kernels.hip).
 template <int SLOTS, bool DENSE>
-__global__ __launch_bounds__(SLOTS + kHelperLanes) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(SLOTS + kHelperLanes) __attribute__((amdgpu_waves_per_eu(2)))
 void wavefront_flow(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RS = 2 * SLOTS;
     constexpr unsigned XB = 0;
-    constexpr unsigned FR = XB + (SLOTS + 1) * 16;
-    constexpr unsigned TAB = FR + SLOTS * 24;
+    constexpr unsigned FR = XB + (RS + 1) * 16;
+    constexpr unsigned TAB = FR + RS * 24;
     const int T = a.T;
     const unsigned XE = TAB + (unsigned)a.table_cap * 16;
     const unsigned XSLOT = (unsigned)a.ext_cap * kChunk * 8;
@@ -171,7 +175,7 @@ void wavefront_flow(WaveArgs a) {
     for (int idx = tid; idx < T; idx += nthr) tab[idx] = a.stab[idx];
     for (int idx = tid; idx < next; idx += nthr)
         reinterpret_cast<int*>(lds + EG)[idx] = a.ext_g[e0 + idx];
-    if (tid < 2) xbp[SLOTS * 2 + tid] = 0.0;
+    if (tid < 2) xbp[RS * 2 + tid] = 0.0;
 
     if (tid >= SLOTS) {
         // ================================ helper wave ================================
@@ -210,141 +214,152 @@ void wavefront_flow(WaveArgs a) {
     }
 
     // ================================ compute waves ================================
-    const int64_t d = (int64_t)w * SLOTS + tid;
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
-    const uint8_t fl = a.flags[d];
-    const int Gr = a.G[d];
-    const bool real = fl != kSlotPad;
-    const bool routed = fl == kSlotRouted;
-    const bool psum = fl == kSlotSum;                   // partial-sum node: outputs I
-    const int G = real ? Gr : (1 << 29);                // padding lanes are never active
-    const double st_o = a.st_o[d], st_i = a.st_i[d];
-    const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
-    const int cnt = real ? a.up_cnt[d] : 0;
-    const uint64_t up4 = a.up4[d];
-    const int xsid = a.xid[d];
     const int64_t wb = a.wbase[w];
-
-    double op = st_o;                                   // every lane starts at step 0 here
-    double ip = st_i;
-    xbp[tid * 2 + ((kb - 1) & 1)] = op;
+    Slot A, B;                                          // every real slot runs steps 0 .. T-1
+    load_slot(A, a, (int64_t)w * RS + tid, 0, kb, wend - kb, T);
+    load_slot(B, a, (int64_t)w * RS + SLOTS + tid, 0, kb, wend - kb, T);
+    const uint64_t up4A = a.up4[A.d], up4B = a.up4[B.d];
+    xbp[tid * 2 + ((kb - 1) & 1)] = A.op;
+    xbp[(SLOTS + tid) * 2 + ((kb - 1) & 1)] = B.op;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();                                    // LDS tables staged
 
-    unsigned ubase[kUpInline], uinc[kUpInline];
-#pragma unroll
-    for (int u = 0; u < kUpInline; ++u) {
-        const unsigned code = u < cnt ? (unsigned)((up4 >> (16 * u)) & 0xffffu) : (unsigned)SLOTS;
-        const bool ext = (code & kExtBit) != 0;
-        ubase[u] = ext ? XE + (code & 0x7fffu) * kChunk * 8 : XB + code * 16;
-        uinc[u] = ext ? 16u : 0u;
-    }
-    const bool any3 = __any(cnt > 2);
-    const unsigned own = XB + (unsigned)tid * 16;
+    decode_codes<RS>(A, up4A, XB, XE, kChunk * 8);
+    decode_codes<RS>(B, up4B, XB, XE, kChunk * 8);
+    const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);
+    const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
 
-    int rb, nr;
-    chunk_rows(tab, 0, kb, G, T, rb, nr);
-    double f0 = a.F[(int64_t)clamp_row(rb, nrow) * ns + d];
-    double f1 = a.F[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
-    double f2 = a.F[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
-    const bool xsrc = real && xsid >= 0;
-    const int64_t xs0 = xsrc ? (int64_t)xsid * T - Gr : 0;
+    int rbA, nrA, rbB, nrB;
+    chunk_rows(tab, 0, kb, A.G, T, rbA, nrA);
+    chunk_rows(tab, 0, kb, B.G, T, rbB, nrB);
+    double fA0 = a.F[(int64_t)clamp_row(rbA, nrow) * ns + A.d];
+    double fA1 = a.F[(int64_t)clamp_row(rbA + 1, nrow) * ns + A.d];
+    double fA2 = a.F[(int64_t)clamp_row(rbA + 2, nrow) * ns + A.d];
+    double fB0 = a.F[(int64_t)clamp_row(rbB, nrow) * ns + B.d];
+    double fB1 = a.F[(int64_t)clamp_row(rbB + 1, nrow) * ns + B.d];
+    double fB2 = a.F[(int64_t)clamp_row(rbB + 2, nrow) * ns + B.d];
     const unsigned epoch = a.epoch;
     __builtin_amdgcn_s_waitcnt(0);                      // nothing pending may enter the loop
     __syncthreads();                                    // prologue barrier (helper staged XE)
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
-    double pv = 0.0;                                    // MCR_EXP_PAIR_STORES only
+    double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
+    double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
     for (int kc = kb; kc < wend; kc += kChunk) {
         const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
-        double* frl = reinterpret_cast<double*>(lds + FR) + tid * 3;
-        frl[0] = f0;
-        frl[1] = f1;
-        frl[2] = f2;
-        const bool slow = DENSE && __any(nr > 3);
-        const unsigned frp = FR + (unsigned)tid * 24 - (unsigned)rb * 8;
-        int rbn, nrn;
-        chunk_rows(tab, 0, kc + kChunk, G, kc + kChunk < wend ? T : 0, rbn, nrn);
-        const double g0 = a.F[(int64_t)clamp_row(rbn, nrow) * ns + d];
-        const double g1 = a.F[(int64_t)clamp_row(rbn + 1, nrow) * ns + d];
-        const double g2 = a.F[(int64_t)clamp_row(rbn + 2, nrow) * ns + d];
-        unsigned m[kUpInline];
+        frA[0] = fA0;
+        frA[1] = fA1;
+        frA[2] = fA2;
+        frB[0] = fB0;
+        frB[1] = fB1;
+        frB[2] = fB2;
+        const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
+        const unsigned frpA = FR + (unsigned)tid * 24 - (unsigned)rbA * 8;
+        const unsigned frpB = FR + (unsigned)(SLOTS + tid) * 24 - (unsigned)rbB * 8;
+        const int Tn = kc + kChunk < wend ? T : 0;
+        int rbAn, nrAn, rbBn, nrBn;
+        chunk_rows(tab, 0, kc + kChunk, A.G, Tn, rbAn, nrAn);
+        chunk_rows(tab, 0, kc + kChunk, B.G, Tn, rbBn, nrBn);
+        const double gA0 = a.F[(int64_t)clamp_row(rbAn, nrow) * ns + A.d];
+        const double gA1 = a.F[(int64_t)clamp_row(rbAn + 1, nrow) * ns + A.d];
+        const double gA2 = a.F[(int64_t)clamp_row(rbAn + 2, nrow) * ns + A.d];
+        const double gB0 = a.F[(int64_t)clamp_row(rbBn, nrow) * ns + B.d];
+        const double gB1 = a.F[(int64_t)clamp_row(rbBn + 1, nrow) * ns + B.d];
+        const double gB2 = a.F[(int64_t)clamp_row(rbBn + 2, nrow) * ns + B.d];
+        unsigned mA[kUpInline], mB[kUpInline];
 #pragma unroll
-        for (int u = 0; u < kUpInline; ++u) m[u] = uinc[u] ? ubase[u] + sb - 8u : ubase[u];
-        const unsigned tp = TAB + (unsigned)(kc - G) * 16u;
-        double qv[kChunk];
+        for (int u = 0; u < kUpInline; ++u) {
+            mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
+            mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
+        }
+        const unsigned tpA = TAB + (unsigned)(kc - A.G) * 16u;
+        const unsigned tpB = TAB + (unsigned)(kc - B.G) * 16u;
+        double qA[kChunk], qB[kChunk];
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
-            const int4 e = *reinterpret_cast<const int4*>(lds + tp + 16u * j);
-            double flo, fhi;
+            const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
+            const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
+            double aLo, aHi, bLo, bHi;
             if (DENSE && slow) {
-                flo = a.F[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + d];
-                fhi = a.F[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + d];
+                aLo = a.F[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
+                aHi = a.F[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
+                bLo = a.F[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
+                bHi = a.F[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
             } else {
-                flo = lds_f64(lds, frp + 8u * (unsigned)e.x);
-                fhi = lds_f64(lds, frp + 8u * (unsigned)e.y);
+                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
+                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
+                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
+                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
             }
-            const double fr = __hiloint2double(e.w, e.z);
-            const double qi = (1.0 - fr) * flo + fr * fhi;
-            qv[j] = MCR_EXP_NO_Q ? 0.0 : (e.y < 0 ? flo : qi);
+            const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
+            const double qa = (1.0 - fa) * aLo + fa * aHi;
+            const double qb = (1.0 - fb) * bLo + fb * bHi;
+            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
+            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
         }
         if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int i = 0; i < kChunk; ++i) {
             if (i & 1) {
 #pragma unroll
-                for (int u = 0; u < kUpInline; ++u) m[u] += uinc[u];
+                for (int u = 0; u < kUpInline; ++u) {
+                    mA[u] += A.uinc[u];
+                    mB[u] += B.uinc[u];
+                }
             }
             const unsigned rd = 8u * ((i + 1) & 1);
             const int k = kc + i;
-            const int t = k - G;
-            const bool act = (unsigned)t < (unsigned)T;
-            double I = lds_f64(lds, m[0] + rd);   // published values are never -0.0
-            I = I + lds_f64(lds, m[1] + rd);
-            if (any3) {
-                I = I + lds_f64(lds, m[2] + rd);
-                I = I + lds_f64(lds, m[3] + rd);
-            }
-            const double rv = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[i]);
-            const double ov = psum ? I : rv;
-            *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = ov;
-            op = act ? ov : op;
-            ip = act ? I : ip;
+            const bool actA = (unsigned)(k - A.G) < (unsigned)T;
+            const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
+            const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
+            const double oA = A.psum ? IA : rA;
+            const bool actB = (unsigned)(k - B.G) < (unsigned)T;
+            const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
+            const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
+            const double oB = B.psum ? IB : rB;
+            *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
+            *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+            A.op = actA ? oA : A.op;
+            A.ip = actA ? IA : A.ip;
+            B.op = actB ? oB : B.op;
+            B.ip = actB ? IB : B.ip;
             const bool inwin = k >= gminw && k < wend;
-            const int64_t row = inwin ? wb + (int64_t)(k - gminw) * SLOTS : 0;
-            double* orow = inwin ? a.O + row : a.dummy;
-            if (MCR_EXP_PAIR_STORES) {
-                // timing experiment only: one 16-byte store per lane every second tick
-                const double sv = routed ? ov : 0.0;
-                if (i & 1) {
-                    const int kp = k - 1 >= gminw ? k - 1 : gminw;
-                    const int r0 = (kp - gminw) & ~1;
-                    const bool fits = inwin && r0 + 2 <= wend - gminw;
-                    const int64_t prow = wb + (int64_t)r0 * SLOTS;
-                    double2* pr = reinterpret_cast<double2*>(fits ? a.O + prow : a.dummy);
-                    pr[tid] = make_double2(pv, sv);
-                }
-                pv = sv;
-            } else if (!MCR_EXP_NO_STORES) {
-                orow[tid] = routed ? ov : 0.0;
+            double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
+            if (!MCR_EXP_NO_STORES) {
+                orow[tid] = A.routed ? oA : 0.0;
+                orow[SLOTS + tid] = B.routed ? oB : 0.0;
             }
-            if (xsrc && act) {
-                const uint64_t bits = (uint64_t)__double_as_longlong(ov);
+            if (A.xsrc && actA) {
+                const uint64_t bits = (uint64_t)__double_as_longlong(oA);
                 const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((xs0 + k) * 16), 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16), 0, 16);
+            }
+            if (B.xsrc && actB) {
+                const uint64_t bits = (uint64_t)__double_as_longlong(oB);
+                const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
             }
             __syncthreads();
         }
-        rb = rbn;
-        nr = nrn;
-        f0 = g0;
-        f1 = g1;
-        f2 = g2;
+        rbA = rbAn;
+        nrA = nrAn;
+        rbB = rbBn;
+        nrB = nrBn;
+        fA0 = gA0;
+        fA1 = gA1;
+        fA2 = gA2;
+        fB0 = gB0;
+        fB1 = gB1;
+        fB2 = gB2;
     }
-    a.st_o[d] = routed || psum ? op : 0.0;              // session state after the horizon
-    a.st_i[d] = ip;
+    // session state after the horizon; never-processed reaches hold o = 0
+    a.st_o[A.d] = A.routed || A.psum ? A.op : 0.0;
+    a.st_i[A.d] = A.ip;
+    a.st_o[B.d] = B.routed || B.psum ? B.op : 0.0;
+    a.st_i[B.d] = B.ip;
     if (a.trace && tid == 0) {
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
         rec[0] = t_start;
@@ -380,7 +395,8 @@ hipError_t flow_occupancy(int slots, bool dense, size_t lds, int* blocks_per_cu)
     e = hipFuncGetAttributes(&attr, fn);
     if (e != hipSuccess) return e;
     // Measured on gfx950 (launch trace, 5-wave workgroups at 128 VGPRs): a workgroup of W waves
-    // takes ceil(W / 4) wave slots on EVERY SIMD, so the API's answer can be too high.
+    // takes ceil(W / 4) wave slots on EVERY SIMD, so the API's answer can be too high.  A SIMD
+    // holds 512 VGPRs per lane.
     const int vgpr = ((attr.numRegs > 0 ? attr.numRegs : 512) + 7) / 8 * 8;
     const int per_simd = std::min(8, 512 / vgpr);
     const int waves = (threads + 63) / 64;

@@ -39,24 +39,31 @@ namespace {
 using dev::chunk_rows;
 using dev::clamp_row;
 using dev::lds_f64;
-constexpr int kHalf = kChunk;  // ticks whose lateral inflow is formed in one burst
+using dev::Slot;
+using dev::load_slot;
+using dev::decode_codes;
+using dev::fold;
 
-// LDS layout of one workgroup (bytes):
-//   XB  [SLOTS + 1][2] f64  outflow of each slot at tick parity 0/1; slot SLOTS stays 0.0
-//   FR  [SLOTS][3]     f64  the lane's forcing rows rb .. rb + 2 of the current chunk
-//   TAB [table_cap]    int4 step-table window {row_lo, row_hi, frac}
+// LDS layout of one workgroup (bytes), RS = 2 * SLOTS node slots (lane l: slots l and
+// SLOTS + l):
+//   XB  [RS + 1][2] f64   output of each node slot at tick parity 0/1; slot RS stays 0.0
+//   FR  [RS][3]     f64   each slot's forcing rows rb .. rb + 2 of the current chunk
+//   TAB [table_cap] int4  step-table window {row_lo, row_hi, frac}
 //   XE  [ext_cap][tile] f64 external inputs of this launch
+// Each tick a lane routes its low slot, then its high slot; a fused pair's high node takes the
+// low output of the same tick from a register (SELF code), so a fused edge costs no tick.
 // DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
 template <int SLOTS, bool DENSE>
-__global__ __launch_bounds__(SLOTS) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(SLOTS) __attribute__((amdgpu_waves_per_eu(2)))
 void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RS = 2 * SLOTS;
     const int tile = a.tile;
     constexpr unsigned XB = 0;
-    constexpr unsigned FR = XB + (SLOTS + 1) * 16;
-    constexpr unsigned TAB = FR + SLOTS * 24;
+    constexpr unsigned FR = XB + (RS + 1) * 16;
+    constexpr unsigned TAB = FR + RS * 24;
     const unsigned XE = TAB + (unsigned)a.table_cap * 16;
     double* xbp = reinterpret_cast<double*>(lds + XB);
     int4* tab = reinterpret_cast<int4*>(lds + TAB);
@@ -71,29 +78,18 @@ void wavefront_det(WaveArgs a) {
     double* Om = a.O + mem * a.mO;
     double* XSm = a.XS + mem * a.mX;
     double* dum = a.dummy + mem * kDummyPerMember;
-    const int64_t d = (int64_t)w * SLOTS + tid;
     const int T = a.T;
     const int k0 = a.kappa0;
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
-
-    // ---- per-reach registers and state at step t_first - 1 (issued first: longest latency)
-    const uint8_t fl = a.flags[d];
-    const int Gr = a.G[d];
-    const bool real = fl != kSlotPad;
-    const bool routed = fl == kSlotRouted;
-    const bool psum = fl == kSlotSum;                   // partial-sum node: outputs I
-    const int t_first = k0 - Gr;                        // step at this launch's first tick
-    const bool live = real && (t_first < T) && (t_first + tile > 0);
-    const int G = live ? Gr : (1 << 29);                // never active when not live
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
     const int64_t wb = a.wbase[w];
-    // the state after the last step this lane ran in an earlier launch (or the initial state)
-    const double st_o = a.st_o[mem * a.mS + d], st_i = a.st_i[mem * a.mS + d];
-    const double al = a.alpha[d], be = a.beta[d], ch = a.chi[d], ga = a.gamma[d];
-    const int cnt = live ? a.up_cnt[d] : 0;
-    const uint64_t up4 = a.up4[d];
-    const int xsid = a.xid[d];
+
+    // ---- per-slot registers (issued first: longest latency)
+    Slot A, B;
+    load_slot(A, a, (int64_t)w * RS + tid, mem, k0, tile, T);
+    load_slot(B, a, (int64_t)w * RS + SLOTS + tid, mem, k0, tile, T);
+    const uint64_t up4A = a.up4[A.d], up4B = a.up4[B.d];
 
     // ---- step-table window of this workgroup -> LDS
     int tw0 = k0 - gmaxw, tw1 = k0 + tile - gminw;
@@ -126,133 +122,153 @@ void wavefront_det(WaveArgs a) {
         for (int k = 0; k < 8; ++k)
             if (base + k * SLOTS < ntot) xe[base + k * SLOTS] = v[k];
     }
-    double op = st_o;
-    double ip = st_i;
-    // the downstream reach (one tick behind) reads step t_first - 1 at the first tick
-    xbp[tid * 2 + ((k0 - 1) & 1)] = op;
-    if (tid < 2) xbp[SLOTS * 2 + tid] = 0.0;            // zero slot for unused upstream codes
+    // the consumer (one tick behind) reads step t_first - 1 at the first tick
+    xbp[tid * 2 + ((k0 - 1) & 1)] = A.op;
+    xbp[(SLOTS + tid) * 2 + ((k0 - 1) & 1)] = B.op;
+    if (tid < 2) xbp[RS * 2 + tid] = 0.0;               // zero slot for unused codes
     // drain every prologue load: otherwise the wait-count pass carries "pending" state into
     // the tick loop and waits for each chunk's stores at every tick
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 
-    // upstream codes -> LDS byte bases; unused codes read the zero slot (adding +0.0 to a sum
-    // that started as 0.0 + v is exact, so the sum needs no predicate)
-    unsigned ubase[kUpInline], uinc[kUpInline];
-#pragma unroll
-    for (int u = 0; u < kUpInline; ++u) {
-        const unsigned code = u < cnt ? (unsigned)((up4 >> (16 * u)) & 0xffffu) : (unsigned)SLOTS;
-        const bool ext = (code & kExtBit) != 0;
-        ubase[u] = ext ? XE + (code & 0x7fffu) * (unsigned)tile * 8 : XB + code * 16;
-        uinc[u] = ext ? 16u : 0u;
-    }
-    const bool any3 = __any(cnt > 2);                   // wave-uniform
-    const unsigned own = XB + (unsigned)tid * 16;
+    decode_codes<RS>(A, up4A, XB, XE, (unsigned)tile * 8);
+    decode_codes<RS>(B, up4B, XB, XE, (unsigned)tile * 8);
+    const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);   // wave-uniform
+    const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
 
     // forcing rows of the first chunk
-    int rb, nr;
-    chunk_rows(tab, tw0, k0, G, T, rb, nr);
-    double f0 = Fm[(int64_t)clamp_row(rb, nrow) * ns + d];
-    double f1 = Fm[(int64_t)clamp_row(rb + 1, nrow) * ns + d];
-    double f2 = Fm[(int64_t)clamp_row(rb + 2, nrow) * ns + d];
+    int rbA, nrA, rbB, nrB;
+    chunk_rows(tab, tw0, k0, A.G, T, rbA, nrA);
+    chunk_rows(tab, tw0, k0, B.G, T, rbB, nrB);
+    double fA0 = Fm[(int64_t)clamp_row(rbA, nrow) * ns + A.d];
+    double fA1 = Fm[(int64_t)clamp_row(rbA + 1, nrow) * ns + A.d];
+    double fA2 = Fm[(int64_t)clamp_row(rbA + 2, nrow) * ns + A.d];
+    double fB0 = Fm[(int64_t)clamp_row(rbB, nrow) * ns + B.d];
+    double fB1 = Fm[(int64_t)clamp_row(rbB + 1, nrow) * ns + B.d];
+    double fB2 = Fm[(int64_t)clamp_row(rbB + 2, nrow) * ns + B.d];
     __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
     const int wend = gmaxw + T;                         // end of this workgroup's window
-    // feeds another cluster: step t also goes to XS[xsid][t] (address at tick k: xs0 + k)
-    const bool xsrc = live && xsid >= 0;
-    const int64_t xs0 = xsrc ? (int64_t)xsid * T - Gr : 0;
+    double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
+    double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
-        // this chunk's forcing rows -> the lane's LDS slots (private: no barrier needed)
-        double* frl = reinterpret_cast<double*>(lds + FR) + tid * 3;
-        frl[0] = f0;
-        frl[1] = f1;
-        frl[2] = f2;
-        const bool slow = DENSE && __any(nr > 3);       // more rows than slots: load direct
-        const unsigned frp = FR + (unsigned)tid * 24 - (unsigned)rb * 8;
+        // this chunk's forcing rows -> the slots' LDS rows (private: no barrier needed)
+        frA[0] = fA0;
+        frA[1] = fA1;
+        frA[2] = fA2;
+        frB[0] = fB0;
+        frB[1] = fB1;
+        frB[2] = fB2;
+        const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
+        const unsigned frpA = FR + (unsigned)tid * 24 - (unsigned)rbA * 8;
+        const unsigned frpB = FR + (unsigned)(SLOTS + tid) * 24 - (unsigned)rbB * 8;
         // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
-        int rbn, nrn;
-        chunk_rows(tab, tw0, kc + kChunk, G, c + kChunk < tile ? T : 0, rbn, nrn);
-        const double g0 = Fm[(int64_t)clamp_row(rbn, nrow) * ns + d];
-        const double g1 = Fm[(int64_t)clamp_row(rbn + 1, nrow) * ns + d];
-        const double g2 = Fm[(int64_t)clamp_row(rbn + 2, nrow) * ns + d];
-        // per-chunk LDS cursors: upstream value of tick i at m[u] + 8 * ((i + 1) & 1)
-        unsigned m[kUpInline];
+        const int Tn = c + kChunk < tile ? T : 0;
+        int rbAn, nrAn, rbBn, nrBn;
+        chunk_rows(tab, tw0, kc + kChunk, A.G, Tn, rbAn, nrAn);
+        chunk_rows(tab, tw0, kc + kChunk, B.G, Tn, rbBn, nrBn);
+        const double gA0 = Fm[(int64_t)clamp_row(rbAn, nrow) * ns + A.d];
+        const double gA1 = Fm[(int64_t)clamp_row(rbAn + 1, nrow) * ns + A.d];
+        const double gA2 = Fm[(int64_t)clamp_row(rbAn + 2, nrow) * ns + A.d];
+        const double gB0 = Fm[(int64_t)clamp_row(rbBn, nrow) * ns + B.d];
+        const double gB1 = Fm[(int64_t)clamp_row(rbBn + 1, nrow) * ns + B.d];
+        const double gB2 = Fm[(int64_t)clamp_row(rbBn + 2, nrow) * ns + B.d];
+        // per-chunk LDS cursors: input value of tick i at m[u] + 8 * ((i + 1) & 1)
+        unsigned mA[kUpInline], mB[kUpInline];
 #pragma unroll
-        for (int u = 0; u < kUpInline; ++u) m[u] = uinc[u] ? ubase[u] + 8u * c - 8u : ubase[u];
-        const unsigned tp = TAB + (unsigned)(kc - G - tw0) * 16u;
-#pragma unroll
-        for (int h = 0; h < kChunk; h += kHalf) {
-            // lateral inflow of the next kHalf ticks, interpolate_sample (nutils.py:23-33); it
-            // does not depend on the routing state, so it is formed off the tick's critical path
-            double qv[kHalf];
-#pragma unroll
-            for (int j = 0; j < kHalf; ++j) {
-                const int4 e = *reinterpret_cast<const int4*>(lds + tp + 16u * (h + j));
-                double flo, fhi;
-                if (DENSE && slow) {
-                    flo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + d];
-                    fhi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + d];
-                } else {
-                    flo = lds_f64(lds, frp + 8u * (unsigned)e.x);
-                    fhi = lds_f64(lds, frp + 8u * (unsigned)e.y);
-                }
-                const double fr = __hiloint2double(e.w, e.z);
-                const double qi = (1.0 - fr) * flo + fr * fhi;
-                qv[j] = MCR_EXP_NO_Q ? 0.0 : (e.y < 0 ? flo : qi);
-            }
-            if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
-#pragma unroll
-            for (int j = 0; j < kHalf; ++j) {
-                const int i = h + j;
-                if (i & 1) {
-#pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) m[u] += uinc[u];
-                }
-                const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
-                const int t = kc + i - G;
-                const bool act = (unsigned)t < (unsigned)T;
-                // inflow: upstream outflows in reference finalisation order.  Every value a
-                // lane publishes is 0 + (...) or such a sum, never -0.0, so the reference's
-                // leading 0 + is exact without an add
-                double I = lds_f64(lds, m[0] + rd);
-                I = I + lds_f64(lds, m[1] + rd);
-                if (any3) {
-                    I = I + lds_f64(lds, m[2] + rd);
-                    I = I + lds_f64(lds, m[3] + rd);
-                }
-                const double rv = 0.0 + (((al * I + be * ip) + ch * op) + ga * qv[j]);
-                const double ov = psum ? I : rv;
-                // inactive ticks write garbage that no active reach reads (its consumer is
-                // inactive one tick later); never-processed reaches (no consumer) output 0
-                *reinterpret_cast<double*>(lds + own + 8u * (i & 1)) = ov;
-                op = act ? ov : op;
-                ip = act ? I : ip;
-                // one contiguous row per wave; ticks outside the window go to the dummy row
-                const int k = kc + i;
-                const bool inwin = k >= gminw && k < wend;
-                const int64_t row = inwin ? wb + (int64_t)(k - gminw) * SLOTS : 0;
-                double* orow = inwin ? Om + row : dum;
-                if (!MCR_EXP_NO_STORES) {
-                    orow[tid] = routed ? ov : 0.0;
-                    if (xsrc && act) XSm[xs0 + k] = ov;
-                }
-                if (!MCR_EXP_NO_BARRIER) __syncthreads();
-            }
+        for (int u = 0; u < kUpInline; ++u) {
+            mA[u] = A.uinc[u] ? A.ubase[u] + 8u * c - 8u : A.ubase[u];
+            mB[u] = B.uinc[u] ? B.ubase[u] + 8u * c - 8u : B.ubase[u];
         }
-        rb = rbn;
-        nr = nrn;
-        f0 = g0;
-        f1 = g1;
-        f2 = g2;
+        const unsigned tpA = TAB + (unsigned)(kc - A.G - tw0) * 16u;
+        const unsigned tpB = TAB + (unsigned)(kc - B.G - tw0) * 16u;
+        // lateral inflow of the chunk's ticks, interpolate_sample (nutils.py:23-33); it does
+        // not depend on the routing state, so it is formed off the tick's critical path
+        double qA[kChunk], qB[kChunk];
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
+            const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
+            double aLo, aHi, bLo, bHi;
+            if (DENSE && slow) {
+                aLo = Fm[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
+                aHi = Fm[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
+                bLo = Fm[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
+                bHi = Fm[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
+            } else {
+                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
+                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
+                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
+                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
+            }
+            const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
+            const double qa = (1.0 - fa) * aLo + fa * aHi;
+            const double qb = (1.0 - fb) * bLo + fb * bHi;
+            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
+            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
+        }
+        if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) {
+            if (i & 1) {
+#pragma unroll
+                for (int u = 0; u < kUpInline; ++u) {
+                    mA[u] += A.uinc[u];
+                    mB[u] += B.uinc[u];
+                }
+            }
+            const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
+            const int k = kc + i;
+            // low slot
+            const bool actA = (unsigned)(k - A.G) < (unsigned)T;
+            const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
+            const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
+            const double oA = A.psum ? IA : rA;
+            // high slot (may read oA of this tick)
+            const bool actB = (unsigned)(k - B.G) < (unsigned)T;
+            const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
+            const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
+            const double oB = B.psum ? IB : rB;
+            // inactive ticks write garbage that no active node reads (its consumer is inactive
+            // one tick later); never-processed reaches (no consumer) output 0
+            *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
+            *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+            A.op = actA ? oA : A.op;
+            A.ip = actA ? IA : A.ip;
+            B.op = actB ? oB : B.op;
+            B.ip = actB ? IB : B.ip;
+            // one contiguous row of RS values per tick; ticks outside the window: dummy row
+            const bool inwin = k >= gminw && k < wend;
+            double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
+            if (!MCR_EXP_NO_STORES) {
+                orow[tid] = A.routed ? oA : 0.0;
+                orow[SLOTS + tid] = B.routed ? oB : 0.0;
+                if (A.xsrc && actA) XSm[A.xs0 + k] = oA;
+                if (B.xsrc && actB) XSm[B.xs0 + k] = oB;
+            }
+            if (!MCR_EXP_NO_BARRIER) __syncthreads();
+        }
+        rbA = rbAn;
+        nrA = nrAn;
+        rbB = rbBn;
+        nrB = nrBn;
+        fA0 = gA0;
+        fA1 = gA1;
+        fA2 = gA2;
+        fB0 = gB0;
+        fB1 = gB1;
+        fB2 = gB2;
     }
-    // state for the next launch (lanes that did not run keep theirs); never-processed reaches
+    // state for the next launch (slots that did not run keep theirs); never-processed reaches
     // hold o = 0 as in the reference's fresh o_t_next
-    const int64_t ds = (int64_t)blockIdx.y * a.mS + (int64_t)w * SLOTS + threadIdx.x;
-    a.st_o[ds] = routed || psum ? op : 0.0;
-    a.st_i[ds] = ip;
+    const int64_t sb = (int64_t)blockIdx.y * a.mS;
+    a.st_o[sb + A.d] = A.routed || A.psum ? A.op : 0.0;
+    a.st_i[sb + A.d] = A.ip;
+    a.st_o[sb + B.d] = B.routed || B.psum ? B.op : 0.0;
+    a.st_i[sb + B.d] = B.ip;
     if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;

@@ -20,7 +20,7 @@
 namespace mcr {
 
 // Workgroup sizes (plan slots) the kernels are instantiated for.
-#define MCR_SLOT_LIST(X) X(64) X(128) X(192) X(256) X(384) X(448) X(512) X(1024)
+#define MCR_SLOT_LIST(X) X(64) X(128) X(192) X(256) X(384) X(448) X(512)
 
 // Ticks whose lateral inflow is formed in one burst (and whose forcing rows are prefetched
 // together).  Launch lengths (`tile`) are multiples of it.
@@ -86,14 +86,16 @@ struct WaveArgs {
     int32_t ext_cap;              // LDS rows reserved for external inputs
 };
 
+// LDS bytes for `slots` lanes (2 * slots node slots)
 inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile) {
-    return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)table_cap +
-           8 * (size_t)ext_cap * tile;
+    const size_t rs = 2 * (size_t)slots;
+    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
 }
 
 inline size_t flow_lds_bytes(int slots, int T, int ext_cap) {
-    return 16 * ((size_t)slots + 1) + 24 * (size_t)slots + 16 * (size_t)T +
-           2 * (size_t)ext_cap * kChunk * 8 + 4 * kFlowMaxExt;
+    const size_t rs = 2 * (size_t)slots;
+    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)T + 2 * (size_t)ext_cap * kChunk * 8 +
+           4 * kFlowMaxExt;
 }
 
 // One launch for the whole horizon; grid = every workgroup (all must be co-resident).

@@ -30,13 +30,13 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     const int64_t C = params.slots;
     const int32_t B = params.tile;
     if (n < 0) return "n must be >= 0";
-    if (C < 64 || C > 1024 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 1024]";
+    if (C < 64 || C > 512 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 512]";
     if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
     if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";
-    // hard cap of external inputs: what is left of the LDS after the outflow double buffer,
-    // the step-table window and a reserve for overflow upstream codes
+    // hard cap of external inputs: what is left of the LDS after the outflow double buffer and
+    // forcing rows of the 2 * slots node slots and the step-table window
     {
-        const int64_t left = kLdsBudget - 16 * C - kTableEntryBytes * table_entries(C, B) - 4096;
+        const int64_t left = kLdsBudget - 40 * (2 * C + 1) - kTableEntryBytes * table_entries(C, B);
         const int64_t hard = std::min<int64_t>(left / (8 * (int64_t)B), 0x7fff);
         if (hard < 1) return "slots/tile too large for the 160 KiB LDS of a workgroup";
         P.ext_hard = (int32_t)hard;
@@ -211,34 +211,98 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (int64_t k = gin_off[x]; k < gin_off[x + 1]; ++k) cons[gin_list[k]] = x;
     for (int64_t x = 0; x < N; ++x) P.max_height = std::max(P.max_height, h[x]);
 
-    // ---- 4. clustering (bottom-up greedy) -------------------------------------------------
-    // Each reach starts a cluster that absorbs the clusters of its upstream reaches while the
-    // slot and external-input budgets allow.  The deepest upstream is tried first; a shallow
-    // upstream whose value can arrive `tile` ticks late without delaying j is cut for free.
+    // ---- 4. lane pairs -----------------------------------------------------------------
+    // A lane owns two node slots, low (computed first in a tick) and high.  When the high node
+    // consumes the low one the pair is fused: both run step t at the same tick and the high
+    // node takes low's output from a register, so the fused edge costs no tick.  Fusing
+    // alternate edges of a chain halves its depth.  DP over the forest in topological order:
+    // Sx = height of x when it is not the high node of a pair, Fx = height when it is (fused
+    // with its best input fch).  A node is low for at most one pair (it has one consumer).
+    std::vector<int32_t> Sx(N, 0), Fx(N, INT32_MAX), bx(N, 0);
+    std::vector<int64_t> fch(N, -1);
+    for (int64_t x : nodes) {
+        const int64_t k0 = gin_off[x], k1 = gin_off[x + 1];
+        int32_t sx = 0;
+        for (int64_t k = k0; k < k1; ++k) sx = std::max(sx, bx[gin_list[k]] + 1);
+        Sx[x] = sx;
+        for (int64_t k = k0; k < k1; ++k) {
+            int32_t m = Sx[gin_list[k]];
+            for (int64_t q = k0; q < k1; ++q)
+                if (q != k) m = std::max(m, bx[gin_list[q]] + 1);
+            if (m < Fx[x]) {
+                Fx[x] = m;
+                fch[x] = gin_list[k];
+            }
+        }
+        bx[x] = std::min(Sx[x], Fx[x]);
+    }
+    std::vector<int8_t> role(N, 0);         // 0 single, 1 low of a fused pair, 2 high
+    std::vector<int64_t> mate(N, -1);
+    for (auto it = nodes.rbegin(); it != nodes.rend(); ++it) {
+        const int64_t x = *it;
+        if (role[x] == 1 || Fx[x] >= Sx[x]) continue;
+        role[x] = 2;
+        role[fch[x]] = 1;
+        mate[x] = fch[x];
+        mate[fch[x]] = x;
+        P.n_pairs++;
+    }
+    // lane node of every node (a fused pair is represented by its high node), its inputs and
+    // its consumer; a pair's inputs are low's inputs then high's other inputs
+    auto lane_of = [&](int64_t x) { return role[x] == 1 ? mate[x] : x; };
+    std::vector<int64_t> lin_off(N + 1, 0), lin_list;
+    lin_list.reserve(gin_list.size());
+    for (int64_t x = 0; x < N; ++x) {
+        if (role[x] != 1) {
+            if (role[x] == 2) {
+                const int64_t u = mate[x];
+                for (int64_t k = gin_off[u]; k < gin_off[u + 1]; ++k)
+                    lin_list.push_back(gin_list[k]);
+            }
+            for (int64_t k = gin_off[x]; k < gin_off[x + 1]; ++k)
+                if (gin_list[k] != mate[x] || role[x] != 2) lin_list.push_back(lane_of(gin_list[k]));
+            if (role[x] == 2)
+                for (int64_t k = lin_off[x]; k < (int64_t)lin_list.size(); ++k)
+                    lin_list[k] = lane_of(lin_list[k]);
+        }
+        lin_off[x + 1] = (int64_t)lin_list.size();
+    }
+    std::vector<int64_t> lnodes;            // lane nodes in topological order
+    lnodes.reserve(N);
+    for (int64_t x : nodes)
+        if (role[x] != 1) lnodes.push_back(x);
+    auto lcons = [&](int64_t x) { return cons[x] < 0 ? -1 : lane_of(cons[x]); };
+    auto weight = [&](int64_t x) -> int64_t { return role[x] == 2 ? 2 : 1; };
+
+    // ---- 5. clustering (bottom-up greedy) -------------------------------------------------
+    // Each lane node starts a cluster that absorbs the clusters of its inputs while the slot
+    // (2 * slots node slots per workgroup) and external-input budgets allow.  The deepest input
+    // is tried first; a shallow input whose value can arrive `tile` ticks late is cut for free.
+    const int64_t RS = 2 * C;
     std::vector<int64_t> cl(N, -1);
     std::vector<Cluster> clusters;
     std::vector<int32_t> eh(N, 0);          // critical-path estimate (ticks)
-    std::vector<uint8_t> merged(N, 0);      // edge (j -> consumer) is inside a cluster
+    std::vector<uint8_t> merged(N, 0);      // edge (x -> consumer) is inside a cluster
     std::vector<std::vector<int64_t>> members;
     std::vector<int64_t> ups;
-    for (int64_t j : nodes) {
-        ups.assign(gin_list.begin() + gin_off[j], gin_list.begin() + gin_off[j + 1]);
+    for (int64_t j : lnodes) {
+        ups.assign(lin_list.begin() + lin_off[j], lin_list.begin() + lin_off[j + 1]);
         std::stable_sort(ups.begin(), ups.end(),
                          [&](int64_t a, int64_t b) { return eh[a] > eh[b]; });
         Cluster c;
         c.root = j;
-        c.size = 1;
+        c.size = weight(j);
         std::vector<int64_t> absorb;
         int32_t best = ups.empty() ? -1 : eh[ups[0]];
         int32_t ehj = 0;
         bool first = true;
         for (int64_t u : ups) {
             const Cluster& cu = clusters[cl[u]];
-            // merge the deepest upstream, any upstream a cut would delay, and any upstream
-            // once the external-input budget is used up
+            // merge the deepest input, any input a cut would delay, and any input once the
+            // external-input budget is used up
             const bool want = first || (eh[u] + B > best + 1) || (c.ext + 1 > soft);
             first = false;
-            if (want && c.size + cu.size <= C && c.ext + cu.ext <= hard) {
+            if (want && c.size + cu.size <= RS && c.ext + cu.ext <= hard) {
                 c.size += cu.size;
                 c.ext += cu.ext;
                 absorb.push_back(cl[u]);
@@ -252,7 +316,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         if (c.ext > hard) {
             // more external inputs than the LDS can stage: cannot be scheduled
             std::ostringstream m;
-            m << "reach " << j << " needs " << c.ext << " external inputs (LDS cap " << hard
+            m << "node " << j << " needs " << c.ext << " external inputs (LDS cap " << hard
               << " for slots=" << C << ", tile=" << B << ")";
             return m.str();
         }
@@ -282,20 +346,20 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         cl[j] = id;
     }
 
-    // ---- 5. schedule: local ALAP skew + cluster offsets -----------------------------------
-    // distance to the cluster root: walk nodes in reverse (downstream first)
+    // ---- 6. schedule: local ALAP skew + cluster offsets -----------------------------------
+    // distance to the cluster root: walk lane nodes in reverse (downstream first)
     std::vector<int32_t> dist(N, 0);
-    for (auto it = nodes.rbegin(); it != nodes.rend(); ++it) {
+    for (auto it = lnodes.rbegin(); it != lnodes.rend(); ++it) {
         const int64_t j = *it;
-        const int64_t e = cons[j];
+        const int64_t e = lcons(j);
         dist[j] = (e >= 0 && merged[j]) ? dist[e] + 1 : 0;
         Cluster& c = clusters[cl[j]];
         c.dmax = std::max(c.dmax, dist[j]);
     }
     std::vector<int32_t> G(N, 0);
-    // live clusters in root rank order (roots appear in `nodes` order)
+    // live clusters in root order (roots appear in `lnodes` order)
     std::vector<int64_t> live;
-    for (int64_t j : nodes)
+    for (int64_t j : lnodes)
         if (clusters[cl[j]].root == j) live.push_back(cl[j]);
     P.n_clusters = (int64_t)live.size();
     for (int64_t id : live) {
@@ -303,8 +367,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int64_t off = 0;
         for (int64_t v : members[id]) {
             const int32_t s = c.dmax - dist[v];
-            for (int64_t k = gin_off[v]; k < gin_off[v + 1]; ++k) {
-                const int64_t u = gin_list[k];
+            for (int64_t k = lin_off[v]; k < lin_off[v + 1]; ++k) {
+                const int64_t u = lin_list[k];
                 if (cl[u] != id) off = std::max<int64_t>(off, (int64_t)G[u] + B - s);
             }
         }
@@ -312,9 +376,15 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         c.off = (int32_t)off;
         for (int64_t v : members[id]) G[v] = c.off + c.dmax - dist[v];
     }
-    for (int64_t j = 0; j < N; ++j) P.gmax = std::max(P.gmax, G[j]);
+    for (int64_t x = 0; x < N; ++x) {
+        if (role[x] == 1) {
+            G[x] = G[mate[x]];
+            cl[x] = cl[mate[x]];
+        }
+        P.gmax = std::max(P.gmax, G[x]);
+    }
 
-    // ---- 6. pack clusters into workgroups --------------------------------------------------
+    // ---- 7. pack clusters into workgroups --------------------------------------------------
     // First fit in order of schedule offset, so a workgroup holds clusters that are active at
     // the same ticks; its G span is capped so the step-table window fits the LDS.
     std::vector<int64_t> by_off(live);
@@ -330,7 +400,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int64_t w = -1;
         const int64_t nb = (int64_t)wg_fill.size();
         for (int64_t b = std::max<int64_t>(0, nb - kProbe); b < nb; ++b)
-            if (wg_fill[b] + c.size <= C && wg_ext[b] + c.ext <= std::max<int64_t>(soft, c.ext) &&
+            if (wg_fill[b] + c.size <= RS && wg_ext[b] + c.ext <= std::max<int64_t>(soft, c.ext) &&
                 std::max(bin_hi[b], hi) - std::min(bin_lo[b], lo) <= scap) {
                 w = b;
                 break;
@@ -349,12 +419,16 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         c.wg = w;
     }
     P.nwg = (int32_t)wg_fill.size();
-    P.nslots = (int64_t)P.nwg * C;
+    P.nslots = (int64_t)P.nwg * RS;
 
-    // ---- 7. slot assignment (sorted by G inside each workgroup) ---------------------------
-    std::vector<std::vector<int64_t>> wg_nodes(P.nwg);
+    // ---- 8. slot assignment ----------------------------------------------------------------
+    // node slot of a workgroup: lane + (high ? slots : 0).  Fused pairs take whole lanes, the
+    // other nodes fill the remaining low then high slots; both in order of G, so a wave holds
+    // nodes that are active at the same ticks.
+    std::vector<std::vector<int64_t>> wg_pairs(P.nwg), wg_single(P.nwg);
     for (int64_t id : live)
-        for (int64_t v : members[id]) wg_nodes[clusters[id].wg].push_back(v);
+        for (int64_t v : members[id])
+            (role[v] == 2 ? wg_pairs : wg_single)[clusters[id].wg].push_back(v);
     P.slot_reach.assign(P.nslots, -1);
     P.G.assign(P.nslots, 0);
     P.flags.assign(P.nslots, kSlotPad);
@@ -364,28 +438,46 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     std::vector<int64_t> npos(N, -1);       // node -> slot
     P.wg_gmin.assign(P.nwg, 0);
     P.wg_gmax.assign(P.nwg, 0);
-    for (int32_t w = 0; w < P.nwg; ++w) {
-        auto& v = wg_nodes[w];
-        std::stable_sort(v.begin(), v.end(), [&](int64_t a, int64_t b) { return G[a] < G[b]; });
-        for (size_t k = 0; k < v.size(); ++k) {
-            const int64_t d = (int64_t)w * C + (int64_t)k;
-            const int64_t x = v[k];
-            npos[x] = d;
-            P.G[d] = G[x];
-            if (x < n) {
-                P.slot_reach[d] = x;
-                P.pos[x] = d;
-                P.flags[d] = P.rank[x] >= 0 ? kSlotRouted : kSlotUnrouted;
-            } else {
-                P.flags[d] = kSlotSum;
-            }
+    auto place = [&](int64_t x, int64_t d) {
+        npos[x] = d;
+        P.G[d] = G[x];
+        if (x < n) {
+            P.slot_reach[d] = x;
+            P.pos[x] = d;
+            P.flags[d] = P.rank[x] >= 0 ? kSlotRouted : kSlotUnrouted;
+        } else {
+            P.flags[d] = kSlotSum;
         }
-        P.wg_gmin[w] = v.empty() ? 0 : G[v.front()];
-        P.wg_gmax[w] = v.empty() ? 0 : G[v.back()];
+    };
+    auto byG = [&](int64_t a, int64_t b) { return G[a] < G[b]; };
+    for (int32_t w = 0; w < P.nwg; ++w) {
+        auto& pr = wg_pairs[w];
+        auto& sg = wg_single[w];
+        std::stable_sort(pr.begin(), pr.end(), byG);
+        std::stable_sort(sg.begin(), sg.end(), byG);
+        const int64_t base = (int64_t)w * RS;
+        int64_t lane = 0;
+        for (int64_t x : pr) {
+            place(mate[x], base + lane);
+            place(x, base + C + lane);
+            ++lane;
+        }
+        if ((int64_t)pr.size() * 2 + (int64_t)sg.size() > RS) return "internal: workgroup overfull";
+        size_t k = 0;
+        for (int64_t l = lane; l < C && k < sg.size(); ++l) place(sg[k++], base + l);
+        for (int64_t l = lane; l < C && k < sg.size(); ++l) place(sg[k++], base + C + l);
+        int32_t lo = INT32_MAX, hi = INT32_MIN;
+        for (int64_t d = base; d < base + RS; ++d)
+            if (P.flags[d] != kSlotPad) {
+                lo = std::min(lo, P.G[d]);
+                hi = std::max(hi, P.G[d]);
+            }
+        P.wg_gmin[w] = lo == INT32_MAX ? 0 : lo;
+        P.wg_gmax[w] = lo == INT32_MAX ? 0 : hi;
         P.max_span = std::max(P.max_span, P.wg_gmax[w] - P.wg_gmin[w]);
         if ((int64_t)P.wg_gmax[w] - P.wg_gmin[w] > scap) return "internal: workgroup G span";
     }
-    // upstream codes and external lists
+    // input codes and external lists
     P.ext_off.assign(P.nwg + 1, 0);
     std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src node, consumer G)
     std::vector<int64_t> node_at(P.nslots, -1);
@@ -393,7 +485,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     for (int64_t d = 0; d < P.nslots; ++d) {
         const int64_t j = node_at[d];
         if (j < 0) continue;
-        const int32_t w = (int32_t)(d / C);
+        const int32_t w = (int32_t)(d / RS);
         const int64_t k0 = gin_off[j], k1 = gin_off[j + 1];
         if (k1 - k0 > kUpInline) return "internal: more than kUpInline inputs";
         P.up_cnt[d] = (uint8_t)(k1 - k0);
@@ -401,9 +493,12 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (int64_t k = k0; k < k1; ++k) {
             const int64_t u = gin_list[k];
             uint16_t code;
-            if (cl[u] == cl[j]) {
+            if (role[j] == 2 && u == mate[j]) {
+                if (npos[u] != d - C || G[u] != G[j]) return "internal: fused pair layout";
+                code = kSelfCode;
+            } else if (cl[u] == cl[j]) {
                 if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";
-                code = (uint16_t)(npos[u] - (int64_t)w * C);
+                code = (uint16_t)(npos[u] - (int64_t)w * RS);
             } else {
                 if (G[j] < G[u] + B) return "internal: cross-cluster edge without tile slack";
                 const size_t e = ext[w].size();

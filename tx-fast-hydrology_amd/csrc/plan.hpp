@@ -41,6 +41,8 @@ constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 
 // upstream code: bit 15 set -> index into the workgroup's external-input list, else the
 // workgroup-local slot of the upstream reach.
 constexpr uint16_t kExtBit = 0x8000;
+// code of a fused pair's low node in its high node's list: low's output of the same tick
+constexpr uint16_t kSelfCode = 0x7fff;
 constexpr int kUpInline = 4;  // upstream values one lane reads per tick (codes in registers)
 
 enum SlotFlags : uint8_t {
@@ -61,6 +63,7 @@ struct Plan {
     int64_t n_cross = 0;           // cross-cluster edges
     int32_t max_height = 0;        // longest upstream path (levels - 1, partial sums included)
     int64_t n_partial = 0;         // partial-sum nodes
+    int64_t n_pairs = 0;           // fused lane pairs
     int32_t max_ext_wg = 0;
     int32_t ext_hard = 0;          // LDS-derived hard cap of cross-cluster inputs per workgroup
     int32_t max_span = 0;          // max G span inside one workgroup

@@ -47,7 +47,8 @@ class PlanInfo(ctypes.Structure):
                 ("nslots", ctypes.c_int64), ("nwg", ctypes.c_int32), ("slots", ctypes.c_int32),
                 ("tile", ctypes.c_int32), ("gmax", ctypes.c_int32),
                 ("max_height", ctypes.c_int32), ("max_ext_wg", ctypes.c_int32),
-                ("n_partial", ctypes.c_int64), ("n_ext", ctypes.c_int64)]
+                ("n_partial", ctypes.c_int64), ("n_ext", ctypes.c_int64),
+                ("n_pairs", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
