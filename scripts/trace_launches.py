@@ -73,6 +73,15 @@ def summarize_flow(rec, khz, gmin, gmax, T):
     print(f"SUMMARY total_us={(en.max() - t0) * us:.1f} median_ns_per_tick={np.median(ns_tick):.0f}")
 
 
+def wg_windows(plan):
+    """G range of every workgroup's node slots (2 * slots per workgroup, padding excluded)."""
+    ex, ln = plan.export(), plan.export_links()
+    rs = 2 * plan.info["slots"]
+    G = ex["G"].reshape(-1, rs)
+    used = ln["flags"].reshape(G.shape) != 0
+    return np.where(used, G, 1 << 30).min(1), np.where(used, G, -1).max(1)
+
+
 def main():
     argv = sys.argv[1:]
     quiet = "--quiet" in argv
@@ -98,11 +107,7 @@ def main():
         heads = np.flatnonzero(wl.indeg == 0)
         plan = engine.Plan(wl.end, wl.indeg, heads, slots=net.info["slots"],
                            tile=net.info["tile"])
-        ex = plan.export()
-        G = ex["G"].reshape(-1, net.info["slots"])
-        real = ex["slot_reach"].reshape(G.shape) >= 0
-        gmin = np.where(real, G, 1 << 30).min(1)
-        gmax = np.where(real, G, -1).max(1)
+        gmin, gmax = wg_windows(plan)
         summarize_flow(rec, khz, gmin, gmax, len(wl.x))
     else:
         summarize(rec, khz, net.info["tile"], quiet)

@@ -10,6 +10,7 @@ namespace mcr {
 
 namespace {
 
+
 struct Cluster {
     int64_t root = -1;
     int64_t size = 0;
@@ -217,7 +218,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // node takes low's output from a register, so the fused edge costs no tick.  Fusing
     // alternate edges of a chain halves its depth.  DP over the forest in topological order:
     // Sx = height of x when it is not the high node of a pair, Fx = height when it is (fused
-    // with its best input fch).  A node is low for at most one pair (it has one consumer).
+    // with its last input fch).  A node is low for at most one pair (it has one consumer).
     std::vector<int32_t> Sx(N, 0), Fx(N, INT32_MAX), bx(N, 0);
     std::vector<int64_t> fch(N, -1);
     for (int64_t x : nodes) {
@@ -225,7 +226,9 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int32_t sx = 0;
         for (int64_t k = k0; k < k1; ++k) sx = std::max(sx, bx[gin_list[k]] + 1);
         Sx[x] = sx;
-        for (int64_t k = k0; k < k1; ++k) {
+        // only x's last input (in fold order) may be its low mate: the high node then adds the
+        // register value last, one add after low's output (kernels.hip, fold)
+        for (int64_t k = std::max(k0, k1 - 1); k < k1; ++k) {
             int32_t m = Sx[gin_list[k]];
             for (int64_t q = k0; q < k1; ++q)
                 if (q != k) m = std::max(m, bx[gin_list[q]] + 1);
@@ -279,6 +282,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // (2 * slots node slots per workgroup) and external-input budgets allow.  The deepest input
     // is tried first; a shallow input whose value can arrive `tile` ticks late is cut for free.
     const int64_t RS = 2 * C;
+    const int64_t scap = span_cap(C);
     std::vector<int64_t> cl(N, -1);
     std::vector<Cluster> clusters;
     std::vector<int32_t> eh(N, 0);          // critical-path estimate (ticks)
@@ -302,9 +306,12 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             // external-input budget is used up
             const bool want = first || (eh[u] + B > best + 1) || (c.ext + 1 > soft);
             first = false;
-            if (want && c.size + cu.size <= RS && c.ext + cu.ext <= hard) {
+            // the cluster's tick span (in-cluster depth) must fit one workgroup's window
+            if (want && c.size + cu.size <= RS && c.ext + cu.ext <= hard &&
+                cu.dmax + 1 <= scap) {
                 c.size += cu.size;
                 c.ext += cu.ext;
+                c.dmax = std::max(c.dmax, cu.dmax + 1);
                 absorb.push_back(cl[u]);
                 merged[u] = 1;
                 ehj = std::max(ehj, eh[u] + 1);
@@ -349,6 +356,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // ---- 6. schedule: local ALAP skew + cluster offsets -----------------------------------
     // distance to the cluster root: walk lane nodes in reverse (downstream first)
     std::vector<int32_t> dist(N, 0);
+    for (Cluster& c : clusters) c.dmax = 0;
     for (auto it = lnodes.rbegin(); it != lnodes.rend(); ++it) {
         const int64_t j = *it;
         const int64_t e = lcons(j);
@@ -391,7 +399,6 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     std::stable_sort(by_off.begin(), by_off.end(), [&](int64_t a, int64_t b) {
         return clusters[a].off < clusters[b].off;
     });
-    const int64_t scap = span_cap(C);
     std::vector<int64_t> wg_fill, wg_ext, bin_lo, bin_hi;
     const int kProbe = 64;  // bounded first fit over the most recent bins keeps packing O(n)
     for (int64_t id : by_off) {
@@ -482,19 +489,26 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src node, consumer G)
     std::vector<int64_t> node_at(P.nslots, -1);
     for (int64_t x = 0; x < N; ++x) node_at[npos[x]] = x;
+    // code positions: the first cnt - 1 inputs in positions 0.., the LAST input (in fold order)
+    // in position kUpInline - 1, the zero slot (RS) elsewhere.  The kernel folds
+    // ((v0 + v1) + v2) + v3; adding the zero slot's +0.0 to a value that is never -0.0 is
+    // exact, so this is the reference's left fold for every cnt.
     for (int64_t d = 0; d < P.nslots; ++d) {
         const int64_t j = node_at[d];
+        uint64_t packed = 0;
+        for (int u = 0; u < kUpInline; ++u) packed |= (uint64_t)RS << (16 * u);
+        P.up4[d] = packed;
         if (j < 0) continue;
         const int32_t w = (int32_t)(d / RS);
         const int64_t k0 = gin_off[j], k1 = gin_off[j + 1];
         if (k1 - k0 > kUpInline) return "internal: more than kUpInline inputs";
         P.up_cnt[d] = (uint8_t)(k1 - k0);
-        uint64_t packed = 0;
         for (int64_t k = k0; k < k1; ++k) {
             const int64_t u = gin_list[k];
             uint16_t code;
             if (role[j] == 2 && u == mate[j]) {
-                if (npos[u] != d - C || G[u] != G[j]) return "internal: fused pair layout";
+                if (npos[u] != d - C || G[u] != G[j] || k != k1 - 1)
+                    return "internal: fused pair layout";
                 code = kSelfCode;
             } else if (cl[u] == cl[j]) {
                 if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";
@@ -507,7 +521,9 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
                 code = (uint16_t)(kExtBit | e);
                 P.n_cross++;
             }
-            packed |= (uint64_t)code << (16 * (k - k0));
+            const int pos = k == k1 - 1 ? kUpInline - 1 : (int)(k - k0);
+            packed &= ~((uint64_t)0xffff << (16 * pos));
+            packed |= (uint64_t)code << (16 * pos);
         }
         P.up4[d] = packed;
     }
