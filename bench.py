@@ -44,8 +44,9 @@ def parse():
     ap.add_argument("--depth", type=int, default=1500)
     ap.add_argument("--T", type=int, default=288)
     ap.add_argument("--dt", type=float, default=300.0)
-    # 0 = per workload: 448 lanes + the helper wave make the deterministic Texas network one
-    # resident dataflow launch; ensembles run the multi-launch path at 256
+    # 0 = per workload: 384 lanes (2 node slots each) + the helper wave make the deterministic
+    # Texas network one resident dataflow launch (one workgroup per CU); ensembles run the
+    # multi-launch path at 256
     ap.add_argument("--slots", type=int, default=0)
     ap.add_argument("--members", type=int, default=1,
                     help="ensemble members (BASELINE configs[2]: 64); 1 = deterministic")
@@ -131,7 +132,7 @@ def build_workload(args, rank=0, world=1):
     i0 = np.zeros(o0.shape)
     np.add.at(i0, end, o0)                                      # muskingum.py:416-417
 
-    slots = args.slots or (448 if E == 1 else 256)
+    slots = args.slots or (384 if E == 1 else 256)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=args.tile, members=E)
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)

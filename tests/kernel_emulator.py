@@ -65,6 +65,7 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
     lo, hi, w0, w1 = step_tables(np.asarray(x, float), np.asarray(xp, float))
     G = ex["G"].astype(np.int64)
     fl = ln["flags"]
+    cnt = ln["up_cnt"].astype(np.int64)
     codes = np.zeros((nslots, 4), np.int64)
     for c in range(4):
         codes[:, c] = (ln["up4"] >> np.uint64(16 * c)).astype(np.int64) & 0xFFFF
@@ -101,6 +102,7 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
             xb[:, RS] = 0.0
             xb[(k0 - 1) & 1, :RS] = op
             cd = codes[d]
+            cn = cnt[d]
             for i in range(tile):
                 kk = k0 + i
                 t = kk - g
@@ -115,8 +117,8 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
                 cur = xb[kk & 1]
                 for half in (slice(0, C), slice(C, RS)):
                     Iv = np.zeros(RS)
-                    for c in range(4):                 # positional codes, pad = zero slot
-                        m = act.copy()
+                    for c in range(4):
+                        m = act & (c < cn)
                         m[:half.start] = False
                         m[half.stop:] = False
                         code = cd[:, c]

@@ -133,15 +133,11 @@ int64_t searchsorted_left(const double* xp, int64_t n, double x) {
     return lo;
 }
 
-// {row_lo, row_hi (-1: copy row_lo), 1 - frac, frac}: the device forms
-// (1 - frac) * f[lo] + frac * f[hi] exactly as numpy does (nutils.py:31-33)
-mcr::StepEntry step_entry(int lo, int hi, double frac) {
-    mcr::StepEntry e{};
-    e.lo = lo;
-    e.hi = hi;
-    e.w0 = 1.0 - frac;
-    e.w1 = frac;
-    return e;
+// {row_lo, row_hi (-1: copy row_lo), frac as two 32-bit halves (lo, hi)}
+int4 step_entry(int lo, int hi, double frac) {
+    uint64_t bits;
+    std::memcpy(&bits, &frac, sizeof(bits));
+    return make_int4(lo, hi, (int)(uint32_t)(bits & 0xffffffffu), (int)(uint32_t)(bits >> 32));
 }
 
 struct Net {
@@ -162,7 +158,7 @@ struct Net {
     int64_t n_rows = 0;
     std::vector<double> xp;
     // per-step interpolation table {row_lo, row_hi, frac}
-    DBuf<mcr::StepEntry> stab;
+    DBuf<int4> stab;
     // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
     // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
     // and the dummy row of out-of-window ticks
@@ -604,7 +600,7 @@ struct Net {
             hit->wbase.upload(wb.data(), wb.size(), stream);
             hit->Otot = total;
             hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
-            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, plan.p.slots,
+            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, row_width(),
                                           plan.n, hit->jbase.p, stream));
             sync();
         }
@@ -623,8 +619,7 @@ struct Net {
     }
 
     // Run T steps using forcing buffer `Fsrc` with `rows` rows and the host step table.
-    void run_tables(int64_t T, const double* Fsrc, int64_t rows,
-                    const std::vector<mcr::StepEntry>& tabh) {
+    void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int4>& tabh) {
         REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
         REQUIRE(T >= 1 && T < (1ll << 30), "T out of range");
         const int64_t n = plan.n;
@@ -637,8 +632,8 @@ struct Net {
         bool dense = false;
         for (int64_t t = 0; t < T && !dense; ++t) {
             const int64_t t2 = std::min<int64_t>(t + mcr::kChunk - 1, T - 1);
-            const int last = std::max(tabh[t2].lo, tabh[t2].hi);
-            dense = last - tabh[t].lo + 1 > 3;
+            const int last = std::max(tabh[t2].x, tabh[t2].y);
+            dense = last - tabh[t].x + 1 > 3;
         }
         upload_async(stab, tabh.data(), tabh.size());
         last_path = 0;
@@ -775,7 +770,7 @@ struct Net {
         REQUIRE(x != nullptr, "x must not be NULL");
         for (int64_t t = 1; t < T; ++t)
             REQUIRE(!(x[t] < x[t - 1]), "step times x must be non-decreasing");
-        std::vector<mcr::StepEntry> tab(T);
+        std::vector<int4> tab(T);
         for (int64_t t = 0; t < T; ++t) {  // nutils.py:21-33
             const double xt = x[t];
             const int64_t ix = searchsorted_left(xp.data(), n_rows, xt);
@@ -798,7 +793,7 @@ struct Net {
         const int64_t n = plan.n;
         Fstep.reserve((size_t)(std::max<int64_t>(plan.nslots, 1) * E));
         if (n) to_slots(q, Fstep, E);
-        run_tables(1, Fstep.p, 1, std::vector<mcr::StepEntry>(1, step_entry(0, -1, 0.0)));
+        run_tables(1, Fstep.p, 1, std::vector<int4>(1, step_entry(0, -1, 0.0)));
         if (n) {  // the new state is the output of the step
             from_slots(st_o, o_out, E);
             from_slots(st_i, i_out, E);

@@ -12,7 +12,7 @@ namespace dev {
 // Forcing rows a lane needs for the chunk starting at tick kc: [rb, rb + nr).  Rows are
 // non-decreasing in t (step times are increasing), so the first step's row_lo and the last
 // step's max(row_lo, row_hi) bound them.  nr = 0 when the lane has no step in the chunk.
-__device__ __forceinline__ void chunk_rows(const StepEntry* tab, int tw0, int kc, int G, int T,
+__device__ __forceinline__ void chunk_rows(const int4* tab, int tw0, int kc, int G, int T,
                                            int& rb, int& nr) {
     int ta = kc - G, tb = kc + kChunk - 1 - G;
     if (tb < 0 || ta >= T) {
@@ -22,9 +22,9 @@ __device__ __forceinline__ void chunk_rows(const StepEntry* tab, int tw0, int kc
     }
     ta = ta < 0 ? 0 : ta;
     tb = tb >= T ? T - 1 : tb;
-    const int lo = tab[ta - tw0].lo;
-    const int2 eb = *reinterpret_cast<const int2*>(&tab[tb - tw0]);
-    rb = lo;
+    const int4 ea = tab[ta - tw0];
+    const int4 eb = tab[tb - tw0];
+    rb = ea.x;
     nr = (eb.y > eb.x ? eb.y : eb.x) - rb + 1;
 }
 
@@ -41,12 +41,11 @@ __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
 struct Slot {
     int64_t d;            // node slot
     int G;                // tick of step 0 (huge when the slot has no work in this launch)
-    bool real;            // not a padding slot (a real slot keeps its state when idle)
     bool routed, psum, xsrc;
     double al, be, ch, ga, op, ip;
     int cnt;
     unsigned ubase[kUpInline], uinc[kUpInline];
-    bool self_last;        // last input = the lane's low output of this tick (fused pair)
+    bool self[kUpInline];  // code reads the lane's low output of this tick (fused pair)
     int64_t xs0;           // XS address of tick 0 when the slot feeds another cluster
 };
 
@@ -59,7 +58,6 @@ __device__ __forceinline__ void load_slot(Slot& s, const WaveArgs& a, int64_t d,
     const int t_first = k0 - Gr;                        // step at this launch's first tick
     const bool live = real && (t_first < T) && (t_first + tile > 0);
     s.d = d;
-    s.real = real;
     s.G = live ? Gr : (1 << 29);                        // never active when not live
     s.routed = fl == kSlotRouted;
     s.psum = fl == kSlotSum;
@@ -76,37 +74,37 @@ __device__ __forceinline__ void load_slot(Slot& s, const WaveArgs& a, int64_t d,
     s.xs0 = s.xsrc ? (int64_t)xsid * T - Gr : 0;
 }
 
-// input codes -> LDS byte bases.  Codes are positional (plan.cpp): the last input sits in
-// position kUpInline - 1, unused positions name the zero slot RS.  A SELF code (only ever in the
-// last position) also reads the zero slot and is replaced by the low output in `fold`.
+// input codes -> LDS byte bases; unused codes read the zero slot (adding +0.0 to a sum that
+// started as a published value is exact, so the sum needs no predicate)
 template <int RS>
 __device__ __forceinline__ void decode_codes(Slot& s, uint64_t up4, unsigned XB, unsigned XE,
                                              unsigned ext_stride) {
 #pragma unroll
     for (int u = 0; u < kUpInline; ++u) {
-        unsigned code = (unsigned)((up4 >> (16 * u)) & 0xffffu);
-        if (s.cnt == 0) code = RS;                      // idle / padding slot: read zeros
-        if (u == kUpInline - 1) s.self_last = code == kSelfCode;
-        if (code == kSelfCode) code = RS;
+        unsigned code = u < s.cnt ? (unsigned)((up4 >> (16 * u)) & 0xffffu) : (unsigned)RS;
+        s.self[u] = code == kSelfCode;
+        if (s.self[u]) code = RS;
         const bool ext = (code & kExtBit) != 0;
         s.ubase[u] = ext ? XE + (code & 0x7fffu) * ext_stride : XB + code * 16;
         s.uinc[u] = ext ? 16u : 0u;
     }
 }
 
-// The four input values of a slot at tick parity rd (issued together at the start of a tick).
-__device__ __forceinline__ void load_inputs(const char* lds, const unsigned* m, unsigned rd,
-                                            double (&v)[kUpInline]) {
-#pragma unroll
-    for (int u = 0; u < kUpInline; ++u) v[u] = lds_f64(lds, m[u] + rd);
-}
-
-// Inflow fold in reference finalisation order: ((v0 + v1) + v2) + last.  Every value a lane
-// publishes is 0 + (...) or such a sum, never -0.0, so the reference's leading 0 + and the
-// zero-slot padding are exact.  `last` is v3, or the lane's low output of this tick when the
-// slot is the high node of a fused pair (one add after the low output is known).
-__device__ __forceinline__ double prefix3(const double (&v)[kUpInline]) {
-    return (v[0] + v[1]) + v[2];
+// inflow fold in reference finalisation order.  Every value a lane publishes is 0 + (...) or
+// such a sum, never -0.0, so the reference's leading 0 + is exact without an add.  HIGH: the
+// slot may read its lane's low output of this tick (`low`) in place of a code.
+template <bool HIGH>
+__device__ __forceinline__ double fold(const char* lds, const unsigned* m, const bool* self,
+                                       unsigned rd, bool any3, double low) {
+    const double v0 = lds_f64(lds, m[0] + rd), v1 = lds_f64(lds, m[1] + rd);
+    double I = HIGH && self[0] ? low : v0;
+    I = I + (HIGH && self[1] ? low : v1);
+    if (any3) {
+        const double v2 = lds_f64(lds, m[2] + rd), v3 = lds_f64(lds, m[3] + rd);
+        I = I + (HIGH && self[2] ? low : v2);
+        I = I + (HIGH && self[3] ? low : v3);
+    }
+    return I;
 }
 
 }  // namespace dev

@@ -19,7 +19,6 @@
 #include "plan.hpp"
 
 #include <algorithm>
-#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -32,9 +31,6 @@
 #ifndef MCR_EXP_NO_HELPER
 #define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
 #endif
-#ifndef MCR_EXP_NO_BARRIER
-#define MCR_EXP_NO_BARRIER 0     // diagnostic: no tick barriers (results are wrong)
-#endif
 
 namespace mcr {
 
@@ -46,8 +42,7 @@ using dev::lds_f64;
 using dev::Slot;
 using dev::load_slot;
 using dev::decode_codes;
-using dev::load_inputs;
-using dev::prefix3;
+using dev::fold;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -149,7 +144,7 @@ struct Helper {
 };
 
 // LDS layout (bytes), RS = 2 * SLOTS node slots (lane l: slots l and SLOTS + l):
-//   XB [RS + 1][2] f64 | FR [RS][3] f64 | TAB [T] StepEntry (whole step table)
+//   XB [RS + 1][2] f64 | FR [RS][3] f64 | TAB [T] int4 (whole step table)
 //   | XE [2][ext_cap][kChunk] f64 (ring of external inputs, one slot per chunk parity)
 //   | EG [kFlowMaxExt] i32 (consumer G)
 // Each tick a lane routes its low slot, then its high slot (fused pairs: kernels.hip).
@@ -162,11 +157,11 @@ void wavefront_flow(WaveArgs a) {
     constexpr unsigned FR = XB + (RS + 1) * 16;
     constexpr unsigned TAB = FR + RS * 24;
     const int T = a.T;
-    const unsigned XE = TAB + (unsigned)a.table_cap * (unsigned)sizeof(StepEntry);
+    const unsigned XE = TAB + (unsigned)a.table_cap * 16;
     const unsigned XSLOT = (unsigned)a.ext_cap * kChunk * 8;
     const unsigned EG = XE + 2 * XSLOT;
     double* xbp = reinterpret_cast<double*>(lds + XB);
-    StepEntry* tab = reinterpret_cast<StepEntry*>(lds + TAB);
+    int4* tab = reinterpret_cast<int4*>(lds + TAB);
 
     const int tid = threadIdx.x;
     const int nthr = SLOTS + kHelperLanes;
@@ -195,28 +190,28 @@ void wavefront_flow(WaveArgs a) {
         for (int b = 0; b < nb; ++b) h.fetch_now(b, kb, (unsigned)((kb >> 3) & 1));
         __syncthreads();                     // prologue barrier (matches the compute waves)
         for (int kc = kb; kc < wend; kc += kChunk) {
-            // granules of the next chunk: both batches issued at the chunk start, consumed
-            // just before its last tick barrier, so the loads have seven ticks to land
             const int kn = kc + kChunk;
             const bool pre = kn < wend && nb > 0 && !MCR_EXP_NO_HELPER;
             const unsigned slot = (unsigned)((kn >> 3) & 1);
-            u32x4 g0[kBatch], g1[kBatch];
+            u32x4 g[kBatch];
+            if (pre) h.issue(0, kn, g);
+            __syncthreads();                 // tick 0
+            __syncthreads();                 // tick 1
+            __syncthreads();                 // tick 2
             if (pre) {
-                h.issue(0, kn, g0);
-                if (nb > 1) h.issue(1, kn, g1);
-            }
-#pragma unroll
-            for (int i = 0; i < kChunk - 1; ++i)
-                if (!MCR_EXP_NO_BARRIER) __syncthreads();   // ticks 0 .. 6
-            if (pre) {
-                int bad = h.consume(0, kn, slot, g0);
+                const int bad = h.consume(0, kn, slot, g);
                 if (__any(bad >= 0)) h.settle(0, kn, slot, bad);
-                if (nb > 1) {
-                    bad = h.consume(1, kn, slot, g1);
-                    if (__any(bad >= 0)) h.settle(1, kn, slot, bad);
-                }
+                if (nb > 1) h.issue(1, kn, g);
             }
-            if (!MCR_EXP_NO_BARRIER) __syncthreads();       // tick 7
+            __syncthreads();                 // tick 3
+            __syncthreads();                 // tick 4
+            __syncthreads();                 // tick 5
+            if (pre && nb > 1) {
+                const int bad = h.consume(1, kn, slot, g);
+                if (__any(bad >= 0)) h.settle(1, kn, slot, bad);
+            }
+            __syncthreads();                 // tick 6
+            __syncthreads();                 // tick 7
         }
         return;
     }
@@ -236,6 +231,7 @@ void wavefront_flow(WaveArgs a) {
 
     decode_codes<RS>(A, up4A, XB, XE, kChunk * 8);
     decode_codes<RS>(B, up4B, XB, XE, kChunk * 8);
+    const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);
     const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
 
     int rbA, nrA, rbB, nrB;
@@ -255,12 +251,6 @@ void wavefront_flow(WaveArgs a) {
 
     double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
     double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
-    // a chunk where every real slot of the wave is active at all its ticks takes the FULL path
-    // (no per-tick activity selects); padding slots never matter, a real slot without work in
-    // this chunk keeps its state, so it forces the EDGE path
-    const int loA = A.real ? A.G : INT32_MIN / 2, hiA = A.real ? A.G + T : INT32_MAX / 2;
-    const int loB = B.real ? B.G : INT32_MIN / 2, hiB = B.real ? B.G + T : INT32_MAX / 2;
-    const bool any_real = __any(A.real || B.real);
     for (int kc = kb; kc < wend; kc += kChunk) {
         const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
         frA[0] = fA0;
@@ -288,103 +278,75 @@ void wavefront_flow(WaveArgs a) {
             mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
             mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
         }
-        const unsigned tpA = TAB + (unsigned)(kc - A.G) * sizeof(StepEntry);
-        const unsigned tpB = TAB + (unsigned)(kc - B.G) * sizeof(StepEntry);
+        const unsigned tpA = TAB + (unsigned)(kc - A.G) * 16u;
+        const unsigned tpB = TAB + (unsigned)(kc - B.G) * 16u;
         double qA[kChunk], qB[kChunk];
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
-            const StepEntry ea = *reinterpret_cast<const StepEntry*>(lds + tpA + 32u * j);
-            const StepEntry eb = *reinterpret_cast<const StepEntry*>(lds + tpB + 32u * j);
+            const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
+            const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
             double aLo, aHi, bLo, bHi;
             if (DENSE && slow) {
-                aLo = a.F[(int64_t)clamp_row(ea.lo < 0 ? 0 : ea.lo, nrow) * ns + A.d];
-                aHi = a.F[(int64_t)clamp_row(ea.hi < 0 ? 0 : ea.hi, nrow) * ns + A.d];
-                bLo = a.F[(int64_t)clamp_row(eb.lo < 0 ? 0 : eb.lo, nrow) * ns + B.d];
-                bHi = a.F[(int64_t)clamp_row(eb.hi < 0 ? 0 : eb.hi, nrow) * ns + B.d];
+                aLo = a.F[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
+                aHi = a.F[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
+                bLo = a.F[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
+                bHi = a.F[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
             } else {
-                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.lo);
-                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.hi);
-                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.lo);
-                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.hi);
+                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
+                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
+                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
+                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
             }
-            const double qa = ea.w0 * aLo + ea.w1 * aHi;
-            const double qb = eb.w0 * bLo + eb.w1 * bHi;
-            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.hi < 0 ? aLo : qa);
-            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.hi < 0 ? bLo : qb);
+            const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
+            const double qa = (1.0 - fa) * aLo + fa * aHi;
+            const double qb = (1.0 - fb) * bLo + fb * bHi;
+            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
+            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
         }
         if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
-        auto ticks = [&](auto full_tag) {
-            constexpr bool FULL = decltype(full_tag)::value;
 #pragma unroll
-            for (int i = 0; i < kChunk; ++i) {
-                if (i & 1) {
+        for (int i = 0; i < kChunk; ++i) {
+            if (i & 1) {
 #pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) {
-                        mA[u] += A.uinc[u];
-                        mB[u] += B.uinc[u];
-                    }
+                for (int u = 0; u < kUpInline; ++u) {
+                    mA[u] += A.uinc[u];
+                    mB[u] += B.uinc[u];
                 }
-                const unsigned rd = 8u * ((i + 1) & 1);
-                const int k = kc + i;
-                // all eight input reads of the tick first: the high slot's reads must not
-                // wait behind the low slot's recurrence
-                double vA[kUpInline], vB[kUpInline];
-                load_inputs(lds, mA, rd, vA);
-                load_inputs(lds, mB, rd, vB);
-                __builtin_amdgcn_sched_barrier(0);
-                const double IA = prefix3(vA) + vA[kUpInline - 1];
-                const double PB = prefix3(vB);   // independent of the low slot's chain
-                const double rA =
-                    0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
-                const double oA = A.psum ? IA : rA;
-                const double IB = PB + (B.self_last ? oA : vB[kUpInline - 1]);
-                const double rB =
-                    0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
-                const double oB = B.psum ? IB : rB;
-                *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
-                bool actA = true, actB = true;
-                double* orow;
-                if (FULL) {
-                    A.op = oA;
-                    A.ip = IA;
-                    B.op = oB;
-                    B.ip = IB;
-                    orow = a.O + wb + (int64_t)(k - gminw) * RS;
-                } else {
-                    actA = (unsigned)(k - A.G) < (unsigned)T;
-                    actB = (unsigned)(k - B.G) < (unsigned)T;
-                    A.op = actA ? oA : A.op;
-                    A.ip = actA ? IA : A.ip;
-                    B.op = actB ? oB : B.op;
-                    B.ip = actB ? IB : B.ip;
-                    const bool inwin = k >= gminw && k < wend;
-                    orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
-                }
-                if (!MCR_EXP_NO_STORES)
-                    reinterpret_cast<double2*>(orow)[tid] =
-                        make_double2(A.routed ? oA : 0.0, B.routed ? oB : 0.0);
-                if (A.xsrc && actA) {
-                    const uint64_t bits = (uint64_t)__double_as_longlong(oA);
-                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16),
-                                                           0, 16);
-                }
-                if (B.xsrc && actB) {
-                    const uint64_t bits = (uint64_t)__double_as_longlong(oB);
-                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16),
-                                                           0, 16);
-                }
-                if (!MCR_EXP_NO_BARRIER) __syncthreads();
             }
-        };
-        const bool full = any_real && __all((loA <= kc && kc + kChunk <= hiA) &&
-                                             (loB <= kc && kc + kChunk <= hiB));
-        if (full)
-            ticks(std::true_type{});
-        else
-            ticks(std::false_type{});
+            const unsigned rd = 8u * ((i + 1) & 1);
+            const int k = kc + i;
+            const bool actA = (unsigned)(k - A.G) < (unsigned)T;
+            const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
+            const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
+            const double oA = A.psum ? IA : rA;
+            const bool actB = (unsigned)(k - B.G) < (unsigned)T;
+            const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
+            const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
+            const double oB = B.psum ? IB : rB;
+            *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
+            *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+            A.op = actA ? oA : A.op;
+            A.ip = actA ? IA : A.ip;
+            B.op = actB ? oB : B.op;
+            B.ip = actB ? IB : B.ip;
+            const bool inwin = k >= gminw && k < wend;
+            double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
+            if (!MCR_EXP_NO_STORES) {
+                orow[tid] = A.routed ? oA : 0.0;
+                orow[SLOTS + tid] = B.routed ? oB : 0.0;
+            }
+            if (A.xsrc && actA) {
+                const uint64_t bits = (uint64_t)__double_as_longlong(oA);
+                const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16), 0, 16);
+            }
+            if (B.xsrc && actB) {
+                const uint64_t bits = (uint64_t)__double_as_longlong(oB);
+                const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
+            }
+            __syncthreads();
+        }
         rbA = rbAn;
         nrA = nrAn;
         rbB = rbBn;

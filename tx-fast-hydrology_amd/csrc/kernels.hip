@@ -18,8 +18,6 @@
 #include "plan.hpp"
 #include "device_common.hpp"
 
-#include <type_traits>
-
 #pragma clang fp contract(off)
 
 // Diagnostic builds only (scripts/exp_variants.sh): each MCR_EXP_* switch removes one part of the
@@ -44,12 +42,13 @@ using dev::lds_f64;
 using dev::Slot;
 using dev::load_slot;
 using dev::decode_codes;
+using dev::fold;
 
 // LDS layout of one workgroup (bytes), RS = 2 * SLOTS node slots (lane l: slots l and
 // SLOTS + l):
 //   XB  [RS + 1][2] f64   output of each node slot at tick parity 0/1; slot RS stays 0.0
 //   FR  [RS][3]     f64   each slot's forcing rows rb .. rb + 2 of the current chunk
-//   TAB [table_cap] StepEntry step-table window
+//   TAB [table_cap] int4  step-table window {row_lo, row_hi, frac}
 //   XE  [ext_cap][tile] f64 external inputs of this launch
 // Each tick a lane routes its low slot, then its high slot; a fused pair's high node takes the
 // low output of the same tick from a register (SELF code), so a fused edge costs no tick.
@@ -65,9 +64,9 @@ void wavefront_det(WaveArgs a) {
     constexpr unsigned XB = 0;
     constexpr unsigned FR = XB + (RS + 1) * 16;
     constexpr unsigned TAB = FR + RS * 24;
-    const unsigned XE = TAB + (unsigned)a.table_cap * (unsigned)sizeof(StepEntry);
+    const unsigned XE = TAB + (unsigned)a.table_cap * 16;
     double* xbp = reinterpret_cast<double*>(lds + XB);
-    StepEntry* tab = reinterpret_cast<StepEntry*>(lds + TAB);
+    int4* tab = reinterpret_cast<int4*>(lds + TAB);
     double* xe = reinterpret_cast<double*>(lds + XE);
 
     const int tid = threadIdx.x;
@@ -134,8 +133,8 @@ void wavefront_det(WaveArgs a) {
 
     decode_codes<RS>(A, up4A, XB, XE, (unsigned)tile * 8);
     decode_codes<RS>(B, up4B, XB, XE, (unsigned)tile * 8);
+    const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);   // wave-uniform
     const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
-    const bool wide = __any(A.cnt > 2 || B.cnt > 2);   // wave-uniform
 
     // forcing rows of the first chunk
     int rbA, nrA, rbB, nrB;
@@ -154,12 +153,6 @@ void wavefront_det(WaveArgs a) {
     const int wend = gmaxw + T;                         // end of this workgroup's window
     double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
     double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
-    // a chunk where every real slot of the wave is active at all its ticks takes the FULL path
-    // (no per-tick activity selects); padding slots never matter, a real slot without work in
-    // this chunk keeps its state, so it forces the EDGE path
-    const int loA = A.real ? A.G : INT32_MIN / 2, hiA = A.real ? A.G + T : INT32_MAX / 2;
-    const int loB = B.real ? B.G : INT32_MIN / 2, hiB = B.real ? B.G + T : INT32_MAX / 2;
-    const bool any_real = __any(A.real || B.real);
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         // this chunk's forcing rows -> the slots' LDS rows (private: no barrier needed)
@@ -190,105 +183,74 @@ void wavefront_det(WaveArgs a) {
             mA[u] = A.uinc[u] ? A.ubase[u] + 8u * c - 8u : A.ubase[u];
             mB[u] = B.uinc[u] ? B.ubase[u] + 8u * c - 8u : B.ubase[u];
         }
-        const unsigned tpA = TAB + (unsigned)(kc - A.G - tw0) * sizeof(StepEntry);
-        const unsigned tpB = TAB + (unsigned)(kc - B.G - tw0) * sizeof(StepEntry);
+        const unsigned tpA = TAB + (unsigned)(kc - A.G - tw0) * 16u;
+        const unsigned tpB = TAB + (unsigned)(kc - B.G - tw0) * 16u;
         // lateral inflow of the chunk's ticks, interpolate_sample (nutils.py:23-33); it does
         // not depend on the routing state, so it is formed off the tick's critical path
         double qA[kChunk], qB[kChunk];
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
-            const StepEntry ea = *reinterpret_cast<const StepEntry*>(lds + tpA + 32u * j);
-            const StepEntry eb = *reinterpret_cast<const StepEntry*>(lds + tpB + 32u * j);
+            const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
+            const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
             double aLo, aHi, bLo, bHi;
             if (DENSE && slow) {
-                aLo = Fm[(int64_t)clamp_row(ea.lo < 0 ? 0 : ea.lo, nrow) * ns + A.d];
-                aHi = Fm[(int64_t)clamp_row(ea.hi < 0 ? 0 : ea.hi, nrow) * ns + A.d];
-                bLo = Fm[(int64_t)clamp_row(eb.lo < 0 ? 0 : eb.lo, nrow) * ns + B.d];
-                bHi = Fm[(int64_t)clamp_row(eb.hi < 0 ? 0 : eb.hi, nrow) * ns + B.d];
+                aLo = Fm[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
+                aHi = Fm[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
+                bLo = Fm[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
+                bHi = Fm[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
             } else {
-                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.lo);
-                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.hi);
-                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.lo);
-                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.hi);
+                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
+                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
+                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
+                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
             }
-            const double qa = ea.w0 * aLo + ea.w1 * aHi;
-            const double qb = eb.w0 * bLo + eb.w1 * bHi;
-            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.hi < 0 ? aLo : qa);
-            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.hi < 0 ? bLo : qb);
+            const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
+            const double qa = (1.0 - fa) * aLo + fa * aHi;
+            const double qb = (1.0 - fb) * bLo + fb * bHi;
+            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
+            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
         }
         if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
-        // ticks of the chunk; FULL: every real slot of the wave is active at all of them
-        auto ticks = [&](auto full_tag) {
-            constexpr bool FULL = decltype(full_tag)::value;
 #pragma unroll
-            for (int i = 0; i < kChunk; ++i) {
-                if (i & 1) {
+        for (int i = 0; i < kChunk; ++i) {
+            if (i & 1) {
 #pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) {
-                        mA[u] += A.uinc[u];
-                        mB[u] += B.uinc[u];
-                    }
+                for (int u = 0; u < kUpInline; ++u) {
+                    mA[u] += A.uinc[u];
+                    mB[u] += B.uinc[u];
                 }
-                const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
-                const int k = kc + i;
-                // low slot, then the high slot (may read oA of this tick)
-                // positions 1 and 2 hold only zero-slot codes in waves where no slot has more
-                // than 2 inputs (wave-uniform skip: this kernel is throughput-bound)
-                const double a0 = lds_f64(lds, mA[0] + rd), a3 = lds_f64(lds, mA[3] + rd);
-                const double b0 = lds_f64(lds, mB[0] + rd), b3 = lds_f64(lds, mB[3] + rd);
-                double PA = a0, PB = b0;
-                if (wide) {
-                    PA = (PA + lds_f64(lds, mA[1] + rd)) + lds_f64(lds, mA[2] + rd);
-                    PB = (PB + lds_f64(lds, mB[1] + rd)) + lds_f64(lds, mB[2] + rd);
-                }
-                const double IA = PA + a3;
-                const double rA =
-                    0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
-                const double oA = A.psum ? IA : rA;
-                const double IB = PB + (B.self_last ? oA : b3);
-                const double rB =
-                    0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
-                const double oB = B.psum ? IB : rB;
-                // inactive ticks write garbage that no active node reads (its consumer is
-                // inactive one tick later); never-processed reaches (no consumer) output 0
-                *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
-                bool actA = true, actB = true;
-                double* orow;
-                if (FULL) {
-                    A.op = oA;
-                    A.ip = IA;
-                    B.op = oB;
-                    B.ip = IB;
-                    orow = Om + wb + (int64_t)(k - gminw) * RS;
-                } else {
-                    actA = (unsigned)(k - A.G) < (unsigned)T;
-                    actB = (unsigned)(k - B.G) < (unsigned)T;
-                    A.op = actA ? oA : A.op;
-                    A.ip = actA ? IA : A.ip;
-                    B.op = actB ? oB : B.op;
-                    B.ip = actB ? IB : B.ip;
-                    // ticks outside the workgroup window go to the dummy row
-                    const bool inwin = k >= gminw && k < wend;
-                    orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
-                }
-                // one row of RS values per tick, lane-interleaved {low, high}: one 16-byte
-                // store per lane
-                if (!MCR_EXP_NO_STORES) {
-                    reinterpret_cast<double2*>(orow)[tid] =
-                        make_double2(A.routed ? oA : 0.0, B.routed ? oB : 0.0);
-                    if (A.xsrc && actA) XSm[A.xs0 + k] = oA;
-                    if (B.xsrc && actB) XSm[B.xs0 + k] = oB;
-                }
-                if (!MCR_EXP_NO_BARRIER) __syncthreads();
             }
-        };
-        const bool full = any_real && __all((loA <= kc && kc + kChunk <= hiA) &&
-                                             (loB <= kc && kc + kChunk <= hiB));
-        if (full)
-            ticks(std::true_type{});
-        else
-            ticks(std::false_type{});
+            const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
+            const int k = kc + i;
+            // low slot
+            const bool actA = (unsigned)(k - A.G) < (unsigned)T;
+            const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
+            const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
+            const double oA = A.psum ? IA : rA;
+            // high slot (may read oA of this tick)
+            const bool actB = (unsigned)(k - B.G) < (unsigned)T;
+            const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
+            const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
+            const double oB = B.psum ? IB : rB;
+            // inactive ticks write garbage that no active node reads (its consumer is inactive
+            // one tick later); never-processed reaches (no consumer) output 0
+            *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
+            *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+            A.op = actA ? oA : A.op;
+            A.ip = actA ? IA : A.ip;
+            B.op = actB ? oB : B.op;
+            B.ip = actB ? IB : B.ip;
+            // one contiguous row of RS values per tick; ticks outside the window: dummy row
+            const bool inwin = k >= gminw && k < wend;
+            double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
+            if (!MCR_EXP_NO_STORES) {
+                orow[tid] = A.routed ? oA : 0.0;
+                orow[SLOTS + tid] = B.routed ? oB : 0.0;
+                if (A.xsrc && actA) XSm[A.xs0 + k] = oA;
+                if (B.xsrc && actB) XSm[B.xs0 + k] = oB;
+            }
+            if (!MCR_EXP_NO_BARRIER) __syncthreads();
+        }
         rbA = rbAn;
         nrA = nrAn;
         rbB = rbBn;
@@ -359,20 +321,15 @@ __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restri
     }
 }
 
-// jbase[j]: where reach j's step 0 lives in its workgroup window.  A window row holds the
-// workgroup's 2 * lanes node slots lane-interleaved: slot (lane, high) at column 2 lane + high.
 __global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __restrict__ G,
                              const int32_t* __restrict__ wg_gmin,
-                             const int64_t* __restrict__ wbase, int lanes, int64_t n,
+                             const int64_t* __restrict__ wbase, int slots, int64_t n,
                              int64_t* __restrict__ jbase) {
-    const int64_t rs = 2 * (int64_t)lanes;
     for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
          j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t d = pos[j];
-        const int64_t w = d / rs;
-        const int64_t dl = d - w * rs;
-        const int64_t col = (dl % lanes) * 2 + dl / lanes;
-        jbase[j] = wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * rs + col;
+        const int64_t w = d / slots;
+        jbase[j] = wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * slots + (d - w * slots);
     }
 }
 
@@ -479,11 +436,11 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
 }
 
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
-                               const int64_t* wbase, int lanes, int64_t n, int64_t* jbase,
+                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
                                hipStream_t s) {
     if (n > 0)
         hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
-                           lanes, n, jbase);
+                           slots, n, jbase);
     return hipGetLastError();
 }
 

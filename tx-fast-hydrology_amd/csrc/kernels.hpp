@@ -2,16 +2,15 @@
 // functions so the C-ABI layer (capi.cpp) stays free of kernel syntax.
 //
 // Output layout ("workgroup windows").  Workgroup w owns the ticks [gmin[w], gmax[w] + T) of the
-// space-time schedule; its outputs are stored tick-major inside that window, one row of its
-// RS = 2 * SLOTS node slots per tick, lane-interleaved:
-//     O[wbase[w] + (tick - gmin[w]) * RS + 2 * lane + high]
-// so each lane writes its {low, high} pair with one 16-byte store and a wave writes one
-// contiguous 1 KiB run per tick.  Inflows are not stored: i[j][t] = ((0 + o[u1][t]) + o[u2][t])
-// + ... over j's inflow list (plan.hpp) is recomputed bit-exactly wherever it is needed
-// (fetches).  A node that feeds a node of another cluster (an "external input" of the
-// consumer's workgroup) also writes its output to a step-contiguous stream XS[e][t], which the
-// consumer reads coalesced.  Step t of caller reach j lives at  jbase[j] + t * RS  (jbase is
-// computed per horizon by launch_window_index).
+// space-time schedule; its outputs are stored tick-major inside that window:
+//     O[wbase[w] + (tick - gmin[w]) * SLOTS + lane]
+// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  Inflows are not stored:
+// i[j][t] = ((0 + o[u1][t]) + o[u2][t]) + ... over j's inflow list (plan.hpp) is recomputed
+// bit-exactly wherever it is needed (fetches, final state).  A reach that feeds a
+// reach of another cluster (an "external input" of the consumer's workgroup) also writes its
+// outflow to a step-contiguous stream XS[e][t], which the consumer reads coalesced.  Step t of the reach in
+// slot d = w * SLOTS + lane lives at tick G[d] + t, i.e. at  jbase[j] + t * SLOTS  for its caller
+// index j (jbase is computed per horizon by launch_window_index).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,14 +21,6 @@ namespace mcr {
 
 // Workgroup sizes (plan slots) the kernels are instantiated for.
 #define MCR_SLOT_LIST(X) X(64) X(128) X(192) X(256) X(384) X(448) X(512)
-
-// Forcing lookup of one model step (interpolate_sample, nutils.py:21-33): q = w0 * f[lo] +
-// w1 * f[hi] with w0 = 1 - frac, w1 = frac formed on the host exactly as numpy does; hi = -1
-// (x outside the forcing index): q = f[lo].
-struct alignas(16) StepEntry {
-    int32_t lo, hi, pad0, pad1;
-    double w0, w1;
-};
 
 // Ticks whose lateral inflow is formed in one burst (and whose forcing rows are prefetched
 // together).  Launch lengths (`tile`) are multiples of it.
@@ -70,7 +61,7 @@ struct WaveArgs {
     double* st_o;
     double* st_i;
     const double* F;              // forcing rows in slot order [n_rows][nslots]
-    const StepEntry* stab;        // per step forcing rows and interpolation weights
+    const int4* stab;             // per step {row_lo, row_hi (-1 = copy row_lo), frac (f64)}
     const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
     const int32_t* wg_gmax;
     const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
@@ -98,14 +89,13 @@ struct WaveArgs {
 // LDS bytes for `slots` lanes (2 * slots node slots)
 inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile) {
     const size_t rs = 2 * (size_t)slots;
-    return 16 * (rs + 1) + 24 * rs + sizeof(StepEntry) * (size_t)table_cap +
-           8 * (size_t)ext_cap * tile;
+    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
 }
 
 inline size_t flow_lds_bytes(int slots, int T, int ext_cap) {
     const size_t rs = 2 * (size_t)slots;
-    return 16 * (rs + 1) + 24 * rs + sizeof(StepEntry) * (size_t)T +
-           2 * (size_t)ext_cap * kChunk * 8 + 4 * kFlowMaxExt;
+    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)T + 2 * (size_t)ext_cap * kChunk * 8 +
+           4 * kFlowMaxExt;
 }
 
 // One launch for the whole horizon; grid = every workgroup (all must be co-resident).
@@ -131,9 +121,9 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
                                    hipStream_t s);
-// jbase[j] = window index of step 0 of caller reach j (`lanes` = plan slots)
+// jbase[j] = window index of step 0 of caller reach j
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
-                               const int64_t* wbase, int lanes, int64_t n, int64_t* jbase,
+                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
                                hipStream_t s);
 // Output gathers (caller order, member innermost).  inflow = false: outflow O; true: the inflow
 // of reach j, summed from O over its inflow list.

@@ -10,7 +10,6 @@ namespace mcr {
 
 namespace {
 
-
 struct Cluster {
     int64_t root = -1;
     int64_t size = 0;
@@ -218,7 +217,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // node takes low's output from a register, so the fused edge costs no tick.  Fusing
     // alternate edges of a chain halves its depth.  DP over the forest in topological order:
     // Sx = height of x when it is not the high node of a pair, Fx = height when it is (fused
-    // with its last input fch).  A node is low for at most one pair (it has one consumer).
+    // with its best input fch).  A node is low for at most one pair (it has one consumer).
     std::vector<int32_t> Sx(N, 0), Fx(N, INT32_MAX), bx(N, 0);
     std::vector<int64_t> fch(N, -1);
     for (int64_t x : nodes) {
@@ -226,9 +225,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int32_t sx = 0;
         for (int64_t k = k0; k < k1; ++k) sx = std::max(sx, bx[gin_list[k]] + 1);
         Sx[x] = sx;
-        // only x's last input (in fold order) may be its low mate: the high node then adds the
-        // register value last, one add after low's output (kernels.hip, fold)
-        for (int64_t k = std::max(k0, k1 - 1); k < k1; ++k) {
+        for (int64_t k = k0; k < k1; ++k) {
             int32_t m = Sx[gin_list[k]];
             for (int64_t q = k0; q < k1; ++q)
                 if (q != k) m = std::max(m, bx[gin_list[q]] + 1);
@@ -356,7 +353,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // ---- 6. schedule: local ALAP skew + cluster offsets -----------------------------------
     // distance to the cluster root: walk lane nodes in reverse (downstream first)
     std::vector<int32_t> dist(N, 0);
-    for (Cluster& c : clusters) c.dmax = 0;
+    for (Cluster& c : clusters) c.dmax = 0;      // recomputed exactly from the final clusters
     for (auto it = lnodes.rbegin(); it != lnodes.rend(); ++it) {
         const int64_t j = *it;
         const int64_t e = lcons(j);
@@ -489,26 +486,19 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src node, consumer G)
     std::vector<int64_t> node_at(P.nslots, -1);
     for (int64_t x = 0; x < N; ++x) node_at[npos[x]] = x;
-    // code positions: the first cnt - 1 inputs in positions 0.., the LAST input (in fold order)
-    // in position kUpInline - 1, the zero slot (RS) elsewhere.  The kernel folds
-    // ((v0 + v1) + v2) + v3; adding the zero slot's +0.0 to a value that is never -0.0 is
-    // exact, so this is the reference's left fold for every cnt.
     for (int64_t d = 0; d < P.nslots; ++d) {
         const int64_t j = node_at[d];
-        uint64_t packed = 0;
-        for (int u = 0; u < kUpInline; ++u) packed |= (uint64_t)RS << (16 * u);
-        P.up4[d] = packed;
         if (j < 0) continue;
         const int32_t w = (int32_t)(d / RS);
         const int64_t k0 = gin_off[j], k1 = gin_off[j + 1];
         if (k1 - k0 > kUpInline) return "internal: more than kUpInline inputs";
         P.up_cnt[d] = (uint8_t)(k1 - k0);
+        uint64_t packed = 0;
         for (int64_t k = k0; k < k1; ++k) {
             const int64_t u = gin_list[k];
             uint16_t code;
             if (role[j] == 2 && u == mate[j]) {
-                if (npos[u] != d - C || G[u] != G[j] || k != k1 - 1)
-                    return "internal: fused pair layout";
+                if (npos[u] != d - C || G[u] != G[j]) return "internal: fused pair layout";
                 code = kSelfCode;
             } else if (cl[u] == cl[j]) {
                 if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";
@@ -521,9 +511,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
                 code = (uint16_t)(kExtBit | e);
                 P.n_cross++;
             }
-            const int pos = k == k1 - 1 ? kUpInline - 1 : (int)(k - k0);
-            packed &= ~((uint64_t)0xffff << (16 * pos));
-            packed |= (uint64_t)code << (16 * pos);
+            packed |= (uint64_t)code << (16 * (k - k0));
         }
         P.up4[d] = packed;
     }

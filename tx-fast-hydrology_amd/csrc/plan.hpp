@@ -41,8 +41,7 @@ constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 
 // upstream code: bit 15 set -> index into the workgroup's external-input list, else the
 // workgroup-local slot of the upstream reach.
 constexpr uint16_t kExtBit = 0x8000;
-// code of a fused pair's low node in its high node's list (always the last position): low's
-// output of the same tick
+// code of a fused pair's low node in its high node's list: low's output of the same tick
 constexpr uint16_t kSelfCode = 0x7fff;
 constexpr int kUpInline = 4;  // upstream values one lane reads per tick (codes in registers)
 
@@ -80,7 +79,7 @@ struct Plan {
     std::vector<int32_t> G;            // tick of model step 0
     std::vector<uint8_t> flags;
     std::vector<uint8_t> up_cnt;
-    std::vector<uint64_t> up4;         // kUpInline input codes, 16 bits each, positional (plan.cpp)
+    std::vector<uint64_t> up4;         // first kUpInline codes, 16 bits each
     std::vector<int32_t> xid;          // external input this slot feeds (index into ext_*), -1
 
     // per workgroup
