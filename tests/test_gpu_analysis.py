@@ -169,3 +169,35 @@ def test_staged_driver_single_rank_equals_enkf_analysis():
     oa, ia = a.get_state()
     ob, ib = b.get_state()
     assert np.array_equal(oa, ob) and np.array_equal(ia, ib)
+
+
+@pytest.mark.parametrize("E,m", [(16, 40), (48, 12)])
+def test_ensemble_space_solve_equals_observation_space(E, m):
+    """Diagonal R with E <= m takes the E x E ensemble-space solve (push-through identity); a
+    numerically identical R with a 1e-300 off-diagonal entry forces the m x m observation-space
+    Cholesky.  Both must give the same analysis (and the numpy restatement)."""
+    end = synthetic.river_network(3000, 4, 120, np.random.default_rng(31))
+    n = end.size
+    rng = np.random.default_rng(E + m)
+    X = rng.uniform(0.5, 5, n)[:, None] * rng.lognormal(0, 0.3, (n, E))
+    I0 = rng.uniform(0, 5, (n, E))
+    s = np.sort(rng.choice(n, m, replace=False))
+    R = np.diag(rng.uniform(5e-3, 5e-2, m))
+    Y = X[s].mean(1, keepdims=True) + 0.2 + rng.normal(0, 0.1, (m, E))
+    Rd = R.copy()
+    Rd[0, 1] = Rd[1, 0] = 1e-300
+    out = []
+    for RR in (R, Rd):
+        net, _, _ = _net(end, members=E)
+        net.set_state(X, I0)
+        net.enkf_analysis(s, Y, RR)
+        out.append(net.get_state())
+    G = _numpy_enkf(X, s, Y, R)
+    scale = np.abs(G).max()
+    for k in range(2):
+        np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10 * scale * 10)
+    start = np.arange(n)
+    indeg = orc.compute_indegree(start, end)
+    for e in range(0, E, 7):
+        _, og = orc.apply_gain(start[indeg == 0], end, G[:, e], indeg)
+        np.testing.assert_allclose(out[0][0][:, e] - X[:, e], og, rtol=0, atol=1e-10 * scale)

@@ -97,6 +97,23 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
             }
 }
 
+// U[g + e m] = HA[g + e m] / r[g]  (R^-1 HA for a diagonal R)
+__global__ void scale_rows(const double* __restrict__ HA, const double* __restrict__ r,
+                           double* __restrict__ U, int64_t m, int64_t E) {
+    const int64_t total = m * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x)
+        U[x] = HA[x] / r[x % m];
+}
+
+// M = I (k x k, column-major)
+__global__ void set_identity(double* __restrict__ M, int64_t k) {
+    const int64_t total = k * k;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x)
+        M[x] = (x % k) == (x / k) ? 1.0 : 0.0;
+}
+
 // xbar[d] = (sum_e X[e][d]) / E ;  A[e][d] = X[e][d] - xbar[d]
 __global__ void mean_anomalies(const double* __restrict__ X, double* __restrict__ A,
                                int64_t ns, int64_t E) {
@@ -235,6 +252,18 @@ hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, doubl
     else
         hipLaunchKernelGGL((dgemm_mfma<true, true>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
                            ldb, beta, C, ldc);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64_t m, int64_t E,
+                             hipStream_t s) {
+    if (m * E > 0)
+        hipLaunchKernelGGL(scale_rows, grid_for(m * E, 256), 256, 0, s, HA, r, U, m, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s) {
+    if (k > 0) hipLaunchKernelGGL(set_identity, grid_for(k * k, 256), 256, 0, s, M, k);
     return hipGetLastError();
 }
 

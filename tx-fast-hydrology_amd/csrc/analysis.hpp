@@ -13,6 +13,11 @@ hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, doubl
                         const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                         double* C, int64_t ldc, hipStream_t s);
 // ensemble mean over members and anomalies A = X - mean (both [E][ns])
+// U = R^-1 HA for a diagonal R (r = its diagonal), column-major m x E
+hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64_t m, int64_t E,
+                             hipStream_t s);
+// M = I (k x k)
+hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s);
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s);
 // HA (m x E) = A at the gauge slots; D (m x E) = Y[g][e] - X at the gauge slots (D may be NULL)

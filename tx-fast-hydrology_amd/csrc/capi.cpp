@@ -192,7 +192,7 @@ struct Net {
     int64_t E = 1;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
-    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, XsB, GsB;
+    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, XsB, GsB, Rd, Ub, Mb;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
     rocblas_handle blas = nullptr;
@@ -378,6 +378,19 @@ struct Net {
         sync();
     }
 
+    // R diagonal with a positive diagonal?  (its diagonal into rd)
+    static bool diagonal_R(const double* R, int64_t m, std::vector<double>& rd) {
+        rd.resize(m);
+        for (int64_t i = 0; i < m; ++i) {
+            const double* row = R + i * m;
+            for (int64_t j = 0; j < m; ++j)
+                if (j != i && row[j] != 0.0) return false;
+            if (!(row[i] > 0.0)) return false;
+            rd[i] = row[i];
+        }
+        return true;
+    }
+
     rocblas_handle solver() {
         if (!blas && rocblas_create_handle(&blas) != rocblas_status_success)
             throw Fail(MC_E_HIP, "rocblas_create_handle failed");
@@ -458,33 +471,63 @@ struct Net {
         const int64_t Et = E * N, S = slice_size(N);
         REQUIRE(Et >= 2, "the ensemble analysis needs at least 2 members");
         const double inv = 1.0 / (double)(Et - 1);
-        // gauge anomalies HA = HX - mean over members;  C = HA HA^T / (Et-1) + R
+        // gauge anomalies HA = HX - mean over members
         HA.reserve((size_t)(m * Et));
         HIPC(mcr::launch_mean_anomalies(HXall, HA.p, m, Et, stream));
-        upload_async(C2, R, (size_t)(m * m));          // symmetric: row-major == column-major
-        HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
-                               stream));
-        info.reserve(1);
-        if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p, (rocblas_int)m,
-                             info.p) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
-        // status checked at the next sync (a failed factorisation leaves the update unusable)
         if (!info_host)
             HIPC(hipHostMalloc(reinterpret_cast<void**>(&info_host), sizeof(int32_t),
                                hipHostMallocDefault));
-        HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
-        info_pending = true;
-        // W = C^-1 D  (every member),  Z = HA^T W / (Et-1)  (Et x Et)
-        Dn.reserve((size_t)(m * Et));
-        HIPC(hipMemcpyAsync(Dn.p, Dall, (size_t)(m * Et) * sizeof(double),
-                            hipMemcpyDeviceToDevice, stream));
-        if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)m, (rocblas_int)Et,
-                             C2.p, (rocblas_int)m, Dn.p, (rocblas_int)m) !=
-            rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+        info.reserve(1);
         Zn.reserve((size_t)(Et * Et));
-        HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, Et,
-                               stream));
+        std::vector<double> rd;
+        if (Et <= m && diagonal_R(R, m, rd)) {
+            // ensemble space (diagonal R): with S = HA / sqrt(Et-1),
+            //   S^T (S S^T + R)^-1 D = (I + S^T R^-1 S)^-1 S^T R^-1 D   (push-through identity)
+            // so Z = HA^T C^-1 D / (Et-1) = M^-1 V with M = I + HA^T R^-1 HA / (Et-1) (Et x Et,
+            // SPD, eigenvalues >= 1) and V = (R^-1 HA)^T D / (Et-1): an Et x Et solve instead
+            // of m x m
+            upload_async(Rd, rd.data(), rd.size());
+            Ub.reserve((size_t)(m * Et));
+            HIPC(mcr::launch_scale_rows(HA.p, Rd.p, Ub.p, m, Et, stream));
+            Mb.reserve((size_t)(Et * Et));
+            HIPC(mcr::launch_set_identity(Mb.p, Et, stream));
+            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Ub.p, m, 1.0, Mb.p, Et,
+                                   stream));
+            if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)Et, Mb.p,
+                                 (rocblas_int)Et, info.p) != rocblas_status_success)
+                throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
+            HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                stream));
+            info_pending = true;
+            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p, Et,
+                                   stream));
+            if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)Et, (rocblas_int)Et,
+                                 Mb.p, (rocblas_int)Et, Zn.p, (rocblas_int)Et) !=
+                rocblas_status_success)
+                throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+        } else {
+            // observation space: C = HA HA^T / (Et-1) + R (m x m), W = C^-1 D,
+            // Z = HA^T W / (Et-1)
+            upload_async(C2, R, (size_t)(m * m));      // symmetric: row-major == column-major
+            HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
+                                   stream));
+            if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p,
+                                 (rocblas_int)m, info.p) != rocblas_status_success)
+                throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
+            // status checked at the next sync (a failed factorisation leaves the update unusable)
+            HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                stream));
+            info_pending = true;
+            Dn.reserve((size_t)(m * Et));
+            HIPC(hipMemcpyAsync(Dn.p, Dall, (size_t)(m * Et) * sizeof(double),
+                                hipMemcpyDeviceToDevice, stream));
+            if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)m, (rocblas_int)Et,
+                                 C2.p, (rocblas_int)m, Dn.p, (rocblas_int)m) !=
+                rocblas_status_success)
+                throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, Et,
+                                   stream));
+        }
         // slice anomalies and increments G = A Z  (= K D per member)
         An.reserve((size_t)(S * Et));
         HIPC(mcr::launch_mean_anomalies(Xs, An.p, S, Et, stream));
