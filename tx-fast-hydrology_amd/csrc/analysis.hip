@@ -192,21 +192,20 @@ __global__ void unpack_slices(const double* __restrict__ in, double* __restrict_
 //   i_gain[j] = ((0 + o_gain[u1]) + o_gain[u2]) + ...  over j's routed upstreams in rank order;
 //   o += o_gain,  i += i_gain   (da.py:124-126)
 __global__ void apply_gain(const double* __restrict__ G, double* __restrict__ st_o,
-                           double* __restrict__ st_i, const int64_t* __restrict__ slot_reach,
-                           const int64_t* __restrict__ pos, const uint8_t* __restrict__ flags,
-                           const int64_t* __restrict__ in_off,
-                           const int64_t* __restrict__ in_list, int64_t ns, int64_t E) {
+                           double* __restrict__ st_i, const uint8_t* __restrict__ flags,
+                           const int32_t* __restrict__ up_off, const int32_t* __restrict__ up,
+                           int64_t ns, int64_t E) {
     const int64_t total = ns * E;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e = x / ns;
         const int64_t d = x - e * ns;
-        const int64_t j = slot_reach[d];
-        if (j < 0) continue;
+        const uint8_t f = flags[d];
+        if (f != kSlotRouted && f != kSlotUnrouted) continue;   // padding / partial sums
         const double* Ge = G + e * ns;
-        const double og = flags[d] == kSlotRouted ? 0.0 + Ge[d] : 0.0;
+        const double og = f == kSlotRouted ? 0.0 + Ge[d] : 0.0;
         double ig = 0.0;
-        for (int64_t k = in_off[j]; k < in_off[j + 1]; ++k) ig = ig + (0.0 + Ge[pos[in_list[k]]]);
+        for (int32_t k = up_off[d]; k < up_off[d + 1]; ++k) ig = ig + (0.0 + Ge[up[k]]);
         st_o[x] = st_o[x] + og;
         st_i[x] = st_i[x] + ig;
     }
@@ -303,12 +302,11 @@ hipError_t launch_unpack_slices(const double* in, double* G, int64_t ns, int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i,
-                             const int64_t* slot_reach, const int64_t* pos,
-                             const uint8_t* flags, const int64_t* in_off,
-                             const int64_t* in_list, int64_t ns, int64_t E, hipStream_t s) {
-    hipLaunchKernelGGL(apply_gain, grid_for(ns * E, 256), 256, 0, s, G, st_o, st_i, slot_reach,
-                       pos, flags, in_off, in_list, ns, E);
+hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i, const uint8_t* flags,
+                             const int32_t* up_off, const int32_t* up, int64_t ns, int64_t E,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(apply_gain, grid_for(ns * E, 256), 256, 0, s, G, st_o, st_i, flags,
+                       up_off, up, ns, E);
     return hipGetLastError();
 }
 

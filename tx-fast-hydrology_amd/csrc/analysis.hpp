@@ -33,11 +33,11 @@ hipError_t launch_pack_slices(const double* X, double* out, int64_t ns, int64_t 
                               int64_t N, hipStream_t s);
 hipError_t launch_unpack_slices(const double* in, double* G, int64_t ns, int64_t E, int64_t S,
                                 int64_t N, hipStream_t s);
-// _apply_gain per member: o += 0 + G (routed reaches), i += rank-ordered one-hop sums
-hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i,
-                             const int64_t* slot_reach, const int64_t* pos,
-                             const uint8_t* flags, const int64_t* in_off,
-                             const int64_t* in_list, int64_t ns, int64_t E, hipStream_t s);
+// _apply_gain per member: o += 0 + G (routed reaches), i += rank-ordered one-hop sums;
+// up_off / up: each slot's routed upstream slots in rank order (int32 CSR over slots)
+hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i, const uint8_t* flags,
+                             const int32_t* up_off, const int32_t* up, int64_t ns, int64_t E,
+                             hipStream_t s);
 // Kt (m x nslots, column-major) -> K_out[j][g] in caller reach order
 hipError_t launch_gain_to_caller(const double* Kt, double* out, const int64_t* pos, int64_t m,
                                  int64_t n, hipStream_t s);

@@ -147,7 +147,7 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, ext_off, ext_g, wg_gmin, wg_gmax, xid;
+    DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, xid;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
     DBuf<int64_t> slot_reach, pos;
@@ -192,7 +192,7 @@ struct Net {
     int64_t E = 1;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
-    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, XsB, GsB, Rd, Ub, Mb;
+    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, Rd, Ub, Mb;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
     rocblas_handle blas = nullptr;
@@ -261,6 +261,21 @@ struct Net {
         in_off.upload(plan.in_off.data(), plan.in_off.size(), stream);
         in_list.upload(plan.in_list.data(), plan.in_list.size(), stream);
         in_list.reserve(1);
+        {   // inflow lists in slot space (int32) for the gain scatter
+            REQUIRE(ns < ((size_t)1 << 31), "network too large (node slots must fit int32)");
+            std::vector<int32_t> so(ns + 1, 0), sl;
+            sl.reserve(plan.in_list.size());
+            for (size_t d = 0; d < ns; ++d) {
+                const int64_t j = plan.slot_reach[d];
+                if (j >= 0)
+                    for (int64_t k = plan.in_off[j]; k < plan.in_off[j + 1]; ++k)
+                        sl.push_back((int32_t)plan.pos[plan.in_list[k]]);
+                so[d + 1] = (int32_t)sl.size();
+            }
+            sup_off.upload(so.data(), so.size(), stream);
+            sup.upload(sl.data(), sl.size(), stream);
+            sup.reserve(1);
+        }
         wg_gmin.upload(plan.wg_gmin.data(), plan.wg_gmin.size(), stream);
         wg_gmax.upload(plan.wg_gmax.data(), plan.wg_gmax.size(), stream);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
@@ -373,8 +388,8 @@ struct Net {
         const size_t ns = (size_t)plan.nslots;
         Gn.reserve(ns * E);
         to_slots(gain, Gn, E);
-        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, slot_reach.p, pos.p, flags.p,
-                                    in_off.p, in_list.p, plan.nslots, E, stream));
+        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p,
+                                    plan.nslots, E, stream));
         sync();
     }
 
@@ -541,8 +556,8 @@ struct Net {
         const int64_t ns = plan.nslots;
         Gn.reserve((size_t)(ns * E));
         HIPC(mcr::launch_unpack_slices(Grecv, Gn.p, ns, E, slice_size(N), N, stream));
-        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, slot_reach.p, pos.p, flags.p,
-                                    in_off.p, in_list.p, ns, E, stream));
+        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, ns, E,
+                                    stream));
     }
 
     void enkf_analysis(int64_t m, const int64_t* gauges, const double* y, const double* R) {
@@ -552,12 +567,13 @@ struct Net {
         const int64_t ns = plan.nslots;
         HXb.reserve((size_t)(m * E));
         Db.reserve((size_t)(m * E));
-        XsB.reserve((size_t)(ns * E));
-        GsB.reserve((size_t)(ns * E));
+        Gn.reserve((size_t)(ns * E));
         ens_gauges(m, gauges, y, HXb.p, Db.p);
-        ens_pack(1, XsB.p);
-        ens_slice_update(1, m, XsB.p, HXb.p, Db.p, R, GsB.p);
-        ens_unpack_apply(1, GsB.p);
+        // one rank: the slice of every member IS the member-major state (slice_size(1) = ns),
+        // so the pack / unpack stages are identities
+        ens_slice_update(1, m, st_o.p, HXb.p, Db.p, R, Gn.p);
+        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, ns, E,
+                                    stream));
     }
 
     // K = (A HA^T / (E-1)) C2^-1  as [n][m] in caller order
