@@ -211,6 +211,38 @@ int mc_get_mode(void* net, int* mode, int* last_path);
 int mc_set_trace(void* net, int enable);
 int mc_get_trace(void* net, int64_t* out, int64_t cap, int64_t* n_records, int64_t* clock_khz);
 
+/* ---- Full-covariance Kalman filter (da.py KalmanFilter / KalmanSmoother) ----
+ * A covariance handle compiles the reach graph of one network once (walk replay of nutils._ax,
+ * nutils.py:91-114).  Matrices P, Q, out, P_prior, P_post are row-major n x n float64 DEVICE
+ * buffers owned by the caller (numpy layout, e.g. torch tensors); everything else is host
+ * memory.  Calls are stream-ordered on the handle's stream; host outputs are complete when the
+ * call returns.  Sweeps are bit-identical to the reference walk. */
+int mc_cov_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                  const int64_t* headwaters, int64_t n_head, void** cov);
+int mc_cov_destroy(void* cov);
+int mc_cov_set_stream(void* cov, void* hip_stream);
+/* alpha, beta, chi [n] (gamma does not enter the state transition). */
+int mc_cov_set_coeffs(void* cov, const double* alpha, const double* beta, const double* chi);
+/* out = A P: _ap_par (nutils.py:157-170); P and out must be distinct. */
+int mc_cov_ap(void* cov, const double* P, double* out);
+/* out = A (A P)^T (+ Q when Q != NULL): _aqat_par (nutils.py:194-214) then da.py:117. */
+int mc_cov_aqat(void* cov, const double* P, const double* Q, double* out);
+/* _apply_gain (nutils.py:116-134), stateless: host gain [n] -> host i_gain, o_gain [n]. */
+int mc_cov_apply_gain(void* cov, const double* gain, double* i_gain, double* o_gain);
+/* da.py:118-122 on the prior: K = P_prior[:, s] (P_prior[s, s] + R)^-1 (LU, as np.linalg.inv),
+ * gain = K dz, P_post = P_prior - K P_prior[s, :].  s [m] gauge reach indices (the sorted mask
+ * order of da.py:31-44), R [m][m], dz [m] host; K_out [n][m] host (may be NULL), gain_out [n]
+ * host.  P_post may equal P_prior (in-place posterior). */
+int mc_kf_update(void* cov, int64_t m, const int64_t* s, const double* R, const double* dz,
+                 const double* P_prior, double* P_post, double* K_out, double* gain_out);
+/* One backward step of the RTS smoother (da.py:241-251): J = solve(P_p1, A P_f)^T,
+ * P_s_out = P_f + J (P_s1 - P_p1), and for nvec host vectors x_s_out[v] = x_f[v] + J d[v]
+ * (d = x_s(t+1) - x_p(t+1); [nvec][n] each).  P_s_out may equal P_f. */
+int mc_ks_step(void* cov, const double* P_f, const double* P_p1, const double* P_s1,
+               double* P_s_out, int64_t nvec, const double* x_f, const double* d,
+               double* x_s_out);
+int mc_cov_synchronize(void* cov);
+
 #ifdef __cplusplus
 }
 #endif

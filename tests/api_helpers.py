@@ -1,0 +1,107 @@
+"""Helpers for the API-level tests: models and frames rebuilt from the golden fixtures (the same
+construction tests/golden/make_golden.py used on the reference), and an oracle-backed stand-in
+for the device session so the host logic of the Muskingum mirror runs in the CPU suite."""
+import numpy as np
+import pandas as pd
+
+from oracle import oracle as orc
+
+
+def model_dict(endnodes, K, X, o_t, start, dt_s, name="m"):
+    n = endnodes.size
+    return {
+        "name": name,
+        "datetime": start,
+        "timedelta": pd.to_timedelta(dt_s, unit="s"),
+        "reach_ids": [f"r{i}" for i in range(n)],
+        "startnodes": np.arange(n, dtype=np.int64),
+        "endnodes": np.asarray(endnodes, dtype=np.int64),
+        "K": np.asarray(K, dtype=np.float64),
+        "X": np.asarray(X, dtype=np.float64),
+        "o_t": np.asarray(o_t, dtype=np.float64),
+        "dx": np.ones(n, dtype=np.float64),
+        "paths": [[[[0.0, 0.0], [1.0, 1.0]]] for _ in range(n)],
+    }
+
+
+def golden_model(g, o_key="o0"):
+    from tx_fast_hydrology_amd.muskingum import Muskingum
+    start = pd.Timestamp(int(g["start_ns"]), tz="UTC")
+    return Muskingum(model_dict(g["endnodes"], g["K"], g["X"], g[o_key], start, float(g["dt"])))
+
+
+def golden_frame(g, reach_ids):
+    idx = pd.DatetimeIndex(pd.to_datetime(g["idx_ns"], utc=True))
+    return pd.DataFrame(g["forcing"], index=idx, columns=reach_ids)
+
+
+def run(model, df, **kw):
+    os_, is_, ts = [], [], []
+    for state in model.simulate(df, **kw):
+        os_.append(np.array(state.o_t_next))
+        is_.append(np.array(state.i_t_next))
+        ts.append(state.datetime.value)
+    return np.array(os_), np.array(is_), np.array(ts, dtype=np.int64)
+
+
+class OracleNet:
+    """CPU stand-in for engine.RoutingNet (test double: the oracle routes)."""
+
+    def __init__(self, endnodes, indegree, headwaters):
+        self.end = np.asarray(endnodes)
+        self.deg = np.asarray(indegree)
+        self.heads = np.asarray(headwaters)
+        self.n = self.end.size
+        self.runs = 0
+        self.steps = 0
+
+    def set_coeffs(self, a, b, c, g):
+        self.coef = [np.array(v, dtype=np.float64) for v in (a, b, c, g)]
+
+    def step(self, q, o_prev, i_prev):
+        self.steps += 1
+        i, o = orc.ax_bu(self.heads, self.end, *self.coef, i_prev, o_prev, q, self.deg)
+        self.o, self.i = o, i
+        return i, o
+
+    def load_forcing(self, xp, fp):
+        self.xp, self.fp = np.array(xp), np.array(fp)
+
+    def set_state(self, o, i):
+        self.o, self.i = np.array(o, dtype=np.float64), np.array(i, dtype=np.float64)
+
+    def run(self, x):
+        self.runs += 1
+        start = np.arange(self.n)
+        self.out_o, self.out_i, self.o, self.i = orc.simulate(
+            start, self.end, self.deg, *self.coef, self.o, self.i, x, self.xp, self.fp)
+
+    def fetch_outputs(self):
+        return self.out_o.copy(), self.out_i.copy()
+
+    def close(self):
+        pass
+
+
+def use_oracle_device(monkeypatch):
+    """Route Muskingum models through OracleNet; returns the list of nets created."""
+    from tx_fast_hydrology_amd import muskingum
+    created = []
+    orig = muskingum._DeviceRouting.session
+
+    def make(end, deg, heads):
+        net = OracleNet(end, deg, heads)
+        created.append(net)
+        return net
+
+    def session(self, model):
+        from tx_fast_hydrology_amd import engine
+        saved = engine.RoutingNet
+        engine.RoutingNet = make
+        try:
+            return orig(self, model)
+        finally:
+            engine.RoutingNet = saved
+
+    monkeypatch.setattr(muskingum._DeviceRouting, "session", session)
+    return created

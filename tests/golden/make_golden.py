@@ -15,7 +15,7 @@ identity decorator and whose ``prange`` is ``range``, and a sma
 Both live in a temporary directory that is deleted afterwards.  ``sys.dont_write_bytecode`` keeps
 the read-only reference tree untouched.
 
-Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [g11 ...]  (writes tests/golden/*.npz; names: only those)
 """
 from __future__ import annotations
 
@@ -450,9 +450,53 @@ def g10_model_io(mk, tio):
          indegree=m.indegree, init_i=m.i_t_next, **coeffs)
 
 
+def g11_smoother(mk, da):
+    """G11: KalmanSmoother (da.py:139-264) on 60 reaches, 4 gages, 8 hourly steps: filter
+    estimates, priors and the RTS-smoothed series."""
+    rng = np.random.default_rng(1111)
+    n = 60
+    endnodes = random_forest(n, 2, rng, window=3, p_window=0.7)
+    K = rng.uniform(1800.0, 7200.0, n)
+    X = rng.uniform(0.1, 0.4, n)
+    o0 = rng.uniform(0.5, 5.0, n)
+    start = pd.Timestamp("2024-05-01T00:00:00Z")
+    model = mk.Muskingum(make_model_dict(mk, endnodes, K, X, o0, start, 3600))
+    df = forcing_frame(model.reach_ids, "2024-05-01T00:00:00", 9, "1h", rng)
+    gages = np.sort(rng.choice(np.flatnonzero(model.indegree > 0), size=4, replace=False))
+    meas_idx = pd.date_range("2024-05-01T00:00:00", periods=9, freq="1h", tz="UTC")
+    meas = pd.DataFrame(rng.uniform(0.5, 8.0, size=(9, 4)), index=meas_idx,
+                        columns=[model.reach_ids[g] for g in gages])
+    Q = 2.0 * np.eye(n)
+    R = 1e-2 * np.eye(4)
+    ks = da.KalmanSmoother(model, meas, Q, R, Q.copy())
+    model.bind_callback(ks, key="ks")
+    os_, is_ = [], []
+    for state in model.simulate(df):
+        os_.append(state.o_t_next.copy())
+        is_.append(state.i_t_next.copy())
+    times = sorted(ks.P_s.keys())
+    save("g11_smoother.npz", endnodes=endnodes, K=K, X=X, o0=o0, dt=3600.0,
+         start_ns=start.value, idx_ns=df.index.asi8, forcing=df.values, gages=gages,
+         meas_ns=meas.index.asi8, meas=meas.values, o=np.array(os_), i=np.array(is_),
+         s_ns=np.array([t.value for t in times], dtype=np.int64),
+         o_s=ks.o_hat_s.values, i_s=ks.i_hat_s.values,
+         os_ns=ks.o_hat_s.index.asi8 if hasattr(ks.o_hat_s.index, "asi8") else
+         np.array([pd.Timestamp(t).value for t in ks.o_hat_s.index]),
+         P_s=np.array([ks.P_s[t] for t in times]),
+         P_f_final=ks.P_f[times[-1]], n_times=np.array(len(ks.datetimes)))
+
+
 def main():
     warnings.simplefilter("ignore")
     tmp, mk, nu, sim, da, tio = _import_reference()
+    only = set(sys.argv[1:])
+    if only:
+        try:
+            for name in sorted(only):
+                {"g11": lambda: g11_smoother(mk, da)}[name]()
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     try:
         g1_y_network(mk)
         g2_huc8(mk)
@@ -464,6 +508,7 @@ def main():
         g8_ax_bu_edge(nu)
         g9_interp(nu)
         g10_model_io(mk, tio)
+        g11_smoother(mk, da)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

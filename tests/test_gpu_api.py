@@ -1,0 +1,127 @@
+"""GPU parity of the reference-API mirror: Muskingum / ModelCollection / AsyncSimulation /
+CheckPoint routed by libmcroute.so, bit-exact against the golden vectors generated from the
+reference (tests/golden/make_golden.py).  Both simulation paths run: the fused horizon (no
+callbacks: one mc_run per horizon) and the step-by-step path (a bound callback: one mc_step per
+step, hooks fired in between)."""
+import asyncio
+import hashlib
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from api_helpers import golden_frame, golden_model, run
+from tx_fast_hydrology_amd import engine
+from tx_fast_hydrology_amd.callbacks import BaseCallback
+from tx_fast_hydrology_amd.simulation import AsyncSimulation, CheckPoint
+
+pytestmark = pytest.mark.gpu
+
+
+class Recorder(BaseCallback):
+    def __init__(self, model):
+        self.model = model
+        self.events = []
+
+    def __on_simulation_start__(self):
+        self.events.append(("start", self.model.datetime.value))
+
+    def __on_step_start__(self):
+        self.events.append(("step_start", self.model.datetime.value))
+
+    def __on_step_end__(self):
+        self.events.append(("step_end", self.model.datetime.value))
+
+    def __on_simulation_end__(self):
+        self.events.append(("end", self.model.datetime.value))
+
+
+@pytest.mark.parametrize("callback", [False, True])
+@pytest.mark.parametrize("name", ["g1_ynet.npz", "g3_confluence.npz", "g2_huc8.npz"])
+def test_simulate_golden(golden, name, callback):
+    g = golden(name)
+    m = golden_model(g)
+    rec = None
+    if callback:
+        rec = Recorder(m)
+        m.bind_callback(rec, key="rec")
+    o, i, t = run(m, golden_frame(g, m.reach_ids))
+    assert isinstance(m._device.net, engine.RoutingNet)       # the HIP session routed it
+    if "o_keep" in g:
+        keep = g["keep"]
+        assert np.array_equal(o[keep], g["o_keep"]) and np.array_equal(i[keep], g["i_keep"])
+        sha = np.array([np.frombuffer(hashlib.sha256(np.ascontiguousarray(r)).digest(),
+                                      np.uint8) for r in o])
+        assert np.array_equal(sha, g["o_sha"])
+        assert np.array_equal(t, g["t_ns"])
+    else:
+        k = len(g["o"])
+        assert np.array_equal(o[:k], g["o"]) and np.array_equal(i[:k], g["i"])
+        assert np.array_equal(t[:k], g["t_ns"])
+    if rec is not None:
+        T = len(t)
+        assert rec.events[0][0] == "start" and rec.events[-1][0] == "end"
+        assert [e for e, _ in rec.events[1:-1]] == ["step_start", "step_end"] * T
+        assert [v for e, v in rec.events if e == "step_end"] == t.tolist()
+
+
+def test_dt_change_quirk(golden):
+    g = golden("g6_dt_change.npz")
+    m = golden_model(g)
+    for k, (q, td) in enumerate(zip(g["q"], g["td"])):
+        m.step(q, timedelta=None if td < 0 else pd.Timedelta(int(td), unit="s"))
+        assert np.array_equal(m.o_t_next, g["o"][k]) and np.array_equal(m.i_t_next, g["i"][k])
+        assert m.datetime.value == g["t_ns"][k]
+
+
+def test_fused_fallback_and_continuation(golden):
+    g = golden("g3_confluence.npz")
+    outs = []
+    for fused in (True, False):
+        m = golden_model(g)
+        df = golden_frame(g, m.reach_ids)
+        if not fused:
+            m.bind_callback(BaseCallback(), key="noop")
+        seq = []
+        for k, state in enumerate(m.simulate(df, end_time=df.index[4])):
+            seq.append(np.array(state.o_t_next))
+            if k == 5:
+                state.o_t_next = state.o_t_next * 0.75
+        # a second horizon continues from the state left by the first
+        for state in m.simulate(df):
+            seq.append(np.array(state.o_t_next))
+        outs.append(np.array(seq))
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_async_simulation_golden(golden):
+    g = golden("g4_split_async.npz")
+    whole = golden_model(g)
+    df = golden_frame(g, whole.reach_ids)
+    coll = whole.split(g["cuts"], create_state_space=False)
+    sim = AsyncSimulation(coll, df)
+    outputs = asyncio.run(sim.simulate())
+    for name in g["names"]:
+        p = f"sub{name}_"
+        assert np.array_equal(outputs[str(name)].values, g[p + "o"]), name
+        assert np.array_equal(sim.inputs[str(name)].values, g[p + "inputs"]), name
+        assert np.array_equal(coll.models[str(name)].i_t_next, g[p + "init_i"]), name
+    o, i, _ = run(golden_model(g), df)
+    assert np.array_equal(o, g["o_whole"]) and np.array_equal(i, g["i_whole"])
+
+
+def test_checkpoint_and_reload(golden):
+    g = golden("g2_huc8.npz")
+    m = golden_model(g)
+    df = golden_frame(g, m.reach_ids)
+    cp = CheckPoint(m, timedelta=3600.0)
+    m.bind_callback(cp, key="cp")
+    o, i, t = run(m, df)
+    k = int(np.flatnonzero(t >= t[0] - 300 * 10**9 + 3600 * 10**9)[0])
+    assert m.saved_states["datetime"].value == t[k]
+    assert np.array_equal(m.saved_states["o_t_next"], o[k])
+    # reload the checkpoint and re-route the rest without callbacks (fused): same series
+    m.unbind_callback("cp")
+    m.load_state()
+    o2, i2, t2 = run(m, df)
+    assert np.array_equal(o2, o[k + 1:]) and np.array_equal(i2, i[k + 1:])

@@ -1,0 +1,521 @@
+// Full-covariance Kalman filter on the device: the da.py KalmanFilter and
+// KalmanSmoother products, with the covariance resident in HBM.
+//
+//   _ap_par   (nutils.py:157-170):  out = A P            one _ax sweep per column of P
+//   _aqat_par (nutils.py:194-214):  out = A (A P)^T      = A P A^T for symmetric P
+//   filter    (da.py:91-136):       P- = A P A^T + Q,  K = P-[:, s] (P-[s, s] + R)^-1,
+//                                   gain = K dz,  P+ = P- - K P-[s, :]
+//   _apply_gain (nutils.py:116-134) as a stateless gather
+//
+// A is never formed.  Applying it to a column is the reference walk _ax (nutils.py:91-114):
+//   o[j] = 0 + ((alpha_j I[j] + beta_j Ip[j]) + chi_j x[j])
+//   I[j]  = ((0 + o[u1]) + o[u2]) + ...   routed upstreams in the walk's finalisation order
+//   Ip[j] = ((0 + x[i1]) + x[i2]) + ...   every i with endnodes[i] == j, in index order, self-loops
+//                                         included (numba_init_inflows, nutils.py:136-141)
+// Columns are independent, so they map to lanes (16 per workgroup, coalesced 128-B row
+// segments); reaches are swept level by level (a level's reaches depend only on lower levels),
+// 16 reach lanes per workgroup, one barrier per level.  When the 16 columns of all reaches fit
+// (n <= 1024) their outputs stay in LDS, so the chain reads upstream outflows from LDS.
+// Results are bit-identical to the reference walk: same operations, same association, same
+// summation order, FMA contraction off.  The dense update products run on the f64 MFMA GEMM
+// (analysis.hip); the m x m solve is rocSOLVER LU (getrf / getrs), as np.linalg.inv is LU.
+#include <hip/hip_runtime.h>
+
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "analysis.hpp"
+#include "capi_common.hpp"
+#include "mcroute.h"
+
+#pragma clang fp contract(off)
+
+namespace mcr {
+namespace {
+
+using namespace capi;
+
+constexpr int kCB = 16;                  // columns per workgroup
+constexpr int kRL = 256 / kCB;           // reach lanes per workgroup
+constexpr int64_t kLdsReaches = 1024;    // LDS-resident outputs up to this many reaches
+
+struct GraphArgs {
+    const int32_t* lv_off;   // [n_levels + 1] into lv_reach
+    const int32_t* lv_reach; // routed reaches, level by level
+    const int32_t* up_off;   // [n + 1] routed upstreams in finalisation order
+    const int32_t* up;
+    const int32_t* in_off;   // [n + 1] every upstream (index order, self-loops) for Ip
+    const int32_t* in_src;
+    const int32_t* unrouted; // reaches the walk never finalises (cycles): o = 0
+    const double* alpha;
+    const double* beta;
+    const double* chi;
+    int32_t n_levels;
+    int32_t n_unrouted;
+};
+
+// Y[:, c] = A X[:, c] for the columns c of this workgroup; X, Y row-major n x ld.
+template <bool LDS>
+__global__ __launch_bounds__(256) void ax_columns(GraphArgs a, const double* __restrict__ X,
+                                                  double* __restrict__ Y, int64_t ld,
+                                                  int64_t C) {
+    extern __shared__ double ys[];   // [n][kCB] outputs of this column block (LDS variant)
+    const int cl = threadIdx.x % kCB;
+    const int rl = threadIdx.x / kCB;
+    const int64_t c = (int64_t)blockIdx.x * kCB + cl;
+    const bool col = c < C;
+    const int64_t cs = col ? c : 0;  // keep loads in bounds for idle lanes
+    for (int k = rl; k < a.n_unrouted; k += kRL)
+        if (col) Y[(int64_t)a.unrouted[k] * ld + c] = 0.0;
+    for (int lv = 0; lv < a.n_levels; ++lv) {
+        const int e = a.lv_off[lv + 1];
+        for (int k = a.lv_off[lv] + rl; k < e; k += kRL) {
+            const int j = a.lv_reach[k];
+            double ip = 0.0;
+            for (int q = a.in_off[j], qe = a.in_off[j + 1]; q < qe; ++q)
+                ip += X[(int64_t)a.in_src[q] * ld + cs];
+            double in = 0.0;
+            for (int q = a.up_off[j], qe = a.up_off[j + 1]; q < qe; ++q) {
+                const int u = a.up[q];
+                in += LDS ? ys[u * kCB + cl] : Y[(int64_t)u * ld + cs];
+            }
+            const double o = 0.0 + ((a.alpha[j] * in + a.beta[j] * ip) +
+                                    a.chi[j] * X[(int64_t)j * ld + cs]);
+            if (LDS) ys[j * kCB + cl] = o;
+            if (col) Y[(int64_t)j * ld + c] = o;
+        }
+        __syncthreads();
+    }
+}
+
+// out = in^T (n x n row-major), 32 x 32 tiles through LDS
+__global__ __launch_bounds__(256) void transpose(const double* __restrict__ in,
+                                                 double* __restrict__ out, int64_t n) {
+    __shared__ double t[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+    const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
+    for (int k = ty; k < 32; k += 8)
+        if (r0 + k < n && c0 + tx < n) t[k][tx] = in[(r0 + k) * n + c0 + tx];
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8)
+        if (c0 + k < n && r0 + tx < n) out[(c0 + k) * n + r0 + tx] = t[tx][k];
+}
+
+__global__ void add_into(double* __restrict__ y, const double* __restrict__ q, int64_t cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cnt) y[i] = y[i] + q[i];
+}
+
+__global__ void sub_into(double* __restrict__ y, const double* __restrict__ a,
+                         const double* __restrict__ b, int64_t cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cnt) y[i] = a[i] - b[i];
+}
+
+// _apply_gain: o[j] = 0 + g[j] (routed), i[j] = fold of the routed upstream o in walk order
+__global__ void apply_gain_gather(GraphArgs a, const uint8_t* __restrict__ routed,
+                                  const double* __restrict__ g, double* __restrict__ io,
+                                  double* __restrict__ oo, int64_t n) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    double in = 0.0;
+    for (int q = a.up_off[j], qe = a.up_off[j + 1]; q < qe; ++q) in += 0.0 + g[a.up[q]];
+    io[j] = in;
+    oo[j] = routed[j] ? 0.0 + g[j] : 0.0;
+}
+
+// S (column-major m x m) = P[s][:, s] + R (R row-major, as numpy);
+// Bt (column-major m x n) = P[:, s]^T;  Ps (column-major m x n) = P[s, :]
+__global__ void kf_gather(const double* __restrict__ P, const int64_t* __restrict__ s,
+                          const double* __restrict__ R, double* __restrict__ S,
+                          double* __restrict__ Bt, double* __restrict__ Ps, int64_t n,
+                          int64_t m) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < m * n) {
+        const int64_t g = idx % m, j = idx / m;
+        Bt[idx] = P[j * n + s[g]];
+        Ps[idx] = P[s[g] * n + j];
+    }
+    if (idx < m * m) {
+        const int64_t a = idx % m, b = idx / m;
+        S[idx] = P[s[a] * n + s[b]] + R[a * m + b];
+    }
+}
+
+dim3 blocks_for(int64_t cnt, int threads) {
+    return dim3((unsigned)((cnt + threads - 1) / threads));
+}
+
+template <class T>
+void upload_vec(DBuf<T>& d, const std::vector<T>& v, hipStream_t s) {
+    d.upload(v.data(), v.size(), s);
+}
+
+}  // namespace
+
+// Reach graph of one network for the covariance sweeps (walk replay of nutils._ax).
+struct Cov {
+    int64_t n = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    int32_t n_levels = 0, n_unrouted = 0;
+    DBuf<int32_t> lv_off, lv_reach, up_off, up, in_off, in_src, unrouted;
+    DBuf<uint8_t> routed;
+    DBuf<double> alpha, beta, chi;
+    bool coeffs_set = false;
+    // scratch: A P, the transposed product, KF gathers, gain / dz / R / gauges, LU state
+    DBuf<double> T1, T2, T3, S, Bt, Ps, gdev, ddev, Rdev;
+    DBuf<int64_t> sdev;
+    DBuf<rocblas_int> ipiv, info;
+    rocblas_handle blas = nullptr;
+
+    ~Cov() {
+        if (blas) rocblas_destroy_handle(blas);
+        if (own) (void)hipStreamDestroy(own);
+    }
+
+    void build(int64_t n_, const int64_t* end, const int64_t* indeg, const int64_t* heads,
+               int64_t n_head) {
+        n = n_;
+        REQUIRE(n < (int64_t)INT32_MAX, "network too large for the covariance sweep");
+        for (int64_t j = 0; j < n; ++j)
+            if (end[j] < 0 || end[j] >= n)
+                throw Fail(MC_E_TOPOLOGY, "endnodes index out of range");
+        // walk replay (nutils.py:98-113): finalisation order, levels, routed upstream lists
+        std::vector<int64_t> left(indeg, indeg + n);
+        std::vector<int32_t> level(n, 0), rank(n, -1);
+        std::vector<std::vector<int32_t>> ups(n);
+        int32_t r = 0;
+        for (int64_t k = 0; k < n_head; ++k) {
+            int64_t j = heads[k];
+            if (j < 0 || j >= n) throw Fail(MC_E_TOPOLOGY, "headwater index out of range");
+            while (left[j] == 0) {
+                if (rank[j] >= 0)
+                    throw Fail(MC_E_TOPOLOGY,
+                               "a reach would be finalised twice (inconsistent indegree)");
+                rank[j] = r++;
+                const int64_t d = end[j];
+                if (d != j) {
+                    ups[d].push_back((int32_t)j);
+                    level[d] = std::max(level[d], level[j] + 1);
+                }
+                left[d] -= 1;
+                j = d;
+            }
+        }
+        std::vector<int32_t> uo(n + 1, 0), ul, io(n + 1, 0), il, un;
+        for (int64_t j = 0; j < n; ++j) {
+            uo[j + 1] = uo[j] + (int32_t)ups[j].size();
+            ul.insert(ul.end(), ups[j].begin(), ups[j].end());
+        }
+        std::vector<std::vector<int32_t>> ins(n);
+        for (int64_t i = 0; i < n; ++i) ins[end[i]].push_back((int32_t)i);
+        for (int64_t j = 0; j < n; ++j) {
+            io[j + 1] = io[j] + (int32_t)ins[j].size();
+            il.insert(il.end(), ins[j].begin(), ins[j].end());
+        }
+        int32_t L = 0;
+        std::vector<uint8_t> rt(n, 0);
+        for (int64_t j = 0; j < n; ++j) {
+            if (rank[j] >= 0) {
+                rt[j] = 1;
+                L = std::max(L, level[j] + 1);
+            } else {
+                un.push_back((int32_t)j);
+            }
+        }
+        std::vector<int32_t> lo(L + 1, 0), lr(r);
+        for (int64_t j = 0; j < n; ++j)
+            if (rt[j]) lo[level[j] + 1]++;
+        for (int32_t l = 0; l < L; ++l) lo[l + 1] += lo[l];
+        std::vector<int32_t> fill(lo.begin(), lo.end() - 1);
+        for (int64_t j = 0; j < n; ++j)
+            if (rt[j]) lr[fill[level[j]]++] = (int32_t)j;
+        n_levels = L;
+        n_unrouted = (int32_t)un.size();
+        HIPC(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+        stream = own;
+        upload_vec(lv_off, lo, stream);
+        upload_vec(lv_reach, lr, stream);
+        upload_vec(up_off, uo, stream);
+        upload_vec(up, ul, stream);
+        upload_vec(in_off, io, stream);
+        upload_vec(in_src, il, stream);
+        upload_vec(unrouted, un, stream);
+        upload_vec(routed, rt, stream);
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    GraphArgs args() const {
+        GraphArgs a;
+        a.lv_off = lv_off.p;
+        a.lv_reach = lv_reach.p;
+        a.up_off = up_off.p;
+        a.up = up.p;
+        a.in_off = in_off.p;
+        a.in_src = in_src.p;
+        a.unrouted = unrouted.p;
+        a.alpha = alpha.p;
+        a.beta = beta.p;
+        a.chi = chi.p;
+        a.n_levels = n_levels;
+        a.n_unrouted = n_unrouted;
+        return a;
+    }
+
+    rocblas_handle solver() {
+        if (!blas && rocblas_create_handle(&blas) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocblas_create_handle failed");
+        if (rocblas_set_stream(blas, stream) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocblas_set_stream failed");
+        return blas;
+    }
+
+    // Y = A X (square n x n, row-major); X and Y must not alias
+    void ax(const double* X, double* Y) {
+        REQUIRE(coeffs_set, "mc_cov_set_coeffs has not been called");
+        if (n == 0) return;
+        const dim3 grid((unsigned)((n + kCB - 1) / kCB));
+        if (n <= kLdsReaches) {
+            const size_t lds = (size_t)n * kCB * sizeof(double);
+            HIPC(hipFuncSetAttribute((const void*)ax_columns<true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL(ax_columns<true>, grid, 256, lds, stream, args(), X, Y, n, n);
+        } else {
+            hipLaunchKernelGGL(ax_columns<false>, grid, 256, 0, stream, args(), X, Y, n, n);
+        }
+        HIPC(hipGetLastError());
+    }
+
+    void aqat(const double* P, const double* Q, double* out) {
+        if (n == 0) return;
+        T1.reserve((size_t)n * n);
+        T2.reserve((size_t)n * n);
+        ax(P, T1.p);                                      // A P
+        const dim3 tg((unsigned)((n + 31) / 32), (unsigned)((n + 31) / 32));
+        hipLaunchKernelGGL(transpose, tg, 256, 0, stream, T1.p, T2.p, n);
+        HIPC(hipGetLastError());
+        ax(T2.p, out);                                    // A (A P)^T
+        if (Q) {
+            hipLaunchKernelGGL(add_into, blocks_for(n * n, 256), 256, 0, stream, out, Q, n * n);
+            HIPC(hipGetLastError());
+        }
+    }
+
+    void apply_gain(const double* g, double* io, double* oo) {
+        if (n == 0) return;
+        gdev.reserve(3 * (size_t)n);
+        HIPC(hipMemcpyAsync(gdev.p, g, n * sizeof(double), hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(apply_gain_gather, blocks_for(n, 256), 256, 0, stream, args(),
+                           routed.p, gdev.p, gdev.p + n, gdev.p + 2 * n, n);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(io, gdev.p + n, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+        HIPC(hipMemcpyAsync(oo, gdev.p + 2 * n, n * sizeof(double), hipMemcpyDeviceToHost,
+                            stream));
+        HIPC(hipStreamSynchronize(stream));
+    }
+
+    // da.py:118-122 on the prior P-: K (n x m) = P-[:, s] (P-[s, s] + R)^-1, gain = K dz,
+    // P+ = P- - K P-[s, :].  P_post may alias P_prior (in-place posterior).
+    void kf_update(int64_t m, const int64_t* s, const double* R, const double* dz,
+                   const double* Pp, double* Pq, double* K_out, double* gain_out) {
+        REQUIRE(m >= 1 && m <= n, "need 1 <= m <= n gauges");
+        for (int64_t g = 0; g < m; ++g)
+            REQUIRE(s[g] >= 0 && s[g] < n, "gauge index out of range");
+        S.reserve((size_t)m * m);
+        Bt.reserve((size_t)m * n);
+        Ps.reserve((size_t)m * n);
+        Rdev.upload(R, (size_t)m * m, stream);
+        ddev.upload(dz, (size_t)m, stream);
+        sdev.upload(s, (size_t)m, stream);
+        gdev.reserve((size_t)std::max<int64_t>(3 * n, 1));
+        ipiv.reserve((size_t)m);
+        info.reserve(1);
+        hipLaunchKernelGGL(kf_gather, blocks_for(std::max(m * n, m * m), 256), 256, 0, stream,
+                           Pp, sdev.p, Rdev.p, S.p, Bt.p, Ps.p, n, m);
+        HIPC(hipGetLastError());
+        rocblas_handle h = solver();
+        if (rocsolver_dgetrf(h, (rocblas_int)m, (rocblas_int)m, S.p, (rocblas_int)m, ipiv.p,
+                             info.p) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dgetrf failed");
+        // (S^T) Y = P-[:, s]^T  ->  Y = K^T (column-major m x n = K row-major n x m)
+        if (rocsolver_dgetrs(h, rocblas_operation_transpose, (rocblas_int)m, (rocblas_int)n,
+                             S.p, (rocblas_int)m, ipiv.p, Bt.p, (rocblas_int)m) !=
+            rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dgetrs failed");
+        HIPC(launch_dgemm(true, false, n, 1, m, 1.0, Bt.p, m, ddev.p, m, 0.0, gdev.p, n,
+                          stream));
+        if (Pq != Pp)
+            HIPC(hipMemcpyAsync(Pq, Pp, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice,
+                                stream));
+        // column-major view Pc = P^T:  Pc+ = Pc - Ps^T Y
+        HIPC(launch_dgemm(true, false, n, n, m, -1.0, Ps.p, m, Bt.p, m, 1.0, Pq, n, stream));
+        rocblas_int info_h = 0;
+        HIPC(hipMemcpyAsync(&info_h, info.p, sizeof(rocblas_int), hipMemcpyDeviceToHost,
+                            stream));
+        HIPC(hipMemcpyAsync(gain_out, gdev.p, n * sizeof(double), hipMemcpyDeviceToHost,
+                            stream));
+        if (K_out)
+            HIPC(hipMemcpyAsync(K_out, Bt.p, (size_t)m * n * sizeof(double),
+                                hipMemcpyDeviceToHost, stream));
+        HIPC(hipStreamSynchronize(stream));
+        if (info_h != 0)
+            throw Fail(MC_E_STATE, "P-[s, s] + R is singular (getrf info " +
+                                       std::to_string(info_h) + ")");
+    }
+
+    // RTS step (da.py:241-251): J = (P_p1^-1 A P_f)^T, P_s = P_f + J (P_s1 - P_p1),
+    // x_s = x_f + J d for nvec host vectors d = x_s1 - x_p1.  Row-major buffers are read as
+    // column-major transposes: solving with getrs(transpose) on the LU of P_p1's buffer and the
+    // transposed A P_f leaves a buffer whose row-major view is J.
+    void ks_step(const double* Pf, const double* Pp1, const double* Ps1, double* Ps_out,
+                 int64_t nvec, const double* xf, const double* d, double* xs_out) {
+        if (n == 0) return;
+        REQUIRE(nvec >= 0 && (nvec == 0 || (xf && d && xs_out)), "bad vector arguments");
+        const size_t nn = (size_t)n * n;
+        T1.reserve(nn);
+        T2.reserve(nn);
+        T3.reserve(nn);
+        ipiv.reserve((size_t)n);
+        info.reserve(1);
+        ax(Pf, T1.p);                                               // A P_f
+        const dim3 tg((unsigned)((n + 31) / 32), (unsigned)((n + 31) / 32));
+        hipLaunchKernelGGL(transpose, tg, 256, 0, stream, T1.p, T2.p, n);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(T3.p, Pp1, nn * sizeof(double), hipMemcpyDeviceToDevice, stream));
+        rocblas_handle h = solver();
+        if (rocsolver_dgetrf(h, (rocblas_int)n, (rocblas_int)n, T3.p, (rocblas_int)n, ipiv.p,
+                             info.p) != rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dgetrf failed");
+        if (rocsolver_dgetrs(h, rocblas_operation_transpose, (rocblas_int)n, (rocblas_int)n,
+                             T3.p, (rocblas_int)n, ipiv.p, T2.p, (rocblas_int)n) !=
+            rocblas_status_success)
+            throw Fail(MC_E_HIP, "rocsolver_dgetrs failed");
+        hipLaunchKernelGGL(sub_into, blocks_for((int64_t)nn, 256), 256, 0, stream, T1.p, Ps1,
+                           Pp1, (int64_t)nn);                      // D = P_s1 - P_p1
+        HIPC(hipGetLastError());
+        if (Ps_out != Pf)
+            HIPC(hipMemcpyAsync(Ps_out, Pf, nn * sizeof(double), hipMemcpyDeviceToDevice,
+                                stream));
+        HIPC(launch_dgemm(false, false, n, n, n, 1.0, T1.p, n, T2.p, n, 1.0, Ps_out, n, stream));
+        if (nvec > 0) {
+            gdev.reserve((size_t)std::max<int64_t>(2 * nvec * n, 3 * n));
+            HIPC(hipMemcpyAsync(gdev.p, d, nvec * n * sizeof(double), hipMemcpyHostToDevice,
+                                stream));
+            HIPC(hipMemcpyAsync(gdev.p + nvec * n, xf, nvec * n * sizeof(double),
+                                hipMemcpyHostToDevice, stream));
+            HIPC(launch_dgemm(true, false, n, nvec, n, 1.0, T2.p, n, gdev.p, n, 1.0,
+                              gdev.p + nvec * n, n, stream));
+            HIPC(hipMemcpyAsync(xs_out, gdev.p + nvec * n, nvec * n * sizeof(double),
+                                hipMemcpyDeviceToHost, stream));
+        }
+        rocblas_int info_h = 0;
+        HIPC(hipMemcpyAsync(&info_h, info.p, sizeof(rocblas_int), hipMemcpyDeviceToHost,
+                            stream));
+        HIPC(hipStreamSynchronize(stream));
+        if (info_h != 0)
+            throw Fail(MC_E_STATE, "the predicted covariance is singular (getrf info " +
+                                       std::to_string(info_h) + ")");
+    }
+};
+
+}  // namespace mcr
+
+using mcr::Cov;
+using namespace mcr::capi;
+
+static Cov* as_cov(void* h) {
+    REQUIRE(h, "NULL covariance handle");
+    return static_cast<Cov*>(h);
+}
+
+extern "C" {
+
+int mc_cov_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
+                  const int64_t* headwaters, int64_t n_head, void** cov) {
+    return guarded([&] {
+        REQUIRE(cov, "cov must not be NULL");
+        REQUIRE(n >= 0 && (n == 0 || (endnodes && indegree)), "bad network arrays");
+        REQUIRE(n_head >= 0 && (n_head == 0 || headwaters), "bad headwater list");
+        auto c = std::make_unique<Cov>();
+        c->build(n, endnodes, indegree, headwaters, n_head);
+        *cov = c.release();
+    });
+}
+
+int mc_cov_destroy(void* cov) {
+    return guarded([&] { delete static_cast<Cov*>(cov); });
+}
+
+int mc_cov_set_stream(void* cov, void* hip_stream) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        c->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->own;
+    });
+}
+
+int mc_cov_set_coeffs(void* cov, const double* alpha, const double* beta, const double* chi) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        REQUIRE(c->n == 0 || (alpha && beta && chi), "coefficient arrays must not be NULL");
+        c->alpha.upload(alpha, c->n, c->stream);
+        c->beta.upload(beta, c->n, c->stream);
+        c->chi.upload(chi, c->n, c->stream);
+        HIPC(hipStreamSynchronize(c->stream));
+        c->coeffs_set = true;
+    });
+}
+
+int mc_cov_ap(void* cov, const double* P, double* out) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        REQUIRE(c->n == 0 || (P && out && P != out), "P / out must be distinct device buffers");
+        c->ax(P, out);
+    });
+}
+
+int mc_cov_aqat(void* cov, const double* P, const double* Q, double* out) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        REQUIRE(c->n == 0 || (P && out), "P / out must not be NULL");
+        c->aqat(P, Q, out);
+    });
+}
+
+int mc_cov_apply_gain(void* cov, const double* gain, double* i_gain, double* o_gain) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        REQUIRE(c->n == 0 || (gain && i_gain && o_gain), "gain arrays must not be NULL");
+        c->apply_gain(gain, i_gain, o_gain);
+    });
+}
+
+int mc_kf_update(void* cov, int64_t m, const int64_t* s, const double* R, const double* dz,
+                 const double* P_prior, double* P_post, double* K_out, double* gain_out) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        REQUIRE(s && R && dz && P_prior && P_post && gain_out, "NULL argument");
+        c->kf_update(m, s, R, dz, P_prior, P_post, K_out, gain_out);
+    });
+}
+
+int mc_ks_step(void* cov, const double* P_f, const double* P_p1, const double* P_s1,
+               double* P_s_out, int64_t nvec, const double* x_f, const double* d,
+               double* x_s_out) {
+    return guarded([&] {
+        Cov* c = as_cov(cov);
+        REQUIRE(c->n == 0 || (P_f && P_p1 && P_s1 && P_s_out), "NULL matrix");
+        c->ks_step(P_f, P_p1, P_s1, P_s_out, nvec, x_f, d, x_s_out);
+    });
+}
+
+int mc_cov_synchronize(void* cov) {
+    return guarded([&] { HIPC(hipStreamSynchronize(as_cov(cov)->stream)); });
+}
+
+}  // extern "C"

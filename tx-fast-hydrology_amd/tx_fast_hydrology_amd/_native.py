@@ -104,6 +104,16 @@ SIGNATURES = {
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),
     "mc_get_trace": (_i32, [_vp, _vp, _i64, ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_int64)]),
+    "mc_cov_create": (_i32, [_i64, _vp, _vp, _vp, _i64, _pp]),
+    "mc_cov_destroy": (_i32, [_vp]),
+    "mc_cov_set_stream": (_i32, [_vp, _vp]),
+    "mc_cov_set_coeffs": (_i32, [_vp, _vp, _vp, _vp]),
+    "mc_cov_ap": (_i32, [_vp, _vp, _vp]),
+    "mc_cov_aqat": (_i32, [_vp, _vp, _vp, _vp]),
+    "mc_cov_apply_gain": (_i32, [_vp, _vp, _vp, _vp]),
+    "mc_kf_update": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mc_ks_step": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "mc_cov_synchronize": (_i32, [_vp]),
 }
 
 _lib = None
@@ -119,6 +129,14 @@ def lib():
     if _lib is not None:
         return _lib
     path = lib_path()
+    # PyTorch-ROCm ships its own HIP runtime (libamdhip64.so.7, rocBLAS, rocSOLVER).  One process
+    # can hold only one: when torch is present it is loaded first, so that libmcroute.so binds
+    # to the same runtime (loaded the other way round, torch finds no device) and device
+    # tensors and streams can be shared with the engine.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         try:
             _build.build()

@@ -329,3 +329,145 @@ def ax_bu(startnodes, endnodes, alpha, beta, chi, gamma, i_t_prev, o_t_prev, q_t
                                      ptr(g), ptr(ip), ptr(op), ptr(q), ptr(deg), ptr(i_out),
                                      ptr(o_out)))
     return i_out, o_out
+
+
+class CovGraph:
+    """Covariance propagation and Kalman update on the device (mcroute.h ``mc_cov_*``,
+    ``mc_kf_update``; reference ``nutils.py:91-214`` and ``da.py:91-136``).
+
+    Matrices are row-major n x n float64 CUDA tensors (torch, on the current stream); the
+    handle's stream follows ``torch.cuda.current_stream()`` at every call.
+    """
+
+    def __init__(self, endnodes, indegree, headwaters):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise nat.NativeUnavailable("CovGraph needs a GPU (torch.cuda is not available)")
+        self._torch = torch
+        end, deg, heads = i64(endnodes), i64(indegree), i64(headwaters)
+        self.n = end.size
+        if deg.size != self.n:
+            raise ValueError("indegree and endnodes must have the same length")
+        h = ctypes.c_void_p()
+        nat.check(nat.lib().mc_cov_create(self.n, ptr(end), ptr(deg), ptr(heads), heads.size,
+                                          ctypes.byref(h)))
+        self._h = h
+
+    def _sync_stream(self):
+        """Order the next library call after the work queued on torch's current stream.
+
+        The handle runs on a private torch stream (never the null stream, so the ordering is
+        explicit): it waits for torch's current stream before every call, and ``_done`` makes
+        torch's current stream wait for it afterwards."""
+        t = self._torch
+        if getattr(self, "_stream", None) is None:
+            self._stream = t.cuda.Stream()
+            nat.check(nat.lib().mc_cov_set_stream(self._h,
+                                                  ctypes.c_void_p(self._stream.cuda_stream)))
+        self._stream.wait_stream(t.cuda.current_stream())
+
+    def _done(self, *tensors):
+        t = self._torch
+        for x in tensors:
+            if x is not None:
+                x.record_stream(self._stream)
+        t.cuda.current_stream().wait_stream(self._stream)
+
+    def _mat(self, P):
+        t = self._torch
+        if not isinstance(P, t.Tensor):
+            P = t.as_tensor(np.ascontiguousarray(P, dtype=np.float64), device="cuda")
+        if P.dtype != t.float64 or not P.is_cuda or P.shape != (self.n, self.n):
+            raise ValueError(f"expected a float64 CUDA tensor of shape ({self.n}, {self.n})")
+        return P.contiguous()
+
+    def empty(self):
+        return self._torch.empty((self.n, self.n), dtype=self._torch.float64, device="cuda")
+
+    def set_coeffs(self, alpha, beta, chi):
+        a, b, c = f64(alpha), f64(beta), f64(chi)
+        if not (a.size == b.size == c.size == self.n):
+            raise ValueError("coefficient arrays must have n entries")
+        self._sync_stream()
+        nat.check(nat.lib().mc_cov_set_coeffs(self._h, ptr(a), ptr(b), ptr(c)))
+        self._done()
+
+    def ap(self, P, out=None):
+        """A P (_ap_par)."""
+        P = self._mat(P)
+        out = self.empty() if out is None else out
+        self._sync_stream()
+        nat.check(nat.lib().mc_cov_ap(self._h, ctypes.c_void_p(P.data_ptr()),
+                                      ctypes.c_void_p(out.data_ptr())))
+        self._done(P, out)
+        return out
+
+    def aqat(self, P, Q=None, out=None):
+        """A P A^T (+ Q): _aqat_par then da.py:117."""
+        P = self._mat(P)
+        Q = None if Q is None else self._mat(Q)
+        out = self.empty() if out is None else out
+        self._sync_stream()
+        nat.check(nat.lib().mc_cov_aqat(self._h, ctypes.c_void_p(P.data_ptr()),
+                                        None if Q is None else ctypes.c_void_p(Q.data_ptr()),
+                                        ctypes.c_void_p(out.data_ptr())))
+        self._done(P, Q, out)
+        return out
+
+    def apply_gain(self, gain):
+        """_apply_gain: (i_gain, o_gain) host arrays."""
+        g = f64(gain)
+        if g.size != self.n:
+            raise ValueError("gain must have n entries")
+        io, oo = np.empty(self.n), np.empty(self.n)
+        self._sync_stream()
+        nat.check(nat.lib().mc_cov_apply_gain(self._h, ptr(g), ptr(io), ptr(oo)))
+        self._done()
+        return io, oo
+
+    def kf_update(self, s, R, dz, P_prior, P_post=None, want_K=True):
+        """da.py:118-122: returns (P_post, K [n, m] or None, gain [n])."""
+        s, R, dz = i64(s), f64(R), f64(dz)
+        m = s.size
+        if R.shape != (m, m) or dz.size != m:
+            raise ValueError("R must be [m, m] and dz [m]")
+        P_prior = self._mat(P_prior)
+        P_post = P_prior if P_post is None else P_post
+        K = np.empty((self.n, m)) if want_K else None
+        gain = np.empty(self.n)
+        self._sync_stream()
+        nat.check(nat.lib().mc_kf_update(self._h, m, ptr(s), ptr(R), ptr(dz),
+                                         ctypes.c_void_p(P_prior.data_ptr()),
+                                         ctypes.c_void_p(P_post.data_ptr()), ptr(K), ptr(gain)))
+        self._done(P_prior, P_post)
+        return P_post, K, gain
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.lib().mc_cov_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def ks_step(graph, P_f, P_p1, P_s1, i_f, i_p1, i_s1, o_f, o_p1, o_s1):
+    """One RTS backward step on the device (mc_ks_step, da.py:241-251): returns
+    (P_s [device], i_s, o_s) for time t from the filter / prior / smoothed values at t, t+1."""
+    n = graph.n
+    P_f, P_p1, P_s1 = graph._mat(P_f), graph._mat(P_p1), graph._mat(P_s1)
+    d = np.stack([f64(i_s1) - f64(i_p1), f64(o_s1) - f64(o_p1)])
+    xf = np.ascontiguousarray(np.stack([f64(i_f), f64(o_f)]))
+    xs = np.empty((2, n))
+    P_s = graph.empty()
+    graph._sync_stream()
+    nat.check(nat.lib().mc_ks_step(graph._h, ctypes.c_void_p(P_f.data_ptr()),
+                                   ctypes.c_void_p(P_p1.data_ptr()),
+                                   ctypes.c_void_p(P_s1.data_ptr()),
+                                   ctypes.c_void_p(P_s.data_ptr()), 2, ptr(xf), ptr(d), ptr(xs)))
+    graph._done(P_f, P_p1, P_s1, P_s)
+    return P_s, xs[0], xs[1]

@@ -60,8 +60,17 @@ def distributed_analysis(net, gauges, y_local, R, device=None, group=None) -> No
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     if device.type == "cuda" and hasattr(net, "set_stream"):
-        # the session's kernels and torch's collectives must be ordered on one stream
-        net.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        # the session's kernels and torch's collectives must be ordered on one stream, and it
+        # must not be the null stream (the session maps a NULL stream to its own, unordered one)
+        caller = torch.cuda.current_stream(device)
+        if caller.cuda_stream == 0:
+            side = torch.cuda.Stream(device)
+            side.wait_stream(caller)
+            with torch.cuda.stream(side):
+                distributed_analysis(net, gauges, y_local, R, group=group, device=device)
+            caller.wait_stream(side)
+            return
+        net.set_stream(caller.cuda_stream)
     f64 = dict(dtype=torch.float64, device=device)
     HX = torch.empty((E, m), **f64)
     D = torch.empty((E, m), **f64)
