@@ -167,14 +167,28 @@ def test_fused_horizon_falls_back_when_state_replaced(golden, monkeypatch):
             m.bind_callback(BaseCallback(), key="noop")
         out = []
         for k, state in enumerate(m.simulate(df)):
-            if fused:     # read-only views of the fused outputs, then step-by-step arrays
-                assert state.o_t_next.flags.writeable == (k > 7)
+            if fused:     # read-only views of fused outputs (a new fused horizon after k = 7)
+                assert not state.o_t_next.flags.writeable
             out.append(np.array(state.o_t_next))
             if k == 7:    # a consumer nudges the state: the rest routes from it
                 state.o_t_next = state.o_t_next * 1.5
+                state.i_t_next = np.array(state.i_t_next)
         results.append(np.array(out))
     assert np.array_equal(results[0], results[1])
     assert not np.array_equal(results[0][8:50], g["o"][8:])
+    assert np.array_equal(results[0][:8], g["o"][:8])
+
+
+def test_idle_callbacks_switch_to_fused(golden, monkeypatch):
+    """A checkpoint that has been taken is idle: the rest of the horizon is one fused call."""
+    nets = use_oracle_device(monkeypatch)
+    g = golden("g3_confluence.npz")
+    m = golden_model(g)
+    cp = CheckPoint(m, timedelta=3 * float(g["dt"]))
+    m.bind_callback(cp, key="cp")
+    o, i, t = run(m, golden_frame(g, m.reach_ids))
+    assert np.array_equal(o[:50], g["o"]) and np.array_equal(i[:50], g["i"])
+    assert nets[-1].steps == 3 and nets[-1].runs == 1
 
 
 def test_split_topology_golden(golden):

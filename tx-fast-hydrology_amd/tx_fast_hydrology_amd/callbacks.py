@@ -17,6 +17,12 @@ hook                       fired by (reference line it mirrors)
 Every hook is a no-op here; subclasses override the ones they need.  A model with at least one
 bound callback routes step by step on the device, so hooks observe every timestep exactly as in
 the reference; a model without callbacks may route a whole horizon in one device call.
+
+Extension (not in the reference): ``__idle_steps__`` returns True when the callback's step hooks
+will do nothing for the rest of the current simulation (a filter past its last observation, a
+checkpoint already taken).  When every bound callback is idle, ``simulate_iter`` routes the
+remaining steps as one fused device horizon; the simulation-end hook still fires.  The default
+is False (always step by step).
 """
 
 
@@ -43,3 +49,6 @@ class BaseCallback:
 
     def __on_simulation_end__(self):
         return None
+
+    def __idle_steps__(self):
+        return False

@@ -128,6 +128,11 @@ class KalmanFilter(BaseCallback):
             return None
         return self.filter()
 
+    def __idle_steps__(self):
+        # __on_step_end__ filters only while the model time is at or before the last
+        # observation; model time only grows during a simulation
+        return self.model.datetime > self.latest_timestamp
+
     @property
     def latest_measurement(self):
         return self.measurements.iloc[-1, :].values

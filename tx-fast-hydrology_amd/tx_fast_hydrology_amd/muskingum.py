@@ -395,13 +395,14 @@ class Muskingum:
     def simulate_iter(self, dataframe, start_time=None, end_time=None, o_t_init=None, **kwargs):
         """Generator over timesteps (reference :499-536); yields ``self`` after each step.
 
-        Without bound callbacks and without a ``timedelta`` override, the remaining horizon is
-        routed by the device in fused calls (``mc_run``: interpolation of the forcing rows and
+        Without a ``timedelta`` override and while every bound callback is idle
+        (``BaseCallback.__idle_steps__``; no callbacks at all is the common case), the remaining
+        horizon is routed by the device in fused calls (``mc_run``: interpolation of the forcing rows and
         routing of every step in one launch) and the steps are then replayed on the host: the
         yielded state arrays are read-only views of the fetched outputs.  Replacing a state
-        array, rebinding ``datetime`` or binding a callback between two yields switches the rest
-        of the horizon to step-by-step routing from the state found, as the reference would
-        route it.  Coefficients and topology are read when a fused call starts.
+        array, rebinding ``datetime`` or binding a non-idle callback between two yields switches
+        the rest of the horizon to step-by-step routing from the state found, as the reference
+        would route it.  Coefficients and topology are read when a fused call starts.
         """
         assert isinstance(dataframe.index, pd.DatetimeIndex)
         assert dataframe.index.tz == _dt.timezone.utc
@@ -418,7 +419,7 @@ class Muskingum:
         _fire(self.callbacks, "__on_simulation_start__")
         dataframe = dataframe[self.reach_ids]
         xp = dataframe.index.astype(int).astype(float).values
-        fused = not self.callbacks and kwargs.get("timedelta") is None
+        fused = kwargs.get("timedelta") is None and self._callbacks_idle()
         if fused:
             yield from self._simulate_fused(dataframe, xp, end_time, kwargs)
         else:
@@ -429,10 +430,18 @@ class Muskingum:
         from .nutils import interpolate_sample
         fp = dataframe.values
         while self.datetime < end_time:
+            if kwargs.get("timedelta") is None and self._callbacks_idle():
+                yield from self._simulate_fused(dataframe, xp, end_time, kwargs)
+                return
             next_timestep = self.datetime + self.timedelta
             p_t_next = interpolate_sample(float(next_timestep.value), xp, fp)
             self.step_iter(p_t_next, **kwargs)
             yield self
+
+    def _callbacks_idle(self):
+        """True when no bound callback needs to see the remaining steps (``__idle_steps__``)."""
+        return all(getattr(cb, "__idle_steps__", lambda: False)()
+                   for cb in self.callbacks.values())
 
     def _simulate_fused(self, dataframe, xp, end_time, kwargs):
         xs = []
@@ -462,7 +471,7 @@ class Muskingum:
                 expected_time = self.datetime
                 yield self
                 if (self.o_t_next is not o_next or self.i_t_next is not i_next
-                        or self.callbacks or self.datetime != expected_time
+                        or not self._callbacks_idle() or self.datetime != expected_time
                         or self.timedelta != timedelta):
                     self._own_state()
                     yield from self._simulate_steps(dataframe, xp, end_time, kwargs)

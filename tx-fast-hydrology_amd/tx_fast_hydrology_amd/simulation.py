@@ -177,6 +177,9 @@ class CheckPoint(BaseCallback):
             if hasattr(callback, "load_state"):
                 callback.load_state()
 
+    def __idle_steps__(self):
+        return self.model_saved
+
     def set_checkpoint(self, checkpoint_time):
         logger.info(f"Setting checkpoint time to {checkpoint_time}")
         self.checkpoint_time = checkpoint_time
