@@ -109,3 +109,61 @@ def test_ensemble_rejects_dataflow_and_bad_shapes():
     net.set_mode("dataflow")
     with pytest.raises(nat.RoutingError):
         net.run(xp[0] + 300e9 * np.arange(1, 5))
+
+
+@pytest.mark.parametrize("n,E,slots", [(3000, 33, 256), (1200, 2, 128), (4000, 256, 384),
+                                       (190_000, 32, 384)])
+def test_member_dataflow_single_steps(n, E, slots):
+    """One-step runs of an ensemble (the analysis cycle of the EnKF) as member-dataflow launches:
+    member e of slot d at tick G[d] + e.  Several consecutive one-step runs (interpolated
+    between forcing rows) then a multi-step run must equal every member's serial run."""
+    depth = 1500 if n > 100_000 else 120
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4 if n < 100_000 else 300, depth,
+                                                      n + E, E)
+    n = end.size
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=E)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fpe)
+    x = xp[0] + 300e9 * np.arange(1, 16)          # 12 steps per forcing row: fractional rows
+    outs_o, outs_i = [], []
+    for k in range(5):
+        net.run(x[k:k + 1])
+        assert net.mode()[1] == "dataflow", k
+        oo, ii = net.fetch_outputs()
+        outs_o.append(oo[0])
+        outs_i.append(ii[0])
+    net.run(x[5:])
+    assert net.mode()[1] == "launches"
+    oo, ii = net.fetch_outputs()
+    got_o = np.concatenate([np.array(outs_o), oo])
+    got_i = np.concatenate([np.array(outs_i), ii])
+    so, si = net.get_state()
+    for e in range(E) if E <= 40 else list(range(0, E, 17)) + [E - 1]:
+        want_o, want_i, fo, fi = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x,
+                                              xp, np.ascontiguousarray(fpe[:, :, e]))
+        assert np.array_equal(got_o[:, :, e], want_o), e
+        assert np.array_equal(got_i[:, :, e], want_i), e
+        assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
+
+
+def test_member_dataflow_matches_launches_path():
+    E = 20
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(2000, 3, 80, 99, E)
+    x = xp[0] + 300e9 * np.arange(1, 4)
+    res = []
+    for mode in ("auto", "launches"):
+        net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=256, members=E)
+        net.set_mode(mode)
+        net.set_coeffs(*coef)
+        net.set_state(o0, i0)
+        net.load_forcing(xp, fpe)
+        seq = []
+        for k in range(3):
+            net.run(x[k:k + 1])
+            seq.append(net.fetch_outputs())
+        assert net.mode()[1] == ("dataflow" if mode == "auto" else "launches")
+        res.append((seq, net.get_state()))
+    for (a_o, a_i), (b_o, b_i) in zip(res[0][0], res[1][0]):
+        assert np.array_equal(a_o, b_o) and np.array_equal(a_i, b_i)
+    assert all(np.array_equal(a, b) for a, b in zip(res[0][1], res[1][1]))

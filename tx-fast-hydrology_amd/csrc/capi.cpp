@@ -92,7 +92,7 @@ struct Net {
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
     // forcing (slot order) and single-step forcing
-    DBuf<double> F, Fstep, stage;
+    DBuf<double> F, Fstep, stage, Qm;   // Qm: member lateral inflows of a member-dataflow step
     int64_t n_rows = 0;
     std::vector<double> xp;
     // per-step interpolation table {row_lo, row_hi, frac}
@@ -297,6 +297,23 @@ struct Net {
         if (mode == 2 && !ok)
             throw Fail(MC_E_STATE, "dataflow mode requested but this network/horizon does not fit "
                                    "one resident launch");
+        return ok;
+    }
+
+    // Can one step of all E members run as one member-dataflow launch?
+    bool members_fit(size_t& lds) {
+        if (mode == 1) return false;
+        const int S = plan.p.slots;
+        const size_t xg = plan.ext_src.size() * (size_t)E * 16;
+        lds = mcr::flow_lds_bytes(S, 0, plan.max_ext_wg);
+        bool ok = (S == 64 || S == 128 || S == 192 || S == 256 || S == 384 || S == 448) &&
+                  plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
+                  E < (1 << 24) && xg < (size_t(1) << 31) && lds <= 160 * 1024;
+        if (ok) {
+            int bpc = 0;
+            HIPC(mcr::flow_members_occupancy(S, lds, &bpc));
+            ok = (int64_t)bpc * cu_count >= plan.nwg;
+        }
         return ok;
     }
 
@@ -674,8 +691,54 @@ struct Net {
         trace_launch.clear();
         trace_wg.clear();
         size_t flds = 0;
-        if (E > 1 && mode == 2)
-            throw Fail(MC_E_STATE, "dataflow mode routes one member; ensembles use launches");
+        if (E > 1 && mode == 2 && T != 1)
+            throw Fail(MC_E_STATE, "dataflow mode routes one member, or one step of an ensemble");
+        if (E > 1 && T == 1 && members_fit(flds)) {
+            // ---- one step of all members as one dataflow launch (flow.hip, MEMB): member e
+            // of slot d at tick G[d] + e
+            const size_t words = plan.ext_src.size() * (size_t)E * 4;
+            if (words > xg_words || epoch == 0xffffffffu) {
+                XG.reserve(std::max<size_t>(words, 4));
+                HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(words, 4) * 4, stream));
+                xg_words = std::max(xg_words, words);
+                epoch = 0;
+            }
+            ++epoch;
+            Qm.reserve((size_t)(plan.nslots * E * 3));     // IO [E][nslots][2] + Qm [E][nslots]
+            double* IOp = Qm.p + plan.nslots * E;
+            HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
+                                           st_i.p, IOp, Qm.p, E, stream));
+            a.Qm = Qm.p;
+            a.IO = IOp;
+            a.T = (int32_t)E;
+            a.XG = XG.p;
+            a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
+            a.epoch = epoch;
+            a.status = status.p;
+            a.table_cap = 0;
+            a.active = all_wg.p;
+            if (trace) {
+                trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int32_t>(plan.nwg, 1));
+                a.trace = trace_buf.p;
+                trace_launch.assign(plan.nwg, 0);
+                for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
+            }
+            if (timing) HIPC(hipEventRecord(events[0], stream));
+            HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, flds, stream));
+            if (timing) HIPC(hipEventRecord(events[1], stream));
+            HIPC(mcr::launch_member_unpack(IOp, flags.p, G.p, wg_gmin.p, cur->wbase.p,
+                                           row_width(), O.p, cur->Otot, st_o.p, st_i.p,
+                                           plan.nslots, E, stream));
+            HIPC(hipMemcpyAsync(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                stream));
+            status_pending = true;
+            launched = 1;
+            last_path = 2;
+            a.T = (int32_t)T;
+        } else if (E > 1 && mode == 2) {
+            throw Fail(MC_E_STATE, "member dataflow requested but the network does not fit one "
+                                   "resident launch");
+        }
         if (E == 1 && flow_fits(T, dense, flds)) {
             // ---- one dataflow launch for the whole horizon (flow.hip)
             const size_t words = plan.ext_src.size() * (size_t)T * 4;

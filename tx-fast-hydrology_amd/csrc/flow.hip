@@ -148,7 +148,8 @@ struct Helper {
 //   | XE [2][ext_cap][kChunk] f64 (ring of external inputs, one slot per chunk parity)
 //   | EG [kFlowMaxExt] i32 (consumer G)
 // Each tick a lane routes its low slot, then its high slot (fused pairs: kernels.hip).
-template <int SLOTS, bool DENSE>
+// MEMB: member dataflow (kernels.hpp, launch_flow_members): T = E members in place of steps.
+template <int SLOTS, bool DENSE, bool MEMB>
 __global__ __launch_bounds__(SLOTS + kHelperLanes) __attribute__((amdgpu_waves_per_eu(2)))
 void wavefront_flow(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -175,7 +176,8 @@ void wavefront_flow(WaveArgs a) {
     const auto xg = __builtin_amdgcn_make_buffer_rsrc(a.XG, (short)0, (int)a.xg_bytes, 0x00020000);
 
     // ---- shared prologue: step table, consumer ticks of external inputs
-    for (int idx = tid; idx < T; idx += nthr) tab[idx] = a.stab[idx];
+    if (!MEMB)
+        for (int idx = tid; idx < T; idx += nthr) tab[idx] = a.stab[idx];
     for (int idx = tid; idx < next; idx += nthr)
         reinterpret_cast<int*>(lds + EG)[idx] = a.ext_g[e0 + idx];
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;
@@ -234,135 +236,228 @@ void wavefront_flow(WaveArgs a) {
     const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);
     const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
 
-    int rbA, nrA, rbB, nrB;
-    chunk_rows(tab, 0, kb, A.G, T, rbA, nrA);
-    chunk_rows(tab, 0, kb, B.G, T, rbB, nrB);
-    double fA0 = a.F[(int64_t)clamp_row(rbA, nrow) * ns + A.d];
-    double fA1 = a.F[(int64_t)clamp_row(rbA + 1, nrow) * ns + A.d];
-    double fA2 = a.F[(int64_t)clamp_row(rbA + 2, nrow) * ns + A.d];
-    double fB0 = a.F[(int64_t)clamp_row(rbB, nrow) * ns + B.d];
-    double fB1 = a.F[(int64_t)clamp_row(rbB + 1, nrow) * ns + B.d];
-    double fB2 = a.F[(int64_t)clamp_row(rbB + 2, nrow) * ns + B.d];
     const unsigned epoch = a.epoch;
-    __builtin_amdgcn_s_waitcnt(0);                      // nothing pending may enter the loop
-    __syncthreads();                                    // prologue barrier (helper staged XE)
-    const int64_t t_loop = a.trace ? wall_clock64() : 0;
-    const int64_t c_loop = a.trace ? clock64() : 0;
-
-    double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
-    double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
-    for (int kc = kb; kc < wend; kc += kChunk) {
-        const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
-        frA[0] = fA0;
-        frA[1] = fA1;
-        frA[2] = fA2;
-        frB[0] = fB0;
-        frB[1] = fB1;
-        frB[2] = fB2;
-        const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
-        const unsigned frpA = FR + (unsigned)tid * 24 - (unsigned)rbA * 8;
-        const unsigned frpB = FR + (unsigned)(SLOTS + tid) * 24 - (unsigned)rbB * 8;
-        const int Tn = kc + kChunk < wend ? T : 0;
-        int rbAn, nrAn, rbBn, nrBn;
-        chunk_rows(tab, 0, kc + kChunk, A.G, Tn, rbAn, nrAn);
-        chunk_rows(tab, 0, kc + kChunk, B.G, Tn, rbBn, nrBn);
-        const double gA0 = a.F[(int64_t)clamp_row(rbAn, nrow) * ns + A.d];
-        const double gA1 = a.F[(int64_t)clamp_row(rbAn + 1, nrow) * ns + A.d];
-        const double gA2 = a.F[(int64_t)clamp_row(rbAn + 2, nrow) * ns + A.d];
-        const double gB0 = a.F[(int64_t)clamp_row(rbBn, nrow) * ns + B.d];
-        const double gB1 = a.F[(int64_t)clamp_row(rbBn + 1, nrow) * ns + B.d];
-        const double gB2 = a.F[(int64_t)clamp_row(rbBn + 2, nrow) * ns + B.d];
-        unsigned mA[kUpInline], mB[kUpInline];
+    int64_t t_loop = 0, c_loop = 0;
+    if constexpr (MEMB) {
+        // ---- member dataflow: tick k runs member e = k - G of each slot.  Per-member inputs
+        // (state, lateral inflow) are prefetched kRing ticks ahead into a register ring.
+        const int E = T;
+        const int64_t mS = a.mS;
+        constexpr int kRing = 4;
+        static_assert(kChunk % kRing == 0, "ring slots must be static in the unrolled chunk");
+        const double* __restrict__ Qm = a.Qm;
+        double2* __restrict__ IO = reinterpret_cast<double2*>(const_cast<double*>(a.IO));
+        double2 rA_[kRing], rB_[kRing];
+        double rQA[kRing], rQB[kRing];
 #pragma unroll
-        for (int u = 0; u < kUpInline; ++u) {
-            mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
-            mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
+        for (int r = 0; r < kRing; ++r) {
+            int eA = kb + r - A.G, eB = kb + r - B.G;
+            eA = eA < 0 ? 0 : (eA >= E ? E - 1 : eA);
+            eB = eB < 0 ? 0 : (eB >= E ? E - 1 : eB);
+            const int64_t pa = (int64_t)eA * mS + A.d, pb = (int64_t)eB * mS + B.d;
+            rA_[r] = IO[pa];
+            rQA[r] = Qm[pa];
+            rB_[r] = IO[pb];
+            rQB[r] = Qm[pb];
         }
-        const unsigned tpA = TAB + (unsigned)(kc - A.G) * 16u;
-        const unsigned tpB = TAB + (unsigned)(kc - B.G) * 16u;
-        double qA[kChunk], qB[kChunk];
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();                                // prologue barrier (helper staged XE)
+        t_loop = a.trace ? wall_clock64() : 0;
+        c_loop = a.trace ? clock64() : 0;
+        for (int kc = kb; kc < wend; kc += kChunk) {
+            const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;
+            unsigned mA[kUpInline], mB[kUpInline];
 #pragma unroll
-        for (int j = 0; j < kChunk; ++j) {
-            const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
-            const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
-            double aLo, aHi, bLo, bHi;
-            if (DENSE && slow) {
-                aLo = a.F[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
-                aHi = a.F[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
-                bLo = a.F[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
-                bHi = a.F[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
-            } else {
-                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
-                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
-                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
-                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
+            for (int u = 0; u < kUpInline; ++u) {
+                mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
+                mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
             }
-            const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
-            const double qa = (1.0 - fa) * aLo + fa * aHi;
-            const double qb = (1.0 - fb) * bLo + fb * bHi;
-            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
-            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
-        }
-        if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-            if (i & 1) {
+            for (int i = 0; i < kChunk; ++i) {
+                if (i & 1) {
 #pragma unroll
-                for (int u = 0; u < kUpInline; ++u) {
-                    mA[u] += A.uinc[u];
-                    mB[u] += B.uinc[u];
+                    for (int u = 0; u < kUpInline; ++u) {
+                        mA[u] += A.uinc[u];
+                        mB[u] += B.uinc[u];
+                    }
                 }
+                const unsigned rd = 8u * ((i + 1) & 1);
+                const int k = kc + i;
+                const int r = i % kRing;
+                const int eA = k - A.G, eB = k - B.G;
+                const bool actA = (unsigned)eA < (unsigned)E;
+                const bool actB = (unsigned)eB < (unsigned)E;
+                const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
+                const double rA =
+                    0.0 + (((A.al * IA + A.be * rA_[r].y) + A.ch * rA_[r].x) + A.ga * rQA[r]);
+                const double oA = A.psum ? IA : rA;
+                const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
+                const double rB =
+                    0.0 + (((B.al * IB + B.be * rB_[r].y) + B.ch * rB_[r].x) + B.ga * rQB[r]);
+                const double oB = B.psum ? IB : rB;
+                *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
+                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+                {   // refill this ring slot with the inputs of tick k + kRing
+                    int fA = k + kRing - A.G, fB = k + kRing - B.G;
+                    fA = fA < 0 ? 0 : (fA >= E ? E - 1 : fA);
+                    fB = fB < 0 ? 0 : (fB >= E ? E - 1 : fB);
+                    const int64_t pa = (int64_t)fA * mS + A.d, pb = (int64_t)fB * mS + B.d;
+                    rA_[r] = IO[pa];
+                    rQA[r] = Qm[pa];
+                    rB_[r] = IO[pb];
+                    rQB[r] = Qm[pb];
+                }
+                // the member's new state, in place of its inputs (read kRing ticks ago by this
+                // lane); launch_member_unpack forms the session state and output windows
+                if (actA)
+                    IO[(int64_t)eA * mS + A.d] = make_double2(A.routed || A.psum ? oA : 0.0, IA);
+                if (actB)
+                    IO[(int64_t)eB * mS + B.d] = make_double2(B.routed || B.psum ? oB : 0.0, IB);
+                if (A.xsrc && actA) {
+                    const uint64_t bits = (uint64_t)__double_as_longlong(oA);
+                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16),
+                                                           0, 16);
+                }
+                if (B.xsrc && actB) {
+                    const uint64_t bits = (uint64_t)__double_as_longlong(oB);
+                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16),
+                                                           0, 16);
+                }
+                __syncthreads();
             }
-            const unsigned rd = 8u * ((i + 1) & 1);
-            const int k = kc + i;
-            const bool actA = (unsigned)(k - A.G) < (unsigned)T;
-            const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
-            const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
-            const double oA = A.psum ? IA : rA;
-            const bool actB = (unsigned)(k - B.G) < (unsigned)T;
-            const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
-            const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
-            const double oB = B.psum ? IB : rB;
-            *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-            *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
-            A.op = actA ? oA : A.op;
-            A.ip = actA ? IA : A.ip;
-            B.op = actB ? oB : B.op;
-            B.ip = actB ? IB : B.ip;
-            const bool inwin = k >= gminw && k < wend;
-            double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
-            if (!MCR_EXP_NO_STORES) {
-                orow[tid] = A.routed ? oA : 0.0;
-                orow[SLOTS + tid] = B.routed ? oB : 0.0;
-            }
-            if (A.xsrc && actA) {
-                const uint64_t bits = (uint64_t)__double_as_longlong(oA);
-                const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16), 0, 16);
-            }
-            if (B.xsrc && actB) {
-                const uint64_t bits = (uint64_t)__double_as_longlong(oB);
-                const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
-            }
-            __syncthreads();
         }
-        rbA = rbAn;
-        nrA = nrAn;
-        rbB = rbBn;
-        nrB = nrBn;
-        fA0 = gA0;
-        fA1 = gA1;
-        fA2 = gA2;
-        fB0 = gB0;
-        fB1 = gB1;
-        fB2 = gB2;
+    } else {
+        int rbA, nrA, rbB, nrB;
+        chunk_rows(tab, 0, kb, A.G, T, rbA, nrA);
+        chunk_rows(tab, 0, kb, B.G, T, rbB, nrB);
+        double fA0 = a.F[(int64_t)clamp_row(rbA, nrow) * ns + A.d];
+        double fA1 = a.F[(int64_t)clamp_row(rbA + 1, nrow) * ns + A.d];
+        double fA2 = a.F[(int64_t)clamp_row(rbA + 2, nrow) * ns + A.d];
+        double fB0 = a.F[(int64_t)clamp_row(rbB, nrow) * ns + B.d];
+        double fB1 = a.F[(int64_t)clamp_row(rbB + 1, nrow) * ns + B.d];
+        double fB2 = a.F[(int64_t)clamp_row(rbB + 2, nrow) * ns + B.d];
+        __builtin_amdgcn_s_waitcnt(0);                      // nothing pending may enter the loop
+        __syncthreads();                                    // prologue barrier (helper staged XE)
+        t_loop = a.trace ? wall_clock64() : 0;
+        c_loop = a.trace ? clock64() : 0;
+
+        double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
+        double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
+        for (int kc = kb; kc < wend; kc += kChunk) {
+            const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
+            frA[0] = fA0;
+            frA[1] = fA1;
+            frA[2] = fA2;
+            frB[0] = fB0;
+            frB[1] = fB1;
+            frB[2] = fB2;
+            const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
+            const unsigned frpA = FR + (unsigned)tid * 24 - (unsigned)rbA * 8;
+            const unsigned frpB = FR + (unsigned)(SLOTS + tid) * 24 - (unsigned)rbB * 8;
+            const int Tn = kc + kChunk < wend ? T : 0;
+            int rbAn, nrAn, rbBn, nrBn;
+            chunk_rows(tab, 0, kc + kChunk, A.G, Tn, rbAn, nrAn);
+            chunk_rows(tab, 0, kc + kChunk, B.G, Tn, rbBn, nrBn);
+            const double gA0 = a.F[(int64_t)clamp_row(rbAn, nrow) * ns + A.d];
+            const double gA1 = a.F[(int64_t)clamp_row(rbAn + 1, nrow) * ns + A.d];
+            const double gA2 = a.F[(int64_t)clamp_row(rbAn + 2, nrow) * ns + A.d];
+            const double gB0 = a.F[(int64_t)clamp_row(rbBn, nrow) * ns + B.d];
+            const double gB1 = a.F[(int64_t)clamp_row(rbBn + 1, nrow) * ns + B.d];
+            const double gB2 = a.F[(int64_t)clamp_row(rbBn + 2, nrow) * ns + B.d];
+            unsigned mA[kUpInline], mB[kUpInline];
+    #pragma unroll
+            for (int u = 0; u < kUpInline; ++u) {
+                mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
+                mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
+            }
+            const unsigned tpA = TAB + (unsigned)(kc - A.G) * 16u;
+            const unsigned tpB = TAB + (unsigned)(kc - B.G) * 16u;
+            double qA[kChunk], qB[kChunk];
+    #pragma unroll
+            for (int j = 0; j < kChunk; ++j) {
+                const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
+                const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
+                double aLo, aHi, bLo, bHi;
+                if (DENSE && slow) {
+                    aLo = a.F[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
+                    aHi = a.F[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
+                    bLo = a.F[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
+                    bHi = a.F[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
+                } else {
+                    aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
+                    aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
+                    bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
+                    bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
+                }
+                const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
+                const double qa = (1.0 - fa) * aLo + fa * aHi;
+                const double qb = (1.0 - fb) * bLo + fb * bHi;
+                qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
+                qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
+            }
+            if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
+    #pragma unroll
+            for (int i = 0; i < kChunk; ++i) {
+                if (i & 1) {
+    #pragma unroll
+                    for (int u = 0; u < kUpInline; ++u) {
+                        mA[u] += A.uinc[u];
+                        mB[u] += B.uinc[u];
+                    }
+                }
+                const unsigned rd = 8u * ((i + 1) & 1);
+                const int k = kc + i;
+                const bool actA = (unsigned)(k - A.G) < (unsigned)T;
+                const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
+                const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
+                const double oA = A.psum ? IA : rA;
+                const bool actB = (unsigned)(k - B.G) < (unsigned)T;
+                const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
+                const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
+                const double oB = B.psum ? IB : rB;
+                *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
+                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+                A.op = actA ? oA : A.op;
+                A.ip = actA ? IA : A.ip;
+                B.op = actB ? oB : B.op;
+                B.ip = actB ? IB : B.ip;
+                const bool inwin = k >= gminw && k < wend;
+                double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
+                if (!MCR_EXP_NO_STORES) {
+                    orow[tid] = A.routed ? oA : 0.0;
+                    orow[SLOTS + tid] = B.routed ? oB : 0.0;
+                }
+                if (A.xsrc && actA) {
+                    const uint64_t bits = (uint64_t)__double_as_longlong(oA);
+                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16), 0, 16);
+                }
+                if (B.xsrc && actB) {
+                    const uint64_t bits = (uint64_t)__double_as_longlong(oB);
+                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
+                }
+                __syncthreads();
+            }
+            rbA = rbAn;
+            nrA = nrAn;
+            rbB = rbBn;
+            nrB = nrBn;
+            fA0 = gA0;
+            fA1 = gA1;
+            fA2 = gA2;
+            fB0 = gB0;
+            fB1 = gB1;
+            fB2 = gB2;
+        }
+        // session state after the horizon; never-processed reaches hold o = 0
+        a.st_o[A.d] = A.routed || A.psum ? A.op : 0.0;
+        a.st_i[A.d] = A.ip;
+        a.st_o[B.d] = B.routed || B.psum ? B.op : 0.0;
+        a.st_i[B.d] = B.ip;
     }
-    // session state after the horizon; never-processed reaches hold o = 0
-    a.st_o[A.d] = A.routed || A.psum ? A.op : 0.0;
-    a.st_i[A.d] = A.ip;
-    a.st_o[B.d] = B.routed || B.psum ? B.op : 0.0;
-    a.st_i[B.d] = B.ip;
     if (a.trace && tid == 0) {
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
         rec[0] = t_start;
@@ -374,21 +469,18 @@ void wavefront_flow(WaveArgs a) {
     }
 }
 
-template <bool DENSE>
+template <bool DENSE, bool MEMB>
 const void* flow_fn(int slots) {
     switch (slots) {
 #define MCR_CASE(S) \
-    case S: return reinterpret_cast<const void*>(&wavefront_flow<S, DENSE>);
+    case S: return reinterpret_cast<const void*>(&wavefront_flow<S, DENSE, MEMB>);
         MCR_SLOT_LIST_FLOW(MCR_CASE)
 #undef MCR_CASE
         default: return nullptr;
     }
 }
 
-}  // namespace
-
-hipError_t flow_occupancy(int slots, bool dense, size_t lds, int* blocks_per_cu) {
-    const void* fn = dense ? flow_fn<true>(slots) : flow_fn<false>(slots);
+hipError_t occupancy_of(const void* fn, int slots, size_t lds, int* blocks_per_cu) {
     if (!fn) return hipErrorInvalidValue;
     const int threads = slots + kHelperLanes;
     int api = 0;
@@ -409,12 +501,93 @@ hipError_t flow_occupancy(int slots, bool dense, size_t lds, int* blocks_per_cu)
     return hipSuccess;
 }
 
+// IO[e][d] = {o, i} of the session state, Qm[e][d] = the lateral inflow of member e at the step
+// (same expression as the tick loop)
+__global__ void member_inputs(const double* __restrict__ F, int64_t mF, int64_t ns, int n_rows,
+                              int4 ent, const double* __restrict__ st_o,
+                              const double* __restrict__ st_i, double2* __restrict__ IO,
+                              double* __restrict__ Qm, int64_t cnt) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= cnt) return;
+    const int64_t e = idx / ns, d = idx - e * ns;
+    IO[idx] = make_double2(st_o[idx], st_i[idx]);
+    const double* Fe = F + e * mF;
+    const double lo = Fe[(int64_t)clamp_row(ent.x, n_rows) * ns + d];
+    if (ent.y < 0) {
+        Qm[idx] = lo;
+        return;
+    }
+    const double hi = Fe[(int64_t)clamp_row(ent.y, n_rows) * ns + d];
+    const double f = __hiloint2double(ent.w, ent.z);
+    Qm[idx] = (1.0 - f) * lo + f * hi;
+}
+
+}  // namespace
+
+hipError_t flow_occupancy(int slots, bool dense, size_t lds, int* blocks_per_cu) {
+    return occupancy_of(dense ? flow_fn<true, false>(slots) : flow_fn<false, false>(slots), slots,
+                        lds, blocks_per_cu);
+}
+
+hipError_t flow_members_occupancy(int slots, size_t lds, int* blocks_per_cu) {
+    return occupancy_of(flow_fn<false, true>(slots), slots, lds, blocks_per_cu);
+}
+
 hipError_t launch_flow(const WaveArgs& a, int grid, int slots, size_t lds, bool dense,
                        hipStream_t s) {
-    const void* fn = dense ? flow_fn<true>(slots) : flow_fn<false>(slots);
+    const void* fn = dense ? flow_fn<true, false>(slots) : flow_fn<false, false>(slots);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<WaveArgs*>(&a)};
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);
+}
+
+hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, size_t lds,
+                               hipStream_t s) {
+    const void* fn = flow_fn<false, true>(slots);
+    if (!fn) return hipErrorInvalidValue;
+    void* args[] = {const_cast<WaveArgs*>(&a)};
+    return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);
+}
+
+// After a member-dataflow step: session state and T = 1 output windows from the IO pairs
+__global__ void member_unpack(const double2* __restrict__ IO, const uint8_t* __restrict__ flags,
+                              const int32_t* __restrict__ G, const int32_t* __restrict__ wg_gmin,
+                              const int64_t* __restrict__ wbase, int rs, double* __restrict__ O,
+                              int64_t mO, double* __restrict__ st_o, double* __restrict__ st_i,
+                              int64_t ns, int64_t cnt) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= cnt) return;
+    const int64_t e = idx / ns, d = idx - e * ns;
+    const uint8_t fl = flags[d];
+    if (fl == kSlotPad) return;
+    const double2 v = IO[idx];
+    st_o[idx] = v.x;
+    st_i[idx] = v.y;
+    const int64_t w = d / rs;
+    O[e * mO + wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * rs + (d - w * rs)] =
+        fl == kSlotRouted ? v.x : 0.0;
+}
+
+hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, const int32_t* G,
+                                const int32_t* wg_gmin, const int64_t* wbase, int rs, double* O,
+                                int64_t mO, double* st_o, double* st_i, int64_t ns, int64_t E,
+                                hipStream_t s) {
+    const int64_t cnt = ns * E;
+    if (cnt == 0) return hipSuccess;
+    hipLaunchKernelGGL(member_unpack, dim3((unsigned)((cnt + 255) / 256)), 256, 0, s,
+                       reinterpret_cast<const double2*>(IO), flags, G, wg_gmin, wbase, rs, O, mO,
+                       st_o, st_i, ns, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_rows, int4 ent,
+                                const double* st_o, const double* st_i, double* IO, double* Qm,
+                                int64_t E, hipStream_t s) {
+    const int64_t cnt = ns * E;
+    if (cnt == 0) return hipSuccess;
+    hipLaunchKernelGGL(member_inputs, dim3((unsigned)((cnt + 255) / 256)), 256, 0, s, F, mF, ns,
+                       n_rows, ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, cnt);
+    return hipGetLastError();
 }
 
 }  // namespace mcr

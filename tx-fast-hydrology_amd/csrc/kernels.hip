@@ -345,6 +345,27 @@ __device__ __forceinline__ double inflow_at(const double* __restrict__ O,
     return s;
 }
 
+// Session state after a one-step run, from its step-0 outputs: st_o[e][pos[j]] = o (0 for
+// reaches the walk never processes, as the outputs hold), st_i[e][pos[j]] = the inflow fold
+__global__ void state_from_step(const double* __restrict__ O, int64_t mO,
+                                const int64_t* __restrict__ jbase,
+                                const int64_t* __restrict__ in_off,
+                                const int64_t* __restrict__ in_list,
+                                const int64_t* __restrict__ pos, int slots,
+                                double* __restrict__ st_o, double* __restrict__ st_i, int64_t n,
+                                int64_t ns, int64_t E) {
+    const int64_t total = n * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = x / n;
+        const int64_t j = x - e * n;
+        const double* Oe = O + e * mO;
+        const int64_t d = e * ns + pos[j];
+        st_o[d] = Oe[jbase[j]];
+        st_i[d] = inflow_at(Oe, jbase, in_off, in_list, j, 0, slots);
+    }
+}
+
 // out[t - t0][j][e]: consecutive threads take consecutive (j, e) (coalesced writes)
 __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
                              const int64_t* __restrict__ jbase,
@@ -441,6 +462,16 @@ hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32
     if (n > 0)
         hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
                            slots, n, jbase);
+    return hipGetLastError();
+}
+
+hipError_t launch_state_from_step(const double* O, int64_t mO, const int64_t* jbase,
+                                  const int64_t* in_off, const int64_t* in_list,
+                                  const int64_t* pos, int slots, double* st_o, double* st_i,
+                                  int64_t n, int64_t nslots, int64_t E, hipStream_t s) {
+    if (n * E == 0) return hipSuccess;
+    hipLaunchKernelGGL(state_from_step, grid_for(n * E, 256), 256, 0, s, O, mO, jbase, in_off,
+                       in_list, pos, slots, st_o, st_i, n, nslots, E);
     return hipGetLastError();
 }
 

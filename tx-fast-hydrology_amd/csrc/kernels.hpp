@@ -77,6 +77,8 @@ struct WaveArgs {
     uint32_t xg_bytes;            // size of XG in bytes (< 2^31)
     uint32_t epoch;               // tag of this run's granules (never 0)
     int32_t* status;              // set to 1 when a wait gave up
+    const double* Qm;             // member dataflow: lateral inflow [E][nslots] of the step
+    const double* IO;             // member dataflow: state {o, i} [E][nslots][2]
     int64_t nslots;
     int32_t n_rows;
     int32_t T;
@@ -103,6 +105,34 @@ hipError_t launch_flow(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
                        hipStream_t s);
 // Resident workgroups per CU of the dataflow kernel at this LDS size.
 hipError_t flow_occupancy(int slots, bool dense, size_t lds_bytes, int* blocks_per_cu);
+
+// Member dataflow (flow.hip): ONE step of E ensemble members as one resident launch.  Member e
+// of node slot d runs at tick G[d] + e (the members take the place of the steps of a horizon;
+// a.T = E), reading its state from a.IO and its lateral inflow from a.Qm (launch_member_inputs)
+// and writing the member's step-0 outputs into the T = 1 output windows (member stride a.mO);
+// the new session state is then formed from those outputs (launch_state_from_step).
+hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
+                               hipStream_t s);
+hipError_t flow_members_occupancy(int slots, size_t lds_bytes, int* blocks_per_cu);
+// Inputs of a member-dataflow step, member-major [E][nslots]: IO = {o, i} of the session state
+// (16 B per slot, one load per slot and tick) and Qm = the step's interpolated lateral inflow of
+// the member (the kernels' formula: F[e][lo][d] when ent.y < 0, else
+// (1 - frac) F[e][lo][d] + frac F[e][hi][d]).
+hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t nslots, int n_rows,
+                                int4 ent, const double* st_o, const double* st_i, double* IO,
+                                double* Qm, int64_t E, hipStream_t s);
+// After a member-dataflow step (which leaves each member's new {o, i} in IO): the session state
+// st_o / st_i and the T = 1 output windows O (member stride mO, row width rs).
+hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, const int32_t* G,
+                                const int32_t* wg_gmin, const int64_t* wbase, int rs, double* O,
+                                int64_t mO, double* st_o, double* st_i, int64_t nslots, int64_t E,
+                                hipStream_t s);
+// Session state after a one-step run from its step-0 outputs:
+// st_o[e][pos[j]] = O, st_i[e][pos[j]] = the inflow fold of j (as the output gathers compute it)
+hipError_t launch_state_from_step(const double* O, int64_t mO, const int64_t* jbase,
+                                  const int64_t* in_off, const int64_t* in_list,
+                                  const int64_t* pos, int slots, double* st_o, double* st_i,
+                                  int64_t n, int64_t nslots, int64_t E, hipStream_t s);
 
 // dense: the step table has a kChunk-step window spanning more than 3 forcing rows.
 // members: ensemble members (grid y); member strides are in `a`.
