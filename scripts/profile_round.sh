@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU-box profiling session for the committed profiles/ summaries:
-#   kernel-trace stats of the det / ensemble / EnKF bench workloads, HBM traffic (two PMC passes)
+#   kernel-trace stats of the det / ensemble / EnKF bench workloads and of the full-covariance
+#   KF (scripts/bench_kf.py), HBM traffic (two PMC passes)
 #   and SQ timing counters of the det workload.  Usage: bash scripts/profile_round.sh <tag>
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -19,7 +20,9 @@ stats() {   # name, bench args
 }
 stats det --steps 5 --warmup 1
 stats ens64 --steps 2 --warmup 1 --members 64
-stats enkf32 --steps 1 --warmup 1 --members 32 --enkf
+stats enkf32 --steps 1 --warmup 1 --members 32 --enkf --slots 384
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$O/prof_kf" -o run \
+    -- python3 "$PWD/scripts/bench_kf.py" --no-cpu --steps 1 > $O/prof_kf.log 2>&1 || exit $?
 BENCH_ARGS="" bash scripts/gpu_pmc.sh ${TAG}_hbm FETCH_SIZE WRITE_SIZE || exit $?
 bash scripts/gpu_pmc.sh ${TAG}_sq "SQ_WAVES SQ_WAVE_CYCLES" "SQ_BUSY_CYCLES SQ_WAIT_ANY" \
     "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
