@@ -110,72 +110,86 @@ class AsyncSimulation(Simulation):
 
     async def _simulate(self, taskgroup, model, inputs, name):
         logger.debug(f"Started job for sub-watershed {name}")
-        series = {model.datetime: model.o_t_next}
-        for state in model.simulate_iter(inputs):
-            series[state.datetime] = state.o_t_next
-        outputs = pd.DataFrame.from_dict(series, orient="index")
-        outputs.index = pd.to_datetime(outputs.index, utc=True)
-        outputs.columns = inputs.columns
-        self.outputs[name] = outputs
-        taskgroup.create_task(self._accumulate(taskgroup, outputs, name))
+        self.outputs[name] = _outflow_frame(model, inputs)
+        taskgroup.create_task(self._accumulate(taskgroup, self.outputs[name], name))
 
     async def _accumulate(self, taskgroup, outputs, name):
+        """Fold this sub-basin's outlet series into every downstream sub-basin's inputs and
+        start each downstream sub-basin whose last upstream this was."""
         upstream = self.models[name]
         for link in upstream.sinks:
-            downstream = link.downstream_model
-            target = downstream.name
+            target = link.downstream_model.name
             if target == name:
                 continue
-            inputs = self.inputs[target]
-            reach_out = upstream.reach_ids[link.upstream_index]
-            reach_in = downstream.reach_ids[link.downstream_index]
-            i_prev = outputs[reach_out].shift(1).iloc[1:].fillna(0.0)
-            i_next = outputs[reach_out].iloc[1:]
-            j = link.downstream_index
-            gamma, alpha, beta = downstream.gamma[j], downstream.alpha[j], downstream.beta[j]
-            # same expression and association as simulation.py:158-159
-            inputs.loc[:, reach_in] += (alpha * i_next.values / gamma
-                                        + beta * i_prev.values / gamma)
+            frame = self.inputs[target]
+            column = link.downstream_model.reach_ids[link.downstream_index]
+            series = outputs[upstream.reach_ids[link.upstream_index]]
+            frame.loc[:, column] += _lateral_correction(link.downstream_model,
+                                                        link.downstream_index, series)
             self._indegree[target] -= 1
-            if self._indegree[target] == 0:
-                taskgroup.create_task(self._simulate(taskgroup, downstream, inputs, target))
+            if not self._indegree[target]:
+                taskgroup.create_task(self._simulate(taskgroup, link.downstream_model, frame,
+                                                     target))
         logger.debug(f"Finished job for sub-watershed {name}")
 
 
+def _outflow_frame(model, inputs):
+    """Route ``model`` over its input frame; outflows per timestamp, start time included."""
+    rows = {model.datetime: model.o_t_next}
+    rows.update((state.datetime, state.o_t_next) for state in model.simulate_iter(inputs))
+    frame = pd.DataFrame.from_dict(rows, orient="index")
+    frame.index = pd.to_datetime(frame.index, utc=True)
+    frame.columns = inputs.columns
+    return frame
+
+
+def _lateral_correction(model, j, series):
+    """Inflow of an upstream outlet series expressed as lateral input of entry reach j:
+    alpha I(t) / gamma + beta I(t-1) / gamma with I(t0 - dt) = 0 (simulation.py:152-159, same
+    expression and association)."""
+    now = series.iloc[1:].values
+    before = series.shift(1).iloc[1:].fillna(0.0).values
+    return model.alpha[j] * now / model.gamma[j] + model.beta[j] * before / model.gamma[j]
+
+
 class CheckPoint(BaseCallback):
-    """Save the model state (and the ``save_state`` of every other callback) once, at the
-    first step end at or after ``checkpoint_time`` (or ``timedelta`` seconds after the
-    simulation start)."""
+    """Saves the model state once, at the first step end at or after the checkpoint time, and
+    forwards save / load to every bound callback that keeps state (``save_state`` /
+    ``load_state``).  ``timedelta`` (seconds) re-arms the checkpoint at each simulation start,
+    relative to the model time then."""
 
     def __init__(self, model, checkpoint_time=None, timedelta=None):
+        if checkpoint_time is None and timedelta is None:
+            raise ValueError("Either `checkpoint_time` or `timedelta` must not be `None`.")
         self.model = model
-        if checkpoint_time is None:
-            if timedelta is None:
-                raise ValueError("Either `checkpoint_time` or `timedelta` must not be `None`.")
-            checkpoint_time = model.datetime + datetime.timedelta(seconds=timedelta)
-        self.checkpoint_time = checkpoint_time
         self.timedelta = timedelta
+        self.checkpoint_time = (checkpoint_time if checkpoint_time is not None
+                                else self._offset(timedelta))
         self.model_saved = False
 
+    def _offset(self, seconds):
+        return self.model.datetime + datetime.timedelta(seconds=seconds)
+
     def __on_simulation_start__(self):
-        if self.timedelta is None:
-            return None
-        self.set_checkpoint(self.model.datetime + datetime.timedelta(seconds=self.timedelta))
+        if self.timedelta is not None:
+            self.set_checkpoint(self._offset(self.timedelta))
 
     def __on_step_end__(self):
-        if self.model.datetime >= self.checkpoint_time and not self.model_saved:
+        if not self.model_saved and self.model.datetime >= self.checkpoint_time:
             self.model.save_state()
             self.model_saved = True
 
-    def __on_save_state__(self):
+    def _forward(self, method):
         for callback in self.model.callbacks.values():
-            if hasattr(callback, "save_state"):
-                callback.save_state()
+            hook = getattr(callback, method, None)
+            if hook is not None:
+                hook()
+
+    def __on_save_state__(self):
+        self._forward("save_state")
 
     def __on_load_state__(self):
-        for callback in self.model.callbacks.values():
-            if hasattr(callback, "load_state"):
-                callback.load_state()
+        self._forward("load_state")
 
     def __idle_steps__(self):
         return self.model_saved
