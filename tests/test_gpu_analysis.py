@@ -165,7 +165,7 @@ def test_staged_driver_single_rank_equals_enkf_analysis():
     a.enkf_analysis(s, Y, R)
     b, _, _ = _net(end, members=E)
     b.set_state(X, I0)
-    ensemble.distributed_analysis(b, s, Y, R, device=torch.device("cuda", 0))
+    ensemble.distributed_analysis(b, s, Y, R, device=torch.device("cuda", 0), staged=True)
     oa, ia = a.get_state()
     ob, ib = b.get_state()
     assert np.array_equal(oa, ob) and np.array_equal(ia, ib)
