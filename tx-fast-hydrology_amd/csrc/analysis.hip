@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace mcr {
 
 namespace {
@@ -27,12 +29,15 @@ constexpr int kPad = 1;     // LDS row padding (f64)
 
 // C = alpha op(A) op(B) + beta C, column-major, op = transpose when TA / TB.
 // op(A) is M x K, op(B) is K x N.  beta == 0 never reads C.
+// Split-K (gridDim.z > 1): slice z covers k in [z * kc, (z + 1) * kc) and writes its raw
+// partial product to C + z * ldc * N (alpha = 1, beta = 0 passed by the launcher); splitk_reduce
+// sums the slices in order (deterministic).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
                                                   const double* __restrict__ A, int64_t lda,
                                                   const double* __restrict__ B, int64_t ldb,
                                                   double beta, double* __restrict__ C,
-                                                  int64_t ldc) {
+                                                  int64_t ldc, int64_t kc) {
     __shared__ double As[kBK][kTile + kPad];   // As[k][i] = op(A)(row0 + i, k0 + k)
     __shared__ double Bs[kBK][kTile + kPad];   // Bs[k][j] = op(B)(k0 + k, col0 + j)
     const int tid = threadIdx.x;
@@ -47,7 +52,10 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
 
-    for (int64_t k0 = 0; k0 < K; k0 += kBK) {
+    const int64_t kbeg = (int64_t)blockIdx.z * kc;
+    const int64_t kend = kbeg + kc < K ? kbeg + kc : K;
+    C += (int64_t)blockIdx.z * ldc * N;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += kBK) {
 #pragma unroll
         for (int r = 0; r < (kTile * kBK) / 256; ++r) {
             const int idx = tid + 256 * r;
@@ -56,13 +64,13 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
             if (TA) { k = idx % kBK; i = idx / kBK; } else { i = idx % kTile; k = idx / kTile; }
             const int64_t gi = row0 + i, gk = k0 + k;
             double v = 0.0;
-            if (gi < M && gk < K) v = TA ? A[gk + gi * lda] : A[gi + gk * lda];
+            if (gi < M && gk < kend) v = TA ? A[gk + gi * lda] : A[gi + gk * lda];
             As[k][i] = v;
             int j;
             if (TB) { j = idx % kTile; k = idx / kTile; } else { k = idx % kBK; j = idx / kBK; }
             const int64_t gj = col0 + j, gk2 = k0 + k;
             double w = 0.0;
-            if (gj < N && gk2 < K) w = TB ? B[gj + gk2 * ldb] : B[gk2 + gj * ldb];
+            if (gj < N && gk2 < kend) w = TB ? B[gj + gk2 * ldb] : B[gk2 + gj * ldb];
             Bs[k][j] = w;
         }
         __syncthreads();
@@ -95,6 +103,18 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
                     *c = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *c;
                 }
             }
+}
+
+// C = alpha * (W[0] + W[1] + ... + W[splits-1]) + beta * C  (W[z]: M x N, leading dim M)
+__global__ void splitk_reduce(const double* __restrict__ W, int splits, int64_t M, int64_t N,
+                              double alpha, double beta, double* __restrict__ C, int64_t ldc) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= M * N) return;
+    const int64_t i = idx % M, j = idx / M;
+    double acc = W[idx];
+    for (int z = 1; z < splits; ++z) acc += W[(int64_t)z * M * N + idx];
+    double* c = C + i + j * ldc;
+    *c = beta == 0.0 ? alpha * acc : alpha * acc + beta * *c;
 }
 
 // U[g + e m] = HA[g + e m] / r[g]  (R^-1 HA for a diagonal R)
@@ -232,25 +252,45 @@ inline int grid_for(int64_t work, int block) {
 
 }  // namespace
 
+namespace {
+
+template <bool TA, bool TB>
+void dgemm_go(dim3 grid, hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha,
+              const double* A, int64_t lda, const double* B, int64_t ldb, double beta, double* C,
+              int64_t ldc, int64_t kc) {
+    hipLaunchKernelGGL((dgemm_mfma<TA, TB>), grid, 256, 0, s, M, N, K, alpha, A, lda, B, ldb,
+                       beta, C, ldc, kc);
+}
+
+}  // namespace
+
 hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha,
                         const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
-                        double* C, int64_t ldc, hipStream_t s) {
+                        double* C, int64_t ldc, hipStream_t s, double* work, size_t work_elems) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    if ((M + kTile - 1) / kTile > 0x7fffffff || (N + kTile - 1) / kTile > 65535)
-        return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((M + kTile - 1) / kTile), (unsigned)((N + kTile - 1) / kTile));
-    if (!ta && !tb)
-        hipLaunchKernelGGL((dgemm_mfma<false, false>), grid, 256, 0, s, M, N, K, alpha, A, lda,
-                           B, ldb, beta, C, ldc);
-    else if (!ta && tb)
-        hipLaunchKernelGGL((dgemm_mfma<false, true>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
-                           ldb, beta, C, ldc);
-    else if (ta && !tb)
-        hipLaunchKernelGGL((dgemm_mfma<true, false>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
-                           ldb, beta, C, ldc);
-    else
-        hipLaunchKernelGGL((dgemm_mfma<true, true>), grid, 256, 0, s, M, N, K, alpha, A, lda, B,
-                           ldb, beta, C, ldc);
+    const int64_t gm = (M + kTile - 1) / kTile, gn = (N + kTile - 1) / kTile;
+    if (gm > 0x7fffffff || gn > 65535) return hipErrorInvalidValue;
+    // few output tiles and a deep reduction (the E x E products of the analysis, K = gauges):
+    // split K over workgroups into the workspace, then reduce the slices in order
+    int splits = 1;
+    if (work && gm * gn < 64 && K >= 8 * kBK) {
+        splits = (int)std::min<int64_t>(std::min<int64_t>(256 / (gm * gn), K / (4 * kBK)), 64);
+        while (splits > 1 && (size_t)splits * M * N > work_elems) --splits;
+    }
+    const int64_t kc = splits > 1 ? ((K + splits - 1) / splits + kBK - 1) / kBK * kBK : K;
+    if (splits > 1) splits = (int)((K + kc - 1) / kc);
+    const dim3 grid((unsigned)gm, (unsigned)gn, (unsigned)splits);
+    double* out = splits > 1 ? work : C;
+    const double a = splits > 1 ? 1.0 : alpha, b = splits > 1 ? 0.0 : beta;
+    const int64_t ld = splits > 1 ? M : ldc;
+    if (!ta && !tb) dgemm_go<false, false>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
+    else if (!ta && tb) dgemm_go<false, true>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
+    else if (ta && !tb) dgemm_go<true, false>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
+    else dgemm_go<true, true>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || splits == 1) return e;
+    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), 256, 0, s, work,
+                       splits, M, N, alpha, beta, C, ldc);
     return hipGetLastError();
 }
 

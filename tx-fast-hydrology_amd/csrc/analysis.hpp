@@ -9,9 +9,12 @@
 namespace mcr {
 
 // C = alpha op(A) op(B) + beta C  (op = transpose when ta / tb; op(A) M x K, op(B) K x N)
+// work (optional, work_elems doubles): lets a GEMM with few output tiles and a deep K split K
+// over workgroups (partial products in work, reduced in slice order: deterministic)
 hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha,
                         const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
-                        double* C, int64_t ldc, hipStream_t s);
+                        double* C, int64_t ldc, hipStream_t s, double* work = nullptr,
+                        size_t work_elems = 0);
 // ensemble mean over members and anomalies A = X - mean (both [E][ns])
 // U = R^-1 HA for a diagonal R (r = its diagonal), column-major m x E
 hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64_t m, int64_t E,

@@ -130,7 +130,7 @@ struct Net {
     int64_t E = 1;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
-    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, Rd, Ub, Mb;
+    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, Rd, Ub, Mb, Wk;   // Wk: split-K slices
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
     rocblas_handle blas = nullptr;
@@ -461,8 +461,9 @@ struct Net {
             HIPC(mcr::launch_scale_rows(HA.p, Rd.p, Ub.p, m, Et, stream));
             Mb.reserve((size_t)(Et * Et));
             HIPC(mcr::launch_set_identity(Mb.p, Et, stream));
+            Wk.reserve((size_t)(64 * Et * Et));
             HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Ub.p, m, 1.0, Mb.p, Et,
-                                   stream));
+                                   stream, Wk.p, Wk.cap));
             if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)Et, Mb.p,
                                  (rocblas_int)Et, info.p) != rocblas_status_success)
                 throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
@@ -470,7 +471,7 @@ struct Net {
                                 stream));
             info_pending = true;
             HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p, Et,
-                                   stream));
+                                   stream, Wk.p, Wk.cap));
             if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)Et, (rocblas_int)Et,
                                  Mb.p, (rocblas_int)Et, Zn.p, (rocblas_int)Et) !=
                 rocblas_status_success)
@@ -495,8 +496,9 @@ struct Net {
                                  C2.p, (rocblas_int)m, Dn.p, (rocblas_int)m) !=
                 rocblas_status_success)
                 throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+            Wk.reserve((size_t)(64 * Et * Et));
             HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, Et,
-                                   stream));
+                                   stream, Wk.p, Wk.cap));
         }
         // slice anomalies and increments G = A Z  (= K D per member)
         An.reserve((size_t)(S * Et));
