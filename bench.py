@@ -67,12 +67,15 @@ def parse():
     return apply_presets(ap.parse_args())
 
 
-def measured_traffic(info, n, T):
+def measured_traffic(info, n, T, E=1):
     """HBM bytes per launch of the routing kernel measured with rocprofv3 PMC counters for this
     exact workload (scripts/hbm_traffic.py -> profiles/*_hbm_traffic.json), newest first."""
     import glob
     want = {"slots": info["slots"], "tile": info["tile"], "n": n, "T": T}
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
+    if E > 1:
+        want["E"] = E
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic*.json")),
+                    reverse=True):
         try:
             rec = json.load(open(f))
         except (OSError, ValueError):
@@ -285,11 +288,14 @@ def main():
     per_unit = BYTES_PER_UNIT if E == 1 else 40.0 + 32.0 / E
     bytes_per_launch = per_unit * n * E * args.T * args.timing_runs / max(tm["launches"], 1)
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-    traffic = measured_traffic(info, n, args.T) if E == 1 else None
+    traffic = measured_traffic(info, n, args.T, E) if wl.enkf is None else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
                 "traffic_source": traffic["file"] if traffic else None,
+                # measured HBM bytes per launch / launch time: the DRAM rate the kernel drives
+                "traffic_gbs": (round(traffic["traffic_bytes_per_launch"] / (launch_ms * 1e-3)
+                                      / 1e9, 3) if traffic else None),
                 "kernel": "wavefront_flow" if net.mode()[1] == "dataflow" else "wavefront_det",
                 "launches_per_step": tm["launches"] / args.timing_runs,
                 "avg_launch_us": round(launch_ms * 1e3, 3),

@@ -167,3 +167,34 @@ def test_member_dataflow_matches_launches_path():
     for (a_o, a_i), (b_o, b_i) in zip(res[0][0], res[1][0]):
         assert np.array_equal(a_o, b_o) and np.array_equal(a_i, b_i)
     assert all(np.array_equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+def test_conus_scale_ensemble_members_bitexact():
+    """Maximum size (BASELINE configs[4] network: 2.7M reaches, 4000 outlets, deepest path ~7000
+    reaches, a schedule over thousands of workgroups): a 4-member, 24-step horizon on the
+    multi-launch path; every member's final state and last-step outputs bit-identical to its
+    serial oracle run."""
+    E, T = 4, 24
+    end = synthetic.river_network(2_700_000, 4000, 7000, np.random.default_rng(44))
+    n = end.size
+    start = np.arange(n)
+    indeg = orc.compute_indegree(start, end)
+    K, X, _ = synthetic.model_arrays(n, seed=44)
+    coef = orc.muskingum_coeffs(K, X, 300.0)
+    xp, fpe, o0 = _members(n, E, 3, 45)
+    i0 = np.stack([orc.init_inflows(start, end, o0[:, e]) for e in range(E)], axis=1)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=256, members=E)
+    assert net.info["nwg"] > 1000
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fpe)
+    net.run(x)
+    assert net.mode()[1] == "launches"
+    so, si = net.get_state()
+    last_o, last_i = net.fetch_outputs(T - 1, T)
+    for e in range(E):
+        _, _, fo, fi = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                    np.ascontiguousarray(fpe[:, :, e]), keep_outputs=False)
+        assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
+        assert np.array_equal(last_o[0, :, e], fo) and np.array_equal(last_i[0, :, e], fi), e
