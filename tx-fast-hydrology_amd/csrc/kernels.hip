@@ -244,8 +244,13 @@ void wavefront_det(WaveArgs a) {
             const bool inwin = k >= gminw && k < wend;
             double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
             if (!MCR_EXP_NO_STORES) {
+                #if MCR_NT_STORES
+                __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + tid);
+                __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + tid);
+#else
                 orow[tid] = A.routed ? oA : 0.0;
                 orow[SLOTS + tid] = B.routed ? oB : 0.0;
+#endif
                 if (A.xsrc && actA) XSm[A.xs0 + k] = oA;
                 if (B.xsrc && actB) XSm[B.xs0 + k] = oB;
             }

@@ -13,6 +13,10 @@
 // index j (jbase is computed per horizon by launch_window_index).
 #pragma once
 
+#ifndef MCR_NT_STORES
+#define MCR_NT_STORES 1   // output rows as non-temporal (streaming) stores
+#endif
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
