@@ -31,6 +31,9 @@
 #ifndef MCR_NT_MEMB
 #define MCR_NT_MEMB 0            // member dataflow: new states as non-temporal stores
 #endif
+#ifndef MCR_HELPER_SIMD
+#define MCR_HELPER_SIMD 0        // 1: helper = wave 3 (alone on SIMD 3 below 8 waves); measured slower
+#endif
 #ifndef MCR_HOIST
 #define MCR_HOIST 0              // read both slots' inputs right after the tick barrier
 #endif
@@ -198,9 +201,14 @@ void wavefront_flow(WaveArgs a) {
         reinterpret_cast<int*>(lds + EG)[idx] = a.ext_g[e0 + idx];
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;
 
-    if (tid >= SLOTS) {
+    // Waves go round-robin over the 4 SIMDs.  The helper takes wave index 3 (the last wave when
+    // the group has <= 4), so with fewer than 8 waves it has SIMD 3 to itself and its polling
+    // and staging never take issue cycles from a compute wave.
+    constexpr int kHW = MCR_HELPER_SIMD ? (SLOTS / 64 < 3 ? SLOTS / 64 : 3) : SLOTS / 64;
+    const int wave = tid >> 6;
+    if (wave == kHW) {
         // ================================ helper wave ================================
-        Helper h{lds, xg, XE, XSLOT, EG, tid - SLOTS, e0, next * kChunk, T, a.epoch, a.status,
+        Helper h{lds, xg, XE, XSLOT, EG, tid & 63, e0, next * kChunk, T, a.epoch, a.status,
                  false};
         const int nb = (h.nitems + kBatchItems - 1) / kBatchItems;   // <= 2 (host-checked)
         __builtin_amdgcn_s_waitcnt(0);
@@ -235,15 +243,16 @@ void wavefront_flow(WaveArgs a) {
     }
 
     // ================================ compute waves ================================
+    const int lid = wave < kHW ? tid : tid - 64;        // lane id over the compute waves
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
     const int64_t wb = a.wbase[w];
     Slot A, B;                                          // every real slot runs steps 0 .. T-1
-    load_slot(A, a, (int64_t)w * RS + tid, 0, kb, wend - kb, T);
-    load_slot(B, a, (int64_t)w * RS + SLOTS + tid, 0, kb, wend - kb, T);
+    load_slot(A, a, (int64_t)w * RS + lid, 0, kb, wend - kb, T);
+    load_slot(B, a, (int64_t)w * RS + SLOTS + lid, 0, kb, wend - kb, T);
     const uint64_t up4A = a.up4[A.d], up4B = a.up4[B.d];
-    xbp[tid * 2 + ((kb - 1) & 1)] = A.op;
-    xbp[(SLOTS + tid) * 2 + ((kb - 1) & 1)] = B.op;
+    xbp[lid * 2 + ((kb - 1) & 1)] = A.op;
+    xbp[(SLOTS + lid) * 2 + ((kb - 1) & 1)] = B.op;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();                                    // LDS tables staged
 
@@ -251,7 +260,7 @@ void wavefront_flow(WaveArgs a) {
     decode_codes<RS>(B, up4B, XB, XE, kChunk * 8);
     const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);
     const bool any3AB = any3A || any3B;
-    const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
+    const unsigned ownA = XB + (unsigned)lid * 16, ownB = XB + (unsigned)(SLOTS + lid) * 16;
 
     const unsigned epoch = a.epoch;
     int64_t t_loop = 0, c_loop = 0;
@@ -379,8 +388,8 @@ void wavefront_flow(WaveArgs a) {
         t_loop = a.trace ? wall_clock64() : 0;
         c_loop = a.trace ? clock64() : 0;
 
-        double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
-        double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
+        double* frA = reinterpret_cast<double*>(lds + FR) + lid * 3;
+        double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + lid) * 3;
         for (int kc = kb; kc < wend; kc += kChunk) {
             const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
             frA[0] = fA0;
@@ -390,8 +399,8 @@ void wavefront_flow(WaveArgs a) {
             frB[1] = fB1;
             frB[2] = fB2;
             const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
-            const unsigned frpA = FR + (unsigned)tid * 24 - (unsigned)rbA * 8;
-            const unsigned frpB = FR + (unsigned)(SLOTS + tid) * 24 - (unsigned)rbB * 8;
+            const unsigned frpA = FR + (unsigned)lid * 24 - (unsigned)rbA * 8;
+            const unsigned frpB = FR + (unsigned)(SLOTS + lid) * 24 - (unsigned)rbB * 8;
             const int Tn = kc + kChunk < wend ? T : 0;
             int rbAn, nrAn, rbBn, nrBn;
             chunk_rows(tab, 0, kc + kChunk, A.G, Tn, rbAn, nrAn);
@@ -473,11 +482,11 @@ void wavefront_flow(WaveArgs a) {
                 double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
                 if (!MCR_EXP_NO_STORES) {
                     #if MCR_NT_STORES
-                    __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + tid);
-                    __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + tid);
+                    __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
+                    __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
 #else
-                    orow[tid] = A.routed ? oA : 0.0;
-                    orow[SLOTS + tid] = B.routed ? oB : 0.0;
+                    orow[lid] = A.routed ? oA : 0.0;
+                    orow[SLOTS + lid] = B.routed ? oB : 0.0;
 #endif
                 }
                 if (A.xsrc && actA) {
