@@ -56,6 +56,8 @@ def parse():
                          "2 h (hourly gauge observations)")
     ap.add_argument("--gauges", type=int, default=500)
     ap.add_argument("--obs-hours", type=float, default=2.0)
+    ap.add_argument("--one-plan", action="store_true",
+                    help="EnKF: route the forecast on the analysis plan too (no hand-over)")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--conus", action="store_true",
                     help="BASELINE configs[4]: CONUS NWM-scale synthetic network (2.7M reaches, "
@@ -156,6 +158,13 @@ def build_workload(args, rank=0, world=1):
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
+    if enkf is not None and not args.one_plan:
+        # the forecast after the last analysis runs on its own plan (256 lanes, 64-tick
+        # launches: the multi-launch ensemble shape), the state handed over on the device
+        fnet = engine.RoutingNet(end, indeg, heads, slots=256, tile=64, members=E)
+        fnet.set_coeffs(alpha, beta, chi, gamma)
+        fnet.load_forcing(xp, fp)
+        enkf.fnet = fnet
     w = SimpleNamespace(n=n, start=start, end=end, indeg=indeg, alpha=alpha, beta=beta, chi=chi,
                         gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt, E=E,
                         enkf=enkf)
@@ -249,7 +258,12 @@ def main():
         for k in range(ek.n_an):       # analysis at every model step while obs exist
             net.run(x[k:k + 1])
             ensemble.distributed_analysis(net, ek.gauges, ek.Y[k], ek.R)
-        net.run(x[ek.n_an:])
+        if getattr(ek, "fnet", None) is None:
+            net.run(x[ek.n_an:])
+            return
+        ek.fnet.copy_state_from(net)
+        ek.fnet.run(x[ek.n_an:])
+        net.copy_state_from(ek.fnet)
     info = net.info
     setup_s = time.time() - t_setup
 
@@ -280,13 +294,19 @@ def main():
     value = units / elapsed
 
     # ---- roofline of the dominant kernel (HIP events around every wavefront launch) --------
-    net.reset_timing()
-    net.set_timing(True)
+    nets = [net] + ([wl.enkf.fnet] if getattr(wl.enkf, "fnet", None) is not None else [])
+    for nt in nets:
+        nt.reset_timing()
+        nt.set_timing(True)
     for _ in range(args.timing_runs):
         horizon()
-    net.synchronize()
-    tm = net.timing()
-    net.set_timing(False)
+    tm = {"kernel_ms": 0.0, "launches": 0}
+    for nt in nets:
+        nt.synchronize()
+        t_ = nt.timing()
+        tm["kernel_ms"] += t_["kernel_ms"]
+        tm["launches"] += t_["launches"]
+        nt.set_timing(False)
     launch_ms = tm["kernel_ms"] / max(tm["launches"], 1)
     # 72 B per reach·timestep deterministic, 40 + 32/E per reach·member·timestep
     per_unit = BYTES_PER_UNIT if E == 1 else 40.0 + 32.0 / E

@@ -163,6 +163,11 @@ int mc_set_coeffs(void* net, const double* alpha, const double* beta, const doub
 /* State (o_t_next, i_t_next) of the model, caller order. */
 int mc_set_state(void* net, const double* o_t_next, const double* i_t_next);
 int mc_get_state(void* net, double* o_t_next, double* i_t_next);
+/* Device-to-device state hand-over between two sessions of the SAME network (e.g. plans with
+ * different lane / launch shapes for different run lengths): dst's (o, i) := src's, member by
+ * member, reach by reach (bit copy).  Ordered after src's pending work on dst's stream; src's
+ * later work waits for the copy.  Replaces mc_get_state + mc_set_state through the host. */
+int mc_net_copy_state(void* dst_net, const void* src_net);
 
 /* One timestep with lateral inflow q (muskingum.py:435-465 -> nutils.py:64-89).  If o_prev and
  * i_prev are non-NULL they replace the session state first.  Writes the new (i, o) and keeps

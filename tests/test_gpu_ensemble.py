@@ -169,6 +169,39 @@ def test_member_dataflow_matches_launches_path():
     assert all(np.array_equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 
 
+def test_copy_state_between_plans_continues_bitexact():
+    """mc_net_copy_state: one-step runs on a 384-lane plan (member dataflow), the hand-over to a
+    256-lane 64-tick plan for the rest of the horizon, and back: identical to the serial runs."""
+    E = 12
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(6000, 5, 150, 71, E)
+    heads = start[indeg == 0]
+    a = engine.RoutingNet(end, indeg, heads, slots=384, members=E)
+    b = engine.RoutingNet(end, indeg, heads, slots=256, tile=64, members=E)
+    for net in (a, b):
+        net.set_coeffs(*coef)
+        net.load_forcing(xp, fpe)
+    a.set_state(o0, i0)
+    x = xp[0] + 300e9 * np.arange(1, 41)
+    for k in range(3):
+        a.run(x[k:k + 1])
+    b.copy_state_from(a)
+    b.run(x[3:30])
+    a.copy_state_from(b)
+    a.run(x[30:31])
+    b.copy_state_from(a)
+    b.run(x[31:])
+    so, si = b.get_state()
+    with pytest.raises(Exception):
+        a.copy_state_from(a)
+    other = engine.RoutingNet(end, indeg, heads, members=E + 1)
+    with pytest.raises(Exception):
+        other.copy_state_from(a)
+    for e in (0, 5, E - 1):
+        _, _, fo, fi = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                    np.ascontiguousarray(fpe[:, :, e]), keep_outputs=False)
+        assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
+
+
 def test_conus_scale_ensemble_members_bitexact():
     """Maximum size (BASELINE configs[4] network: 2.7M reaches, 4000 outlets, deepest path ~7000
     reaches, a schedule over thousands of workgroups): a 4-member, 24-step horizon on the

@@ -1091,6 +1091,40 @@ int mc_get_state(void* net, double* o, double* i) {
     });
 }
 
+int mc_net_copy_state(void* dst_net, const void* src_net) {
+    return guarded([&] {
+        Net* D = as_net(dst_net);
+        Net* S = as_net(const_cast<void*>(src_net));
+        REQUIRE(D != S, "source and destination must be different sessions");
+        REQUIRE(D->plan.n == S->plan.n, "sessions route different networks (reach counts differ)");
+        REQUIRE(D->E == S->E, "sessions hold different member counts");
+        const int64_t n = D->plan.n, E = D->E;
+        if (n == 0) return;
+        // order: after the source's pending work, on the destination's stream; the source waits
+        // for the copy before it may overwrite its state again
+        hipEvent_t ev;
+        HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        struct EvGuard {
+            hipEvent_t e;
+            ~EvGuard() { (void)hipEventDestroy(e); }
+        } guard{ev};
+        HIPC(hipEventRecord(ev, S->stream));
+        HIPC(hipStreamWaitEvent(D->stream, ev, 0));
+        D->stage.reserve((size_t)(n * E));
+        for (int k = 0; k < 2; ++k) {
+            const DBuf<double>& from = k ? S->st_i : S->st_o;
+            DBuf<double>& to = k ? D->st_i : D->st_o;
+            // reach-order staging [n][E]: source slots -> reaches -> destination slots
+            HIPC(mcr::launch_gather_from_slots(from.p, D->stage.p, S->pos.p, n, S->plan.nslots, E,
+                                               D->stream));
+            HIPC(mcr::launch_scatter_to_slots(D->stage.p, to.p, D->slot_reach.p, D->plan.nslots, E,
+                                              D->stream));
+        }
+        HIPC(hipEventRecord(ev, D->stream));
+        HIPC(hipStreamWaitEvent(S->stream, ev, 0));
+    });
+}
+
 int mc_step(void* net, const double* o_prev, const double* i_prev, const double* q,
             double* i_out, double* o_out) {
     return guarded([&] {

@@ -75,6 +75,7 @@ SIGNATURES = {
     "mc_net_destroy": (_i32, [_vp]),
     "mc_net_get_info": (_i32, [_vp, ctypes.POINTER(PlanInfo)]),
     "mc_net_set_stream": (_i32, [_vp, _vp]),
+    "mc_net_copy_state": (_i32, [_vp, _vp]),
     "mc_set_coeffs": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "mc_set_state": (_i32, [_vp, _vp, _vp]),
     "mc_get_state": (_i32, [_vp, _vp, _vp]),

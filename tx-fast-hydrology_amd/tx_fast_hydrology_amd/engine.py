@@ -153,6 +153,13 @@ class RoutingNet:
         nat.check(nat.lib().mc_get_state(self._h, ptr(o), ptr(i)))
         return o, i
 
+    def copy_state_from(self, other: "RoutingNet"):
+        """This session's (o, i) := other's, device to device (mc_net_copy_state).  Both
+        sessions route the same network with the same member count; their plans may differ
+        (e.g. a 384-lane plan for one-step assimilation runs and a 256-lane, 64-tick plan for
+        the forecast)."""
+        nat.check(nat.lib().mc_net_copy_state(self._h, other._h))
+
     # -- routing -------------------------------------------------------------------------
     def step(self, q_t_next, o_t_prev=None, i_t_prev=None):
         """One timestep; returns fresh (i_t_next, o_t_next) like nutils._ax_bu."""
