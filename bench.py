@@ -44,9 +44,9 @@ def parse():
     ap.add_argument("--depth", type=int, default=1500)
     ap.add_argument("--T", type=int, default=288)
     ap.add_argument("--dt", type=float, default=300.0)
-    # 0 = per workload: 384 lanes (2 node slots each) + the helper wave make the deterministic
-    # Texas network one resident dataflow launch (one workgroup per CU); ensembles run the
-    # multi-launch path at 256
+    # 0 = per workload: 192 lanes (2 node slots each) + the helper wave make the deterministic
+    # Texas network one resident dataflow launch (two workgroups per CU); ensemble forecasts run
+    # the multi-launch path at 256
     ap.add_argument("--slots", type=int, default=0)
     ap.add_argument("--members", type=int, default=1,
                     help="ensemble members (BASELINE configs[2]: 64); 1 = deterministic")
@@ -149,7 +149,9 @@ def build_workload(args, rank=0, world=1):
     i0 = np.zeros(o0.shape)
     np.add.at(i0, end, o0)                                      # muskingum.py:416-417
 
-    slots = args.slots or (384 if E == 1 else 256)
+    # 192 lanes (3 compute waves + the helper: one wave per SIMD, two workgroups per CU) for
+    # the resident dataflow kernels (det horizon, EnKF member steps); ensemble forecasts 256
+    slots = args.slots or (192 if E == 1 or enkf is not None else 256)
     # ensemble forecasts (multi-launch path): 64-tick launches amortise the per-launch slot
     # loads (Texas ens64 14.1 -> 13.1 ms per horizon); the EnKF keeps 32, whose shorter
     # schedule its one-step member-dataflow launches pay for at every analysis

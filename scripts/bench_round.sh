@@ -16,8 +16,8 @@ run() {   # name, command...
 }
 run det python bench.py --steps 20 --warmup 3
 run ens64 python bench.py --steps 5 --warmup 1 --members 64
-run enkf32 python bench.py --steps 5 --warmup 1 --members 32 --enkf --slots 384
-run enkf256 python bench.py --steps 2 --warmup 1 --members 256 --enkf --slots 384 --no-cpu
+run enkf32 python bench.py --steps 5 --warmup 1 --members 32 --enkf
+run enkf256 python bench.py --steps 2 --warmup 1 --members 256 --enkf --no-cpu
 run conus python bench.py --steps 3 --warmup 1 --conus
 run kf python scripts/bench_kf.py
 exit 0

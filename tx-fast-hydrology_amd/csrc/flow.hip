@@ -34,6 +34,9 @@
 #ifndef MCR_HELPER_SIMD
 #define MCR_HELPER_SIMD 0        // 1: helper = wave 3 (alone on SIMD 3 below 8 waves); measured slower
 #endif
+#ifndef MCR_EXP_CHUNK_BARRIER
+#define MCR_EXP_CHUNK_BARRIER 0  // diagnostic (wrong results): one barrier per chunk, not per tick
+#endif
 #ifndef MCR_HOIST
 #define MCR_HOIST 0              // read both slots' inputs right after the tick barrier
 #endif
@@ -221,22 +224,22 @@ void wavefront_flow(WaveArgs a) {
             const unsigned slot = (unsigned)((kn >> 3) & 1);
             u32x4 g[kBatch];
             if (pre) h.issue(0, kn, g);
-            __syncthreads();                 // tick 0
-            __syncthreads();                 // tick 1
-            __syncthreads();                 // tick 2
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 0
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 1
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 2
             if (pre) {
                 const int bad = h.consume(0, kn, slot, g);
                 if (__any(bad >= 0)) h.settle(0, kn, slot, bad);
                 if (nb > 1) h.issue(1, kn, g);
             }
-            __syncthreads();                 // tick 3
-            __syncthreads();                 // tick 4
-            __syncthreads();                 // tick 5
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 3
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 4
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 5
             if (pre && nb > 1) {
                 const int bad = h.consume(1, kn, slot, g);
                 if (__any(bad >= 0)) h.settle(1, kn, slot, bad);
             }
-            __syncthreads();                 // tick 6
+            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 6
             __syncthreads();                 // tick 7
         }
         return;
@@ -481,12 +484,16 @@ void wavefront_flow(WaveArgs a) {
                 const bool inwin = k >= gminw && k < wend;
                 double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
                 if (!MCR_EXP_NO_STORES) {
-                    #if MCR_NT_STORES
-                    __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
-                    __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
+#if MCR_ACTIVE_STORES
+                // only the ticks of a slot's own steps: the fetch kernels never read the others
+                if (actA) __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
+                if (actB) __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
+#elif MCR_NT_STORES
+                __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
+                __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
 #else
-                    orow[lid] = A.routed ? oA : 0.0;
-                    orow[SLOTS + lid] = B.routed ? oB : 0.0;
+                orow[lid] = A.routed ? oA : 0.0;
+                orow[SLOTS + lid] = B.routed ? oB : 0.0;
 #endif
                 }
                 if (A.xsrc && actA) {
@@ -499,7 +506,7 @@ void wavefront_flow(WaveArgs a) {
                     const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
                     __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
                 }
-                __syncthreads();
+                if (!MCR_EXP_CHUNK_BARRIER || i == kChunk - 1) __syncthreads();
             }
             rbA = rbAn;
             nrA = nrAn;
