@@ -155,7 +155,9 @@ def build_workload(args, rank=0, world=1):
     # ensemble forecasts (multi-launch path): 64-tick launches amortise the per-launch slot
     # loads (Texas ens64 14.1 -> 13.1 ms per horizon); the EnKF keeps 32, whose shorter
     # schedule its one-step member-dataflow launches pay for at every analysis
-    tile = args.tile or (64 if E > 1 and enkf is None else 0)
+    # the dataflow workloads at a 16-tick cross-cluster slack (two chunks, the minimum): Texas
+    # det 0.605 -> 0.594 ms
+    tile = args.tile or (64 if E > 1 and enkf is None else 16)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E)
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
