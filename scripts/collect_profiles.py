@@ -35,12 +35,13 @@ def traffic(tag, fetch, write, line):
 
 
 def sq_counters(tag):
-    tot, n = {}, {}
+    tot, names = {}, set()
     for f in glob.glob(os.path.join(O, f"{tag}_sq_p*", "**", "*counter_collection.csv"),
                        recursive=True):
         for r in csv.DictReader(open(f)):
             if "wavefront_flow" not in r["Kernel_Name"]:
                 continue
+            names.add(r["Kernel_Name"])
             key = (r["Counter_Name"], r["Dispatch_Id"])
             tot[key] = tot.get(key, 0.0) + float(r["Counter_Value"])
     per = {}
@@ -48,8 +49,7 @@ def sq_counters(tag):
         per.setdefault(name, []).append(v)
     c = {k: sum(v) / len(v) for k, v in sorted(per.items())}
     wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
-    rec = {"kernel": "wavefront_flow<384,false,false> (Texas det, bench --steps 1; per dispatch "
-                     "average)",
+    rec = {"kernel": sorted(names), "workload": "Texas det, bench --steps 1; per dispatch average",
            "counters": c,
            "ratios": {"wait_any/wave_cycles": c.get("SQ_WAIT_ANY", 0) / wc,
                       "wait_inst_any/wave_cycles": c.get("SQ_WAIT_INST_ANY", 0) / wc,
