@@ -107,41 +107,5 @@ __device__ __forceinline__ double fold(const char* lds, const unsigned* m, const
     return I;
 }
 
-// Both slots' inputs of one tick, read together right after the tick barrier so the high
-// slot's LDS latency overlaps the low slot's arithmetic (any3: either slot has > 2 inputs;
-// unused codes read the zero slot, so a wave-uniform 4-input read is exact for both).
-struct Inputs {
-    double a[kUpInline], b[kUpInline];
-};
-
-__device__ __forceinline__ void read_inputs(Inputs& x, const char* lds, const unsigned* mA,
-                                            const unsigned* mB, unsigned rd, bool any3) {
-    x.a[0] = lds_f64(lds, mA[0] + rd);
-    x.a[1] = lds_f64(lds, mA[1] + rd);
-    x.b[0] = lds_f64(lds, mB[0] + rd);
-    x.b[1] = lds_f64(lds, mB[1] + rd);
-    if (any3) {
-        x.a[2] = lds_f64(lds, mA[2] + rd);
-        x.a[3] = lds_f64(lds, mA[3] + rd);
-        x.b[2] = lds_f64(lds, mB[2] + rd);
-        x.b[3] = lds_f64(lds, mB[3] + rd);
-    } else {
-        x.a[2] = x.a[3] = x.b[2] = x.b[3] = 0.0;
-    }
-}
-
-// the fold of `fold` over values already read (same association)
-template <bool HIGH>
-__device__ __forceinline__ double fold_of(const double* v, const bool* self, bool any3,
-                                          double low) {
-    double I = HIGH && self[0] ? low : v[0];
-    I = I + (HIGH && self[1] ? low : v[1]);
-    if (any3) {
-        I = I + (HIGH && self[2] ? low : v[2]);
-        I = I + (HIGH && self[3] ? low : v[3]);
-    }
-    return I;
-}
-
 }  // namespace dev
 }  // namespace mcr

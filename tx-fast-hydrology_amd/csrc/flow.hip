@@ -28,17 +28,8 @@
 #ifndef MCR_EXP_NO_Q
 #define MCR_EXP_NO_Q 0
 #endif
-#ifndef MCR_NT_MEMB
-#define MCR_NT_MEMB 0            // member dataflow: new states as non-temporal stores
-#endif
-#ifndef MCR_HELPER_SIMD
-#define MCR_HELPER_SIMD 0        // 1: helper = wave 3 (alone on SIMD 3 below 8 waves); measured slower
-#endif
 #ifndef MCR_EXP_CHUNK_BARRIER
 #define MCR_EXP_CHUNK_BARRIER 0  // diagnostic (wrong results): one barrier per chunk, not per tick
-#endif
-#ifndef MCR_HOIST
-#define MCR_HOIST 0              // read both slots' inputs right after the tick barrier
 #endif
 #ifndef MCR_EXP_NO_HELPER
 #define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
@@ -55,12 +46,8 @@ using dev::Slot;
 using dev::load_slot;
 using dev::decode_codes;
 using dev::fold;
-using dev::fold_of;
-using dev::Inputs;
-using dev::read_inputs;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kHelperLanes = 64;                      // one helper wave per workgroup
 // dataflow instantiations: compute waves + the helper fill whole wave slots on the SIMDs
@@ -70,16 +57,14 @@ constexpr int kBatchItems = kHelperLanes * kBatch;    // (external input, tick) 
 constexpr int64_t kGiveUpTicks = 200000000;           // 2 s of the 100 MHz wall clock
 static_assert(kFlowMaxExt * kChunk == 2 * kBatchItems, "two helper batches per chunk");
 
-#ifndef MCR_SLEEP_UNIT
-#define MCR_SLEEP_UNIT 32        // s_sleep argument (x 64 clocks) per back-off unit
-#endif
-#ifndef MCR_SLEEP_CAP
-#define MCR_SLEEP_CAP 16         // back-off units at most
-#endif
+// poll back-off: s_sleep 32 (x 64 clocks) per unit, at most 16 units (1-64 clocks per unit
+// measured the same)
+constexpr int kSleepUnit = 32;
+constexpr int kSleepCap = 16;
 __device__ __forceinline__ void sleep_backoff(int& sl) {
     // exponential back-off between polls of a granule that is not current yet
-    for (int r = 0; r < sl; ++r) __builtin_amdgcn_s_sleep(MCR_SLEEP_UNIT);
-    sl = sl < MCR_SLEEP_CAP ? sl * 2 : MCR_SLEEP_CAP;
+    for (int r = 0; r < sl; ++r) __builtin_amdgcn_s_sleep(kSleepUnit);
+    sl = sl < kSleepCap ? sl * 2 : kSleepCap;
 }
 
 // Helper wave: stage the external inputs of the chunk starting at tick kn in ring slot `slot`.
@@ -204,11 +189,8 @@ void wavefront_flow(WaveArgs a) {
         reinterpret_cast<int*>(lds + EG)[idx] = a.ext_g[e0 + idx];
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;
 
-    // Waves go round-robin over the 4 SIMDs.  The helper takes wave index 3 (the last wave when
-    // the group has <= 4), so with fewer than 8 waves it has SIMD 3 to itself and its polling
-    // and staging never take issue cycles from a compute wave.
-    constexpr int kHW = MCR_HELPER_SIMD ? (SLOTS / 64 < 3 ? SLOTS / 64 : 3) : SLOTS / 64;
     const int wave = tid >> 6;
+    constexpr int kHW = SLOTS / 64;                     // the helper is the last wave
     if (wave == kHW) {
         // ================================ helper wave ================================
         Helper h{lds, xg, XE, XSLOT, EG, tid & 63, e0, next * kChunk, T, a.epoch, a.status,
@@ -246,7 +228,7 @@ void wavefront_flow(WaveArgs a) {
     }
 
     // ================================ compute waves ================================
-    const int lid = wave < kHW ? tid : tid - 64;        // lane id over the compute waves
+    const int lid = tid;                                // lane id over the compute waves
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
     const int64_t wb = a.wbase[w];
@@ -262,7 +244,6 @@ void wavefront_flow(WaveArgs a) {
     decode_codes<RS>(A, up4A, XB, XE, kChunk * 8);
     decode_codes<RS>(B, up4B, XB, XE, kChunk * 8);
     const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);
-    const bool any3AB = any3A || any3B;
     const unsigned ownA = XB + (unsigned)lid * 16, ownB = XB + (unsigned)(SLOTS + lid) * 16;
 
     const unsigned epoch = a.epoch;
@@ -316,21 +297,11 @@ void wavefront_flow(WaveArgs a) {
                 const int eA = k - A.G, eB = k - B.G;
                 const bool actA = (unsigned)eA < (unsigned)E;
                 const bool actB = (unsigned)eB < (unsigned)E;
-#if MCR_HOIST
-                Inputs in;
-                read_inputs(in, lds, mA, mB, rd, any3AB);
-                const double IA = fold_of<false>(in.a, A.self, any3AB, 0.0);
-#else
                 const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
-#endif
                 const double rA =
                     0.0 + (((A.al * IA + A.be * rA_[r].y) + A.ch * rA_[r].x) + A.ga * rQA[r]);
                 const double oA = A.psum ? IA : rA;
-#if MCR_HOIST
-                const double IB = fold_of<true>(in.b, B.self, any3AB, oA);
-#else
                 const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
-#endif
                 const double rB =
                     0.0 + (((B.al * IB + B.be * rB_[r].y) + B.ch * rB_[r].x) + B.ga * rQB[r]);
                 const double oB = B.psum ? IB : rB;
@@ -348,19 +319,10 @@ void wavefront_flow(WaveArgs a) {
                 }
                 // the member's new state, in place of its inputs (read kRing ticks ago by this
                 // lane); launch_member_unpack forms the session state and output windows
-#if MCR_NT_MEMB
-                if (actA)
-                    __builtin_nontemporal_store(f64x2{A.routed || A.psum ? oA : 0.0, IA},
-                                                reinterpret_cast<f64x2*>(IO) + eA * mS + A.d);
-                if (actB)
-                    __builtin_nontemporal_store(f64x2{B.routed || B.psum ? oB : 0.0, IB},
-                                                reinterpret_cast<f64x2*>(IO) + eB * mS + B.d);
-#else
                 if (actA)
                     IO[(int64_t)eA * mS + A.d] = make_double2(A.routed || A.psum ? oA : 0.0, IA);
                 if (actB)
                     IO[(int64_t)eB * mS + B.d] = make_double2(B.routed || B.psum ? oB : 0.0, IB);
-#endif
                 if (A.xsrc && actA) {
                     const uint64_t bits = (uint64_t)__double_as_longlong(oA);
                     const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
@@ -458,21 +420,11 @@ void wavefront_flow(WaveArgs a) {
                 const unsigned rd = 8u * ((i + 1) & 1);
                 const int k = kc + i;
                 const bool actA = (unsigned)(k - A.G) < (unsigned)T;
-#if MCR_HOIST
-                Inputs in;
-                read_inputs(in, lds, mA, mB, rd, any3AB);
-                const double IA = fold_of<false>(in.a, A.self, any3AB, 0.0);
-#else
                 const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
-#endif
                 const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
                 const double oA = A.psum ? IA : rA;
                 const bool actB = (unsigned)(k - B.G) < (unsigned)T;
-#if MCR_HOIST
-                const double IB = fold_of<true>(in.b, B.self, any3AB, oA);
-#else
                 const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
-#endif
                 const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
                 const double oB = B.psum ? IB : rB;
                 *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
@@ -484,17 +436,10 @@ void wavefront_flow(WaveArgs a) {
                 const bool inwin = k >= gminw && k < wend;
                 double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
                 if (!MCR_EXP_NO_STORES) {
-#if MCR_ACTIVE_STORES
-                // only the ticks of a slot's own steps: the fetch kernels never read the others
-                if (actA) __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
-                if (actB) __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
-#elif MCR_NT_STORES
-                __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
-                __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
-#else
-                orow[lid] = A.routed ? oA : 0.0;
-                orow[SLOTS + lid] = B.routed ? oB : 0.0;
-#endif
+                    // non-temporal: rows are written once and read only by later fetches
+                    // (measured: Texas det horizon 0.734 -> 0.656 ms)
+                    __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
+                    __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
                 }
                 if (A.xsrc && actA) {
                     const uint64_t bits = (uint64_t)__double_as_longlong(oA);

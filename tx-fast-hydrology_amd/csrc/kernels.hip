@@ -244,17 +244,9 @@ void wavefront_det(WaveArgs a) {
             const bool inwin = k >= gminw && k < wend;
             double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
             if (!MCR_EXP_NO_STORES) {
-#if MCR_ACTIVE_STORES
-                // only the ticks of a slot's own steps: the fetch kernels never read the others
-                if (actA) __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + tid);
-                if (actB) __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + tid);
-#elif MCR_NT_STORES
+                // non-temporal: rows are written once and read only by later fetches
                 __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + tid);
                 __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + tid);
-#else
-                orow[tid] = A.routed ? oA : 0.0;
-                orow[SLOTS + tid] = B.routed ? oB : 0.0;
-#endif
                 if (A.xsrc && actA) XSm[A.xs0 + k] = oA;
                 if (B.xsrc && actB) XSm[B.xs0 + k] = oB;
             }

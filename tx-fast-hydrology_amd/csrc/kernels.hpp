@@ -13,12 +13,6 @@
 // index j (jbase is computed per horizon by launch_window_index).
 #pragma once
 
-#ifndef MCR_ACTIVE_STORES
-#define MCR_ACTIVE_STORES 0   // output rows: store only active (slot, tick) entries
-#endif
-#ifndef MCR_NT_STORES
-#define MCR_NT_STORES 1   // output rows as non-temporal (streaming) stores
-#endif
 
 #include <hip/hip_runtime.h>
 
