@@ -40,7 +40,7 @@ def test_nutils_dropins_golden(golden):
     assert np.array_equal(ai, g["ax_i"]) and np.array_equal(ao, g["ax_o"])
 
 
-@pytest.mark.parametrize("n", [700, 1500])      # LDS-resident (n <= 1024) and global variants
+@pytest.mark.parametrize("n", [700, 1500])      # staged (LDS) and global sweeps
 def test_covariance_sweeps_random_forest(n):
     rng = np.random.default_rng(n)
     end = synthetic.river_network(n, 3, max(8, n // 20), rng)

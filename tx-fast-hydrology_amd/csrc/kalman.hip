@@ -14,8 +14,8 @@
 //                                         included (numba_init_inflows, nutils.py:136-141)
 // Columns are independent, so they map to lanes (16 per workgroup, coalesced 128-B row
 // segments); reaches are swept level by level (a level's reaches depend only on lower levels),
-// 16 reach lanes per workgroup, one barrier per level.  When the 16 columns of all reaches fit
-// (n <= 1024) their outputs stay in LDS, so the chain reads upstream outflows from LDS.
+// 16 reach lanes per workgroup, one barrier per level.  Networks up to ~1300 reaches take the
+// staged form (ax_columns_staged: everything a level reads is in LDS).
 // Results are bit-identical to the reference walk: same operations, same association, same
 // summation order, FMA contraction off.  The dense update products run on the f64 MFMA GEMM
 // (analysis.hip); the m x m solve is rocSOLVER LU (getrf / getrs), as np.linalg.inv is LU.
@@ -43,7 +43,7 @@ using namespace capi;
 
 constexpr int kCB = 16;                  // columns per workgroup
 constexpr int kRL = 256 / kCB;           // reach lanes per workgroup
-constexpr int64_t kLdsReaches = 1024;    // LDS-resident outputs up to this many reaches
+constexpr size_t kLdsLimit = 160 * 1024; // LDS of one workgroup
 
 struct GraphArgs {
     const int32_t* lv_off;   // [n_levels + 1] into lv_reach
@@ -60,12 +60,11 @@ struct GraphArgs {
     int32_t n_unrouted;
 };
 
-// Y[:, c] = A X[:, c] for the columns c of this workgroup; X, Y row-major n x ld.
-template <bool LDS>
+// Y[:, c] = A X[:, c] for the columns c of this workgroup; X, Y row-major n x ld (networks
+// too large for the staged sweep below).
 __global__ __launch_bounds__(256) void ax_columns(GraphArgs a, const double* __restrict__ X,
                                                   double* __restrict__ Y, int64_t ld,
                                                   int64_t C) {
-    extern __shared__ double ys[];   // [n][kCB] outputs of this column block (LDS variant)
     const int cl = threadIdx.x % kCB;
     const int rl = threadIdx.x / kCB;
     const int64_t c = (int64_t)blockIdx.x * kCB + cl;
@@ -83,11 +82,85 @@ __global__ __launch_bounds__(256) void ax_columns(GraphArgs a, const double* __r
             double in = 0.0;
             for (int q = a.up_off[j], qe = a.up_off[j + 1]; q < qe; ++q) {
                 const int u = a.up[q];
-                in += LDS ? ys[u * kCB + cl] : Y[(int64_t)u * ld + cs];
+                in += Y[(int64_t)u * ld + cs];
             }
             const double o = 0.0 + ((a.alpha[j] * in + a.beta[j] * ip) +
                                     a.chi[j] * X[(int64_t)j * ld + cs]);
-            if (LDS) ys[j * kCB + cl] = o;
+            if (col) Y[(int64_t)j * ld + c] = o;
+        }
+        __syncthreads();
+    }
+}
+
+// Staged sweep (n small enough that a workgroup keeps all it reads in LDS).  The level chain of
+// ax_columns waits at every level on dependent global loads (the reach index, its upstream
+// lists, x and the inflow-list terms: ~1.5 us per level).  Here the chain-independent terms
+// are formed by one parallel pass (ax_terms) and every workgroup stages its kCS columns of
+// them, the coefficients and the level / upstream lists in LDS before the sweep, so a level
+// costs LDS round trips and one barrier.  Same operations and association:
+//   o = 0 + ((alpha * I + t1) + t2),  t1 = beta * Ip,  t2 = chi * x  (products as before).
+constexpr int kCS = 4;                   // columns per workgroup (staged sweep)
+constexpr int kRS = 256 / kCS;           // reach lanes per workgroup (staged sweep)
+
+// Tm[j * C + c] = {beta_j Ip[j][c], chi_j X[j][c]}  for routed and unrouted reaches alike
+__global__ __launch_bounds__(256) void ax_terms(GraphArgs a, const double* __restrict__ X,
+                                                double2* __restrict__ Tm, int64_t ld, int64_t n,
+                                                int64_t C) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n * C) return;
+    const int64_t j = x / C, c = x - j * C;
+    double ip = 0.0;
+    for (int q = a.in_off[j], qe = a.in_off[j + 1]; q < qe; ++q)
+        ip += X[(int64_t)a.in_src[q] * ld + c];
+    Tm[x] = make_double2(a.beta[j] * ip, a.chi[j] * X[j * ld + c]);
+}
+
+// LDS bytes of the staged sweep: outputs [n][kCS] f64, terms [n][kCS] double2, alpha [n],
+// level offsets [L + 1], level reaches [n_routed], upstream offsets [n + 1], upstreams [n_up]
+inline size_t staged_lds_bytes(int64_t n, int64_t L, int64_t n_routed, int64_t n_up) {
+    return (size_t)n * kCS * 8 + (size_t)n * kCS * 16 + (size_t)n * 8 +
+           4 * (size_t)(L + 1 + n_routed + n + 1 + n_up);
+}
+
+__global__ __launch_bounds__(256) void ax_columns_staged(GraphArgs a,
+                                                         const double2* __restrict__ Tm,
+                                                         double* __restrict__ Y, int64_t ld,
+                                                         int64_t n, int64_t C, int32_t n_routed,
+                                                         int32_t n_up) {
+    extern __shared__ double lsm[];
+    double* ys = lsm;                                            // [n][kCS]
+    double2* tt = reinterpret_cast<double2*>(ys + n * kCS);      // [n][kCS]
+    double* al = reinterpret_cast<double*>(tt + n * kCS);        // [n]
+    int32_t* lo = reinterpret_cast<int32_t*>(al + n);            // [L + 1]
+    int32_t* lr = lo + a.n_levels + 1;                           // [n_routed]
+    int32_t* uo = lr + n_routed;                                 // [n + 1]
+    int32_t* ul = uo + n + 1;                                    // [n_up]
+    const int cl = threadIdx.x % kCS;
+    const int rl = threadIdx.x / kCS;
+    const int64_t c0 = (int64_t)blockIdx.x * kCS;
+    const int64_t c = c0 + cl;
+    const bool col = c < C;
+    for (int64_t x = threadIdx.x; x < n * kCS; x += 256) {
+        const int64_t j = x / kCS, cc = c0 + (x - j * kCS);
+        tt[x] = cc < C ? Tm[j * C + cc] : make_double2(0.0, 0.0);
+    }
+    for (int64_t j = threadIdx.x; j < n; j += 256) al[j] = a.alpha[j];
+    for (int k = threadIdx.x; k <= a.n_levels; k += 256) lo[k] = a.lv_off[k];
+    for (int k = threadIdx.x; k < n_routed; k += 256) lr[k] = a.lv_reach[k];
+    for (int64_t k = threadIdx.x; k <= n; k += 256) uo[k] = a.up_off[k];
+    for (int k = threadIdx.x; k < n_up; k += 256) ul[k] = a.up[k];
+    for (int k = rl; k < a.n_unrouted; k += kRS)
+        if (col) Y[(int64_t)a.unrouted[k] * ld + c] = 0.0;
+    __syncthreads();
+    for (int lv = 0; lv < a.n_levels; ++lv) {
+        const int e = lo[lv + 1];
+        for (int k = lo[lv] + rl; k < e; k += kRS) {
+            const int j = lr[k];
+            double in = 0.0;
+            for (int q = uo[j], qe = uo[j + 1]; q < qe; ++q) in += ys[ul[q] * kCS + cl];
+            const double2 t = tt[j * kCS + cl];
+            const double o = 0.0 + ((al[j] * in + t.x) + t.y);
+            ys[j * kCS + cl] = o;
             if (col) Y[(int64_t)j * ld + c] = o;
         }
         __syncthreads();
@@ -163,13 +236,14 @@ void upload_vec(DBuf<T>& d, const std::vector<T>& v, hipStream_t s) {
 struct Cov {
     int64_t n = 0;
     hipStream_t own = nullptr, stream = nullptr;
-    int32_t n_levels = 0, n_unrouted = 0;
+    int32_t n_levels = 0, n_unrouted = 0, n_routed = 0, n_up = 0;
     DBuf<int32_t> lv_off, lv_reach, up_off, up, in_off, in_src, unrouted;
     DBuf<uint8_t> routed;
     DBuf<double> alpha, beta, chi;
     bool coeffs_set = false;
     // scratch: A P, the transposed product, KF gathers, gain / dz / R / gauges, LU state
     DBuf<double> T1, T2, T3, S, Bt, Ps, gdev, ddev, Rdev;
+    DBuf<double2> Tm;                  // chain-independent terms of the staged sweep
     DBuf<int64_t> sdev;
     DBuf<rocblas_int> ipiv, info;
     rocblas_handle blas = nullptr;
@@ -238,6 +312,8 @@ struct Cov {
             if (rt[j]) lr[fill[level[j]]++] = (int32_t)j;
         n_levels = L;
         n_unrouted = (int32_t)un.size();
+        n_routed = r;
+        n_up = (int32_t)ul.size();
         HIPC(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
         stream = own;
         upload_vec(lv_off, lo, stream);
@@ -280,15 +356,21 @@ struct Cov {
     void ax(const double* X, double* Y) {
         REQUIRE(coeffs_set, "mc_cov_set_coeffs has not been called");
         if (n == 0) return;
-        const dim3 grid((unsigned)((n + kCB - 1) / kCB));
-        if (n <= kLdsReaches) {
-            const size_t lds = (size_t)n * kCB * sizeof(double);
-            HIPC(hipFuncSetAttribute((const void*)ax_columns<true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL(ax_columns<true>, grid, 256, lds, stream, args(), X, Y, n, n);
-        } else {
-            hipLaunchKernelGGL(ax_columns<false>, grid, 256, 0, stream, args(), X, Y, n, n);
+        const size_t slds = staged_lds_bytes(n, n_levels, n_routed, n_up);
+        if (slds <= kLdsLimit) {
+            Tm.reserve((size_t)n * n);
+            hipLaunchKernelGGL(ax_terms, blocks_for(n * n, 256), 256, 0, stream, args(), X, Tm.p,
+                               n, n, n);
+            HIPC(hipGetLastError());
+            HIPC(hipFuncSetAttribute((const void*)ax_columns_staged,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)slds));
+            hipLaunchKernelGGL(ax_columns_staged, dim3((unsigned)((n + kCS - 1) / kCS)), 256,
+                               slds, stream, args(), Tm.p, Y, n, n, n, n_routed, n_up);
+            HIPC(hipGetLastError());
+            return;
         }
+        const dim3 grid((unsigned)((n + kCB - 1) / kCB));
+        hipLaunchKernelGGL(ax_columns, grid, 256, 0, stream, args(), X, Y, n, n);
         HIPC(hipGetLastError());
     }
 
