@@ -116,13 +116,15 @@ __global__ __launch_bounds__(256) void ax_terms(GraphArgs a, const double* __res
 }
 
 // LDS bytes of the staged sweep: outputs [n][kCS] f64, terms [n][kCS] double2, alpha [n],
-// level offsets [L + 1], level reaches [n_routed], upstream offsets [n + 1], upstreams [n_up]
+// level entries [n_routed] int4 {reach, first, end of its upstream list, first upstream},
+// upstreams [n_up], level offsets [L + 1]
 inline size_t staged_lds_bytes(int64_t n, int64_t L, int64_t n_routed, int64_t n_up) {
-    return (size_t)n * kCS * 8 + (size_t)n * kCS * 16 + (size_t)n * 8 +
-           4 * (size_t)(L + 1 + n_routed + n + 1 + n_up);
+    return (size_t)n * kCS * 8 + (size_t)n * kCS * 16 + (size_t)n * 8 + 16 * (size_t)n_routed +
+           4 * (size_t)(n_up + L + 1);
 }
 
 __global__ __launch_bounds__(256) void ax_columns_staged(GraphArgs a,
+                                                         const int4* __restrict__ lvx,
                                                          const double2* __restrict__ Tm,
                                                          double* __restrict__ Y, int64_t ld,
                                                          int64_t n, int64_t C, int32_t n_routed,
@@ -130,39 +132,52 @@ __global__ __launch_bounds__(256) void ax_columns_staged(GraphArgs a,
     extern __shared__ double lsm[];
     double* ys = lsm;                                            // [n][kCS]
     double2* tt = reinterpret_cast<double2*>(ys + n * kCS);      // [n][kCS]
-    double* al = reinterpret_cast<double*>(tt + n * kCS);        // [n]
-    int32_t* lo = reinterpret_cast<int32_t*>(al + n);            // [L + 1]
-    int32_t* lr = lo + a.n_levels + 1;                           // [n_routed]
-    int32_t* uo = lr + n_routed;                                 // [n + 1]
-    int32_t* ul = uo + n + 1;                                    // [n_up]
+    int4* lx = reinterpret_cast<int4*>(tt + n * kCS);            // [n_routed] (16-B aligned)
+    double* al = reinterpret_cast<double*>(lx + n_routed);       // [n]
+    int32_t* ul = reinterpret_cast<int32_t*>(al + n);            // [n_up]
+    int32_t* lo = ul + n_up;                                     // [L + 1]
     const int cl = threadIdx.x % kCS;
     const int rl = threadIdx.x / kCS;
     const int64_t c0 = (int64_t)blockIdx.x * kCS;
     const int64_t c = c0 + cl;
     const bool col = c < C;
-    for (int64_t x = threadIdx.x; x < n * kCS; x += 256) {
-        const int64_t j = x / kCS, cc = c0 + (x - j * kCS);
-        tt[x] = cc < C ? Tm[j * C + cc] : make_double2(0.0, 0.0);
+    // staging: 8 independent loads in flight per lane (one latency per batch, not per item)
+    for (int64_t x0 = threadIdx.x; x0 < n * kCS; x0 += 8 * 256) {
+        double2 v[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int64_t x = x0 + b * 256;
+            const int64_t j = x / kCS, cc = c0 + (x - j * kCS);
+            v[b] = x < n * kCS && cc < C ? Tm[j * C + cc] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            if (x0 + b * 256 < n * kCS) tt[x0 + b * 256] = v[b];
     }
     for (int64_t j = threadIdx.x; j < n; j += 256) al[j] = a.alpha[j];
     for (int k = threadIdx.x; k <= a.n_levels; k += 256) lo[k] = a.lv_off[k];
-    for (int k = threadIdx.x; k < n_routed; k += 256) lr[k] = a.lv_reach[k];
-    for (int64_t k = threadIdx.x; k <= n; k += 256) uo[k] = a.up_off[k];
+    for (int k = threadIdx.x; k < n_routed; k += 256) lx[k] = lvx[k];
     for (int k = threadIdx.x; k < n_up; k += 256) ul[k] = a.up[k];
     for (int k = rl; k < a.n_unrouted; k += kRS)
         if (col) Y[(int64_t)a.unrouted[k] * ld + c] = 0.0;
     __syncthreads();
+    int b = a.n_levels > 0 ? lo[0] : 0, e = a.n_levels > 0 ? lo[1] : 0;
     for (int lv = 0; lv < a.n_levels; ++lv) {
-        const int e = lo[lv + 1];
-        for (int k = lo[lv] + rl; k < e; k += kRS) {
-            const int j = lr[k];
-            double in = 0.0;
-            for (int q = uo[j], qe = uo[j + 1]; q < qe; ++q) in += ys[ul[q] * kCS + cl];
+        const int ne = lv + 2 <= a.n_levels ? lo[lv + 2] : 0;   // next level's end, early
+        for (int k = b + rl; k < e; k += kRS) {
+            const int4 x = lx[k];                 // {j, q0, q1, ul[q0]}: one LDS hop
+            const int j = x.x;
+            const double alj = al[j];             // independent of the fold: read first
             const double2 t = tt[j * kCS + cl];
-            const double o = 0.0 + ((al[j] * in + t.x) + t.y);
+            double in = 0.0;
+            if (x.y < x.z) in += ys[x.w * kCS + cl];
+            for (int q = x.y + 1; q < x.z; ++q) in += ys[ul[q] * kCS + cl];
+            const double o = 0.0 + ((alj * in + t.x) + t.y);
             ys[j * kCS + cl] = o;
             if (col) Y[(int64_t)j * ld + c] = o;
         }
+        b = e;
+        e = ne;
         __syncthreads();
     }
 }
@@ -244,6 +259,7 @@ struct Cov {
     // scratch: A P, the transposed product, KF gathers, gain / dz / R / gauges, LU state
     DBuf<double> T1, T2, T3, S, Bt, Ps, gdev, ddev, Rdev;
     DBuf<double2> Tm;                  // chain-independent terms of the staged sweep
+    DBuf<int4> lvx;                    // staged sweep: {reach, q0, q1, up[q0]} per level slot
     DBuf<int64_t> sdev;
     DBuf<rocblas_int> ipiv, info;
     rocblas_handle blas = nullptr;
@@ -318,6 +334,14 @@ struct Cov {
         stream = own;
         upload_vec(lv_off, lo, stream);
         upload_vec(lv_reach, lr, stream);
+        {
+            std::vector<int4> lx(lr.size());
+            for (size_t k = 0; k < lr.size(); ++k) {
+                const int32_t j = lr[k], q0 = uo[j], q1 = uo[j + 1];
+                lx[k] = make_int4(j, q0, q1, q1 > q0 ? ul[q0] : 0);
+            }
+            upload_vec(lvx, lx, stream);
+        }
         upload_vec(up_off, uo, stream);
         upload_vec(up, ul, stream);
         upload_vec(in_off, io, stream);
@@ -365,7 +389,7 @@ struct Cov {
             HIPC(hipFuncSetAttribute((const void*)ax_columns_staged,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)slds));
             hipLaunchKernelGGL(ax_columns_staged, dim3((unsigned)((n + kCS - 1) / kCS)), 256,
-                               slds, stream, args(), Tm.p, Y, n, n, n, n_routed, n_up);
+                               slds, stream, args(), lvx.p, Tm.p, Y, n, n, n, n_routed, n_up);
             HIPC(hipGetLastError());
             return;
         }
