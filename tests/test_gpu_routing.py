@@ -226,11 +226,12 @@ def test_session_rejects_unaligned_tile():
         engine.RoutingNet(np.array([0]), np.array([0]), np.array([0]), tile=5)
 
 
-@pytest.mark.parametrize("slots", [256, 384, 448])
-def test_texas_scale_bitexact_vs_oracle(exec_mode, slots):
+@pytest.mark.parametrize("slots,tile", [(192, 16), (192, 32), (256, 32), (384, 32), (448, 32)])
+def test_texas_scale_bitexact_vs_oracle(exec_mode, slots, tile):
     """Full Texas-size network (190k reaches, depth ~1500), 24 h @ 300 s: every output of every
-    step bit-identical to the serial oracle.  At 384 / 448 lanes the network fits one resident
-    dataflow launch (auto mode takes it); at 256 it does not (auto falls back to launches)."""
+    step bit-identical to the serial oracle.  At 192 / 384 / 448 lanes the network fits one
+    resident dataflow launch (auto mode takes it; 192 lanes with a 16-tick slack is the bench
+    default); at 256 it does not (auto falls back to launches)."""
     end = synthetic.texas(seed=0)
     n = end.size
     K, X, o0 = synthetic.model_arrays(n, seed=0)
@@ -240,9 +241,9 @@ def test_texas_scale_bitexact_vs_oracle(exec_mode, slots):
     xp = xp.astype(float)
     x = xp[0] + 300e9 * np.arange(1, 289)
     want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
-    net = _net(end, indeg, heads, coef, o0, i0, slots=slots)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=tile)
     got_o, got_i = net.simulate(x, xp, fp)
-    flow = exec_mode != "launches" and slots in (384, 448)
+    flow = exec_mode != "launches" and slots in (192, 384, 448)
     assert net.mode()[1] == ("dataflow" if flow else "launches")
     assert np.array_equal(got_o, want_o)
     assert np.array_equal(got_i, want_i)
