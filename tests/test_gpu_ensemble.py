@@ -111,9 +111,10 @@ def test_ensemble_rejects_dataflow_and_bad_shapes():
         net.run(xp[0] + 300e9 * np.arange(1, 5))
 
 
-@pytest.mark.parametrize("n,E,slots", [(3000, 33, 256), (1200, 2, 128), (4000, 256, 384),
-                                       (190_000, 32, 384)])
-def test_member_dataflow_single_steps(n, E, slots):
+@pytest.mark.parametrize("n,E,slots,tile", [(3000, 33, 256, 0), (1200, 2, 128, 0),
+                                            (4000, 256, 384, 0), (190_000, 32, 384, 0),
+                                            (190_000, 32, 192, 16)])
+def test_member_dataflow_single_steps(n, E, slots, tile):
     """One-step runs of an ensemble (the analysis cycle of the EnKF) as member-dataflow launches:
     member e of slot d at tick G[d] + e.  Several consecutive one-step runs (interpolated
     between forcing rows) then a multi-step run must equal every member's serial run."""
@@ -121,7 +122,7 @@ def test_member_dataflow_single_steps(n, E, slots):
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4 if n < 100_000 else 300, depth,
                                                       n + E, E)
     n = end.size
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=E)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile, members=E)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
     net.load_forcing(xp, fpe)
