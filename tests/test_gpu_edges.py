@@ -1,0 +1,99 @@
+"""GPU edge cases of the session API (empty and minimal inputs, maximum analysis
+sizes): an empty network, a one-reach network, a zero-length horizon, the smallest ensemble
+analysis and one deep enough in gauges that the E x E products take the split-K GEMM."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tx_fast_hydrology_amd import _native as nat
+from tx_fast_hydrology_amd import engine, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _empty():
+    z = np.zeros(0, dtype=np.int64)
+    return engine.RoutingNet(z, z, z)
+
+
+def test_empty_network_session():
+    net = _empty()
+    net.set_coeffs(*(np.zeros(0),) * 4)
+    net.set_state(np.zeros(0), np.zeros(0))
+    net.load_forcing(np.array([0.0, 3.6e12]), np.zeros((2, 0)))
+    net.run(np.array([3e11, 6e11, 9e11]))
+    o, i = net.fetch_outputs()
+    assert o.shape == (3, 0) and i.shape == (3, 0)
+    so, si = net.get_state()
+    assert so.shape == (0,) and si.shape == (0,)
+    other = _empty()
+    other.set_coeffs(*(np.zeros(0),) * 4)
+    other.copy_state_from(net)
+    i_n, o_n = engine.ax_bu(np.zeros(0, np.int64), np.zeros(0, np.int64),
+                            *(np.zeros(0),) * 7, np.zeros(0, np.int64))
+    assert i_n.shape == (0,) and o_n.shape == (0,)
+
+
+def test_zero_length_horizon_is_rejected():
+    end = np.array([1, 1])
+    indeg = orc.compute_indegree(np.arange(2), end)
+    net = engine.RoutingNet(end, indeg, np.array([0]))
+    net.set_coeffs(*(np.full(2, v) for v in (0.1, 0.2, 0.3, 0.4)))
+    net.load_forcing(np.array([0.0]), np.ones((1, 2)))
+    with pytest.raises(nat.RoutingError):
+        net.run(np.zeros(0))
+
+
+@pytest.mark.parametrize("slots,tile", [(64, 16), (192, 16)])
+def test_single_reach_network(slots, tile):
+    end = np.array([0])                     # one outlet (self-loop)
+    start = np.arange(1)
+    indeg = orc.compute_indegree(start, end)
+    coef = orc.muskingum_coeffs(np.array([3600.0]), np.array([0.29]), 300.0)
+    o0, i0 = np.array([2.5]), np.array([0.0])
+    xp = np.array([0.0, 3.6e12, 7.2e12])
+    fp = np.array([[1.0], [2.0], [0.5]])
+    x = 3e11 * np.arange(1, 25)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    got_o, got_i = net.simulate(x, xp, fp)
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+
+
+def _numpy_enkf(X, s, Y, R):
+    E = X.shape[1]
+    A = X - X.mean(1, keepdims=True)
+    HA = A[s]
+    W = np.linalg.solve(HA @ HA.T / (E - 1) + R, Y - X[s])
+    return A @ (HA.T @ W) / (E - 1)
+
+
+@pytest.mark.parametrize("E,m", [(2, 1), (16, 600), (48, 400)])
+def test_enkf_extreme_shapes_vs_numpy(E, m):
+    """E = 2 / one gauge (smallest analysis); m >> E (the E x E products are 600 / 400 gauges
+    deep: split-K over workgroups with the in-order slice reduction)."""
+    end = synthetic.river_network(5000, 6, 150, np.random.default_rng(E + m))
+    n = end.size
+    start = np.arange(n)
+    indeg = orc.compute_indegree(start, end)
+    K, Xk, _ = synthetic.model_arrays(n, seed=3)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
+    net.set_coeffs(*orc.muskingum_coeffs(K, Xk, 300.0))
+    rng = np.random.default_rng(9)
+    X = rng.uniform(0.5, 5, n)[:, None] * rng.lognormal(0, 0.3, (n, E))
+    I0 = rng.uniform(0, 5, (n, E))
+    net.set_state(X, I0)
+    s = np.sort(rng.choice(n, m, replace=False))
+    R = 1e-2 * np.eye(m)
+    Y = X[s].mean(1, keepdims=True) + 0.3 + rng.normal(0, 0.1, (m, E))
+    net.enkf_analysis(s, Y, R)
+    o, i = net.get_state()
+    G = _numpy_enkf(X, s, Y, R)
+    heads = start[indeg == 0]
+    scale = max(np.abs(G).max(), 1e-300)
+    for e in range(E):
+        ig, og = orc.apply_gain(heads, end, G[:, e], indeg)
+        np.testing.assert_allclose(o[:, e] - X[:, e], og, rtol=0, atol=1e-9 * scale)
+        np.testing.assert_allclose(i[:, e] - I0[:, e], ig, rtol=0, atol=1e-8 * scale)
