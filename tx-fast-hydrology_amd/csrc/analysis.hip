@@ -126,6 +126,77 @@ __global__ void scale_rows(const double* __restrict__ HA, const double* __restri
         U[x] = HA[x] / r[x % m];
 }
 
+// Small SPD system M Z = V in one workgroup (k <= kSpdMax): right-looking Cholesky M = L L^T
+// and both triangular solves column-oriented over all right-hand sides at once (every step is
+// a parallel update between two barriers).  M, V column-major k x k; the solution overwrites V.  A pivot
+// <= 0 (not positive definite) stores j + 1 in info (rocSOLVER's convention) and zeroes V.
+// The ensemble-space analysis matrix M = I + S^T R^-1 S is k = E <= 64 in the EnKF cycle:
+// one launch replaces rocSOLVER's potrf + potrs small-size kernels (~65 us per analysis).
+constexpr int kSpdMax = 64;
+__global__ __launch_bounds__(256) void spd_solve_small(const double* __restrict__ M,
+                                                       double* __restrict__ V, int k,
+                                                       int32_t* __restrict__ info) {
+    __shared__ double L[kSpdMax][kSpdMax + 1];   // L[i][j], lower triangle
+    __shared__ double B[kSpdMax][kSpdMax + 1];   // B[i][c] = V(i, c)
+    __shared__ int bad;
+    const int tid = threadIdx.x;
+    for (int x = tid; x < k * k; x += 256) {
+        const int i = x % k, j = x / k;
+        L[i][j] = M[x];
+        B[i][j] = V[x];
+    }
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    // right-looking Cholesky: pivot, scale the column below it, update the trailing triangle
+    for (int j = 0; j < k; ++j) {
+        if (tid == 0) {
+            const double d = L[j][j];
+            if (!(d > 0.0)) bad = j + 1;
+            L[j][j] = sqrt(d);
+        }
+        __syncthreads();
+        if (bad) break;
+        const double ljj = L[j][j];
+        for (int i = j + 1 + tid; i < k; i += 256) L[i][j] = L[i][j] / ljj;
+        __syncthreads();
+        const int r = k - j - 1;                      // trailing rows / columns
+        for (int x = tid; x < r * r; x += 256) {
+            const int i = j + 1 + x / r, c = j + 1 + x % r;
+            if (c <= i) L[i][c] = L[i][c] - L[i][j] * L[c][j];
+        }
+        __syncthreads();
+    }
+    if (bad) {                         // no usable solution: a zero update, reported at sync
+        for (int x = tid; x < k * k; x += 256) V[x] = 0.0;
+        if (tid == 0) *info = bad;
+        return;
+    }
+    // L Y = B, column-oriented: finish row i of every right-hand side, then eliminate it below
+    for (int i = 0; i < k; ++i) {
+        if (tid < k) B[i][tid] = B[i][tid] / L[i][i];
+        __syncthreads();
+        const int r = k - i - 1;
+        for (int x = tid; x < r * k; x += 256) {
+            const int t = i + 1 + x / k, c = x % k;
+            B[t][c] = B[t][c] - L[t][i] * B[i][c];
+        }
+        __syncthreads();
+    }
+    // L^T X = Y, backwards
+    for (int i = k - 1; i >= 0; --i) {
+        if (tid < k) B[i][tid] = B[i][tid] / L[i][i];
+        __syncthreads();
+        for (int x = tid; x < i * k; x += 256) {
+            const int t = x / k, c = x % k;
+            B[t][c] = B[t][c] - L[i][t] * B[i][c];
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    for (int x = tid; x < k * k; x += 256) V[x] = B[x % k][x / k];
+    if (tid == 0) *info = 0;
+}
+
 // M = I (k x k, column-major)
 __global__ void set_identity(double* __restrict__ M, int64_t k) {
     const int64_t total = k * k;
@@ -298,6 +369,13 @@ hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64
                              hipStream_t s) {
     if (m * E > 0)
         hipLaunchKernelGGL(scale_rows, grid_for(m * E, 256), 256, 0, s, HA, r, U, m, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_spd_solve_small(const double* M, double* V, int64_t k, int32_t* info,
+                                  hipStream_t s) {
+    if (k < 1 || k > kSpdMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(spd_solve_small, 1, 256, 0, s, M, V, (int)k, info);
     return hipGetLastError();
 }
 

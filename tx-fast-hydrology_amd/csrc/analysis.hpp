@@ -21,6 +21,11 @@ hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64
                              hipStream_t s);
 // M = I (k x k)
 hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s);
+// V := M^-1 V for SPD M (k x k, column-major, k <= 64) in one workgroup; info = 0, or j + 1 when
+// the j-th leading minor is not positive definite (V then zeroed)
+hipError_t launch_spd_solve_small(const double* M, double* V, int64_t k, int32_t* info,
+                                  hipStream_t s);
+constexpr int64_t kSpdSolveMax = 64;
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s);
 // HA (m x E) = A at the gauge slots; D (m x E) = Y[g][e] - X at the gauge slots (D may be NULL)

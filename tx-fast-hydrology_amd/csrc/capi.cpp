@@ -464,18 +464,28 @@ struct Net {
             Wk.reserve((size_t)(64 * Et * Et));
             HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Ub.p, m, 1.0, Mb.p, Et,
                                    stream, Wk.p, Wk.cap));
-            if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)Et, Mb.p,
-                                 (rocblas_int)Et, info.p) != rocblas_status_success)
-                throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
-            HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                stream));
-            info_pending = true;
-            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p, Et,
-                                   stream, Wk.p, Wk.cap));
-            if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)Et, (rocblas_int)Et,
-                                 Mb.p, (rocblas_int)Et, Zn.p, (rocblas_int)Et) !=
-                rocblas_status_success)
-                throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+            if (Et <= mcr::kSpdSolveMax) {
+                // factor + both solves in one workgroup (analysis.hip spd_solve_small)
+                HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p,
+                                       Et, stream, Wk.p, Wk.cap));
+                HIPC(mcr::launch_spd_solve_small(Mb.p, Zn.p, Et, info.p, stream));
+                HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                    stream));
+                info_pending = true;
+            } else {
+                if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)Et, Mb.p,
+                                     (rocblas_int)Et, info.p) != rocblas_status_success)
+                    throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
+                HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                    stream));
+                info_pending = true;
+                HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p,
+                                       Et, stream, Wk.p, Wk.cap));
+                if (rocsolver_dpotrs(solver(), rocblas_fill_lower, (rocblas_int)Et,
+                                     (rocblas_int)Et, Mb.p, (rocblas_int)Et, Zn.p,
+                                     (rocblas_int)Et) != rocblas_status_success)
+                    throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+            }
         } else {
             // observation space: C = HA HA^T / (Et-1) + R (m x m), W = C^-1 D,
             // Z = HA^T W / (Et-1)
