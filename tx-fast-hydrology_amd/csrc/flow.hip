@@ -31,6 +31,9 @@
 #ifndef MCR_EXP_CHUNK_BARRIER
 #define MCR_EXP_CHUNK_BARRIER 0  // diagnostic (wrong results): one barrier per chunk, not per tick
 #endif
+#ifndef MCR_EXP_BARRIER_CLOCK
+#define MCR_EXP_BARRIER_CLOCK 0  // diagnostic: the trace's CU-id word holds tick-barrier cycles
+#endif
 #ifndef MCR_EXP_NO_HELPER
 #define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
 #endif
@@ -250,6 +253,7 @@ void wavefront_flow(WaveArgs a) {
 
     const unsigned epoch = a.epoch;
     int64_t t_loop = 0, c_loop = 0;
+    int64_t bar_cyc = 0;     // MCR_EXP_BARRIER_CLOCK: shader cycles this lane spent in tick barriers
     if constexpr (MEMB) {
         // ---- member dataflow: tick k runs member e = k - G of each slot.  Per-member inputs
         // (state, lateral inflow) are prefetched kRing ticks ahead into a register ring.
@@ -453,7 +457,13 @@ void wavefront_flow(WaveArgs a) {
                     const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
                     __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
                 }
+#if MCR_EXP_BARRIER_CLOCK
+                const int64_t tb0 = clock64();
+                __syncthreads();
+                bar_cyc += clock64() - tb0;
+#else
                 if (!MCR_EXP_CHUNK_BARRIER || i == kChunk - 1) __syncthreads();
+#endif
             }
             rbA = rbAn;
             nrA = nrAn;
@@ -477,7 +487,7 @@ void wavefront_flow(WaveArgs a) {
         rec[0] = t_start;
         rec[1] = t_loop;
         rec[2] = wall_clock64();
-        rec[3] = (int64_t)__smid();
+        rec[3] = MCR_EXP_BARRIER_CLOCK ? bar_cyc : (int64_t)__smid();
         rec[4] = c_loop;
         rec[5] = clock64();
     }
