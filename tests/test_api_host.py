@@ -167,8 +167,7 @@ def test_fused_horizon_falls_back_when_state_replaced(golden, monkeypatch):
             m.bind_callback(BaseCallback(), key="noop")
         out = []
         for k, state in enumerate(m.simulate(df)):
-            if fused:     # read-only views of fused outputs (a new fused horizon after k = 7)
-                assert not state.o_t_next.flags.writeable
+            assert state.o_t_next.flags.writeable and state.i_t_next.flags.writeable
             out.append(np.array(state.o_t_next))
             if k == 7:    # a consumer nudges the state: the rest routes from it
                 state.o_t_next = state.o_t_next * 1.5
@@ -177,6 +176,41 @@ def test_fused_horizon_falls_back_when_state_replaced(golden, monkeypatch):
     assert np.array_equal(results[0], results[1])
     assert not np.array_equal(results[0][8:50], g["o"][8:])
     assert np.array_equal(results[0][:8], g["o"][:8])
+
+
+def test_fused_horizon_routes_in_place_edits(golden, monkeypatch):
+    """``state.o_t_next[j] = obs`` inside the loop (valid in the reference, which allocates fresh
+    arrays every step) is routed like the step-by-step path routes it."""
+    use_oracle_device(monkeypatch)
+    g = golden("g3_confluence.npz")
+    results = []
+    for fused in (True, False):
+        m = golden_model(g)
+        df = golden_frame(g, m.reach_ids)
+        if not fused:
+            m.bind_callback(BaseCallback(), key="noop")
+        out = []
+        for k, state in enumerate(m.simulate(df)):
+            out.append(np.array(state.o_t_next))
+            if k == 5:
+                state.o_t_next[3] = 7.25
+                state.i_t_next *= 0.5
+        results.append(np.array(out))
+    assert np.array_equal(results[0], results[1])
+    assert not np.array_equal(results[0][6:50], g["o"][6:])
+
+
+def test_fused_horizon_early_break_leaves_writable_state(golden, monkeypatch):
+    use_oracle_device(monkeypatch)
+    g = golden("g3_confluence.npz")
+    m = golden_model(g)
+    for k, _ in enumerate(m.simulate(golden_frame(g, m.reach_ids))):
+        if k == 3:
+            break
+    for key in ("o_t_next", "i_t_next", "o_t_prev", "i_t_prev"):
+        assert getattr(m, key).flags.writeable, key
+    m.init_states(o_t_next=np.ones(m.n))          # in-place writes of the reference API
+    assert np.array_equal(m.o_t_next, np.ones(m.n))
 
 
 def test_idle_callbacks_switch_to_fused(golden, monkeypatch):

@@ -197,6 +197,16 @@ __global__ __launch_bounds__(256) void spd_solve_small(const double* __restrict_
     if (tid == 0) *info = 0;
 }
 
+// X := 0 when the factorisation before it failed (*info != 0): a rocSOLVER potrs on a partly
+// factored matrix returns garbage, so the analysis increment becomes zero, as in spd_solve_small
+__global__ void zero_if_failed(double* __restrict__ X, int64_t cnt,
+                               const int32_t* __restrict__ info) {
+    if (*info == 0) return;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < cnt;
+         x += (int64_t)gridDim.x * blockDim.x)
+        X[x] = 0.0;
+}
+
 // M = I (k x k, column-major)
 __global__ void set_identity(double* __restrict__ M, int64_t k) {
     const int64_t total = k * k;
@@ -376,6 +386,12 @@ hipError_t launch_spd_solve_small(const double* M, double* V, int64_t k, int32_t
                                   hipStream_t s) {
     if (k < 1 || k > kSpdMax) return hipErrorInvalidValue;
     hipLaunchKernelGGL(spd_solve_small, 1, 256, 0, s, M, V, (int)k, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_zero_if_failed(double* X, int64_t cnt, const int32_t* info, hipStream_t s) {
+    if (cnt > 0)
+        hipLaunchKernelGGL(zero_if_failed, grid_for(cnt, 256), 256, 0, s, X, cnt, info);
     return hipGetLastError();
 }
 

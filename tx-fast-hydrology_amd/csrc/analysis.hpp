@@ -26,6 +26,8 @@ hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s);
 hipError_t launch_spd_solve_small(const double* M, double* V, int64_t k, int32_t* info,
                                   hipStream_t s);
 constexpr int64_t kSpdSolveMax = 64;
+// X[0 .. cnt) := 0 when *info != 0 (device-side gate after a rocSOLVER potrf / potrs pair)
+hipError_t launch_zero_if_failed(double* X, int64_t cnt, const int32_t* info, hipStream_t s);
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s);
 // HA (m x E) = A at the gauge slots; D (m x E) = Y[g][e] - X at the gauge slots (D may be NULL)

@@ -265,8 +265,10 @@ struct Net {
             info_pending = false;
             if (*info_host != 0) {
                 *info_host = 0;
-                throw Fail(MC_E_INVALID, "ensemble analysis: HPH^T + R is not positive definite "
-                                         "(the state update was skipped by the solver)");
+                throw Fail(MC_E_INVALID, "ensemble analysis: the analysis matrix (HPH^T + R, or "
+                                         "its ensemble-space form) is not positive definite; "
+                                         "the increment was zeroed, the member states are "
+                                         "unchanged by that analysis");
             }
         }
         if (status_pending) {
@@ -485,6 +487,8 @@ struct Net {
                                      (rocblas_int)Et, Mb.p, (rocblas_int)Et, Zn.p,
                                      (rocblas_int)Et) != rocblas_status_success)
                     throw Fail(MC_E_HIP, "rocsolver_dpotrs failed");
+                // a failed factorisation leaves garbage in Zn: zero update instead
+                HIPC(mcr::launch_zero_if_failed(Zn.p, Et * Et, info.p, stream));
             }
         } else {
             // observation space: C = HA HA^T / (Et-1) + R (m x m), W = C^-1 D,
@@ -509,6 +513,7 @@ struct Net {
             Wk.reserve((size_t)(64 * Et * Et));
             HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, Et,
                                    stream, Wk.p, Wk.cap));
+            HIPC(mcr::launch_zero_if_failed(Zn.p, Et * Et, info.p, stream));
         }
         // slice anomalies and increments G = A Z  (= K D per member)
         An.reserve((size_t)(S * Et));

@@ -37,6 +37,9 @@
 #ifndef MCR_EXP_NO_HELPER
 #define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
 #endif
+#ifndef MCR_EXP_EXTRA_CHAIN
+#define MCR_EXP_EXTRA_CHAIN 0    // diagnostic: n dependent node updates chained after the high slot
+#endif
 
 namespace mcr {
 
@@ -361,6 +364,14 @@ void wavefront_flow(WaveArgs a) {
 
         double* frA = reinterpret_cast<double*>(lds + FR) + lid * 3;
         double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + lid) * 3;
+#if MCR_EXP_EXTRA_CHAIN
+        double xop[MCR_EXP_EXTRA_CHAIN], xip[MCR_EXP_EXTRA_CHAIN];
+#pragma unroll
+        for (int r = 0; r < MCR_EXP_EXTRA_CHAIN; ++r) {
+            xop[r] = B.op;
+            xip[r] = B.ip;
+        }
+#endif
         for (int kc = kb; kc < wend; kc += kChunk) {
             const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
             frA[0] = fA0;
@@ -433,8 +444,19 @@ void wavefront_flow(WaveArgs a) {
                 const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
                 const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
                 const double oB = B.psum ? IB : rB;
+                double oX = oB;
+#if MCR_EXP_EXTRA_CHAIN
+#pragma unroll
+                for (int r = 0; r < MCR_EXP_EXTRA_CHAIN; ++r) {
+                    const double IX = oX + lds_f64(lds, mB[r & 1] + rd);
+                    oX = 0.0 + (((B.al * IX + B.be * xip[r]) + B.ch * xop[r]) + B.ga * qB[i]);
+                    xop[r] = actB ? oX : xop[r];
+                    xip[r] = actB ? IX : xip[r];
+                    __builtin_nontemporal_store(oX, a.dummy + ((lid + 64 * r) & 1023));
+                }
+#endif
                 *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
+                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oX;
                 A.op = actA ? oA : A.op;
                 A.ip = actA ? IA : A.ip;
                 B.op = actB ? oB : B.op;

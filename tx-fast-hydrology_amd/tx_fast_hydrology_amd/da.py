@@ -22,14 +22,19 @@ from __future__ import annotations
 import copy
 import datetime as _dt
 import logging
+import weakref
 
 import numpy as np
 import pandas as pd
 
+from . import engine
 from .callbacks import BaseCallback
-from .nutils import cov_graph, interpolate_sample
+from .nutils import interpolate_sample, topology_key
 
 logger = logging.getLogger(__name__)
+
+# filter -> (topology digest, its CovGraph); entries vanish with their filter
+_FILTER_GRAPHS = weakref.WeakKeyDictionary()
 
 
 def _torch():
@@ -162,8 +167,18 @@ class KalmanFilter(BaseCallback):
 
     # -- analysis --------------------------------------------------------------------------------
     def _graph(self):
+        """This filter's CovGraph, rebuilt only when the model topology changes.  Kept in a
+        weak map keyed by the filter (not in __dict__), so copies build their own handle and many
+        bound filters (one per sub-basin, app.py:129-145) never evict each other."""
         m = self.model
-        graph = cov_graph(m.startnodes[m.indegree == 0], m.endnodes, m.indegree)
+        key, arrays = topology_key(m.startnodes[m.indegree == 0], m.endnodes, m.indegree)
+        held = _FILTER_GRAPHS.get(self)
+        if held is None or held[0] != key:
+            if held is not None:
+                held[1].close()
+            held = (key, engine.CovGraph(arrays[1], arrays[2], arrays[0]))
+            _FILTER_GRAPHS[self] = held
+        graph = held[1]
         graph.set_coeffs(m.alpha, m.beta, m.chi)
         return graph
 

@@ -398,11 +398,11 @@ class Muskingum:
         Without a ``timedelta`` override and while every bound callback is idle
         (``BaseCallback.__idle_steps__``; no callbacks at all is the common case), the remaining
         horizon is routed by the device in fused calls (``mc_run``: interpolation of the forcing rows and
-        routing of every step in one launch) and the steps are then replayed on the host: the
-        yielded state arrays are read-only views of the fetched outputs.  Replacing a state
-        array, rebinding ``datetime`` or binding a non-idle callback between two yields switches
-        the rest of the horizon to step-by-step routing from the state found, as the reference
-        would route it.  Coefficients and topology are read when a fused call starts.
+        routing of every step in one launch) and the steps are then replayed on the host, each
+        yielding fresh writable copies of the fetched outputs.  Editing a state array in place,
+        replacing it, rebinding ``datetime`` or binding a non-idle callback between two yields
+        switches the rest of the horizon to step-by-step routing from the state found, as the
+        reference would route it.  Coefficients and topology are read when a fused call starts.
         """
         assert isinstance(dataframe.index, pd.DatetimeIndex)
         assert dataframe.index.tz == _dt.timezone.utc
@@ -460,10 +460,12 @@ class Muskingum:
             x = np.asarray(xs[c0:c0 + chunk])
             net.run(x)
             out_o, out_i = net.fetch_outputs()
-            out_o.flags.writeable = False
-            out_i.flags.writeable = False
             for k in range(x.size):
-                o_next, i_next = out_o[k], out_i[k]
+                # fresh writable arrays each step, as the reference allocates them
+                # (nutils.py:68-70): a caller may edit them in place (state.o_t_next[j] = obs)
+                # or replace them; either is detected against the fetched rows below and the
+                # rest of the horizon is routed step by step from the state found
+                o_next, i_next = out_o[k].copy(), out_i[k].copy()
                 self.o_t_prev, self.i_t_prev = self.o_t_next, self.i_t_next
                 self.o_t_next, self.i_t_next = o_next, i_next
                 self.datetime += timedelta
@@ -471,19 +473,12 @@ class Muskingum:
                 expected_time = self.datetime
                 yield self
                 if (self.o_t_next is not o_next or self.i_t_next is not i_next
+                        or not np.array_equal(o_next, out_o[k], equal_nan=True)
+                        or not np.array_equal(i_next, out_i[k], equal_nan=True)
                         or not self._callbacks_idle() or self.datetime != expected_time
                         or self.timedelta != timedelta):
-                    self._own_state()
                     yield from self._simulate_steps(dataframe, xp, end_time, kwargs)
                     return
-        self._own_state()
-
-    def _own_state(self):
-        """Replace read-only views of fused outputs by writable arrays."""
-        for key in ("o_t_next", "i_t_next", "o_t_prev", "i_t_prev"):
-            value = getattr(self, key)
-            if isinstance(value, np.ndarray) and not value.flags.writeable:
-                setattr(self, key, value.copy())
 
     def simulate(self, dataframe, start_time=None, end_time=None, o_t_init=None, **kwargs):
         """Route over a time range; returns the ``simulate_iter`` generator (yields ``self``).

@@ -15,6 +15,7 @@ path interpolates in-kernel); ``numba_init_inflows`` is the host scatter of ``in
 """
 from __future__ import annotations
 
+import collections
 import hashlib
 
 import numpy as np
@@ -70,18 +71,28 @@ def _ax(startnodes, endnodes, alpha, beta, chi, i_t_prev, o_t_prev, indegree):
                         zeros, indegree)
 
 
-_GRAPHS = {}
+_GRAPHS = collections.OrderedDict()
+_GRAPHS_MAX = 64
+
+
+def topology_key(startnodes, endnodes, indegree):
+    """(digest, int64 arrays) of a topology: headwaters, endnodes, indegree."""
+    arrays = [np.ascontiguousarray(a, dtype=np.int64) for a in (startnodes, endnodes, indegree)]
+    return hashlib.sha1(b"|".join(a.tobytes() for a in arrays)).hexdigest(), arrays
 
 
 def cov_graph(startnodes, endnodes, indegree):
-    """Cached ``engine.CovGraph`` of a topology (headwaters ``startnodes``)."""
-    arrays = [np.ascontiguousarray(a, dtype=np.int64) for a in (startnodes, endnodes, indegree)]
-    key = hashlib.sha1(b"|".join(a.tobytes() for a in arrays)).hexdigest()
+    """Cached ``engine.CovGraph`` of a topology (headwaters ``startnodes``).  The least recently
+    used graph is closed beyond ``_GRAPHS_MAX`` topologies; ``KalmanFilter`` keeps its own graph
+    on the instance (da.py), so many bound filters do not cycle this cache."""
+    key, arrays = topology_key(startnodes, endnodes, indegree)
     graph = _GRAPHS.get(key)
     if graph is None:
-        if len(_GRAPHS) >= 16:
-            _GRAPHS.pop(next(iter(_GRAPHS))).close()
+        while len(_GRAPHS) >= _GRAPHS_MAX:
+            _GRAPHS.popitem(last=False)[1].close()
         graph = _GRAPHS[key] = engine.CovGraph(arrays[1], arrays[2], arrays[0])
+    else:
+        _GRAPHS.move_to_end(key)
     return graph
 
 
