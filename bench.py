@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--one-plan", action="store_true",
                     help="EnKF: route the forecast on the analysis plan too (no hand-over)")
     ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--chain", type=int, default=0,
+                    help="node slots per lane (plan.hpp lane chains); 0 = per workload")
     ap.add_argument("--conus", action="store_true",
                     help="BASELINE configs[4]: CONUS NWM-scale synthetic network (2.7M reaches, "
                          "4000 outlets, deepest path ~7000 reaches); --members per GPU (default "
@@ -158,7 +160,8 @@ def build_workload(args, rank=0, world=1):
     # the dataflow workloads at a 16-tick cross-cluster slack (two chunks, the minimum): Texas
     # det 0.605 -> 0.594 ms
     tile = args.tile or (64 if E > 1 and enkf is None else 16)
-    net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E)
+    net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E,
+                            chain=args.chain)
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)

@@ -39,11 +39,12 @@ extern "C" {
 #define MC_E_STATE (-5)     /* call out of order (e.g. mc_run before mc_load_forcing) */
 
 typedef struct mc_plan_params {
-    int32_t slots;    /* lanes (threads) per workgroup, 2 node slots each (multiple of 64,
-                         <= 1024); 0 = default */
+    int32_t slots;    /* lanes (threads) per workgroup (multiple of 64, <= 512); 0 = default */
     int32_t tile;     /* ticks per launch = slack of a cross-cluster edge; 0 = default.
                          Device sessions need a multiple of 16. */
     int32_t ext_cap;  /* max cross-cluster inputs per workgroup; 0 = default */
+    int32_t chain;    /* node slots per lane, 1..4 (0 = default 2): a run of up to `chain`
+                         consecutive reaches along a flow path shares one lane and one tick */
 } mc_plan_params;
 
 typedef struct mc_plan_info {
@@ -51,7 +52,7 @@ typedef struct mc_plan_info {
     int64_t n_routed;     /* reaches the reference walk processes (others keep o = 0) */
     int64_t n_clusters;
     int64_t n_cross;      /* cross-cluster edges */
-    int64_t nslots;       /* node slots: nwg * 2 * slots */
+    int64_t nslots;       /* node slots: nwg * chain * slots */
     int32_t nwg;          /* workgroups */
     int32_t slots;
     int32_t tile;
@@ -60,7 +61,9 @@ typedef struct mc_plan_info {
     int32_t max_ext_wg;
     int64_t n_partial;    /* partial-sum nodes (reaches with more than 4 routed upstreams) */
     int64_t n_ext;        /* cross-cluster inputs over all workgroups */
-    int64_t n_pairs;      /* fused lane pairs (a reach and its consumer in one lane and tick) */
+    int64_t n_pairs;      /* chained edges (a node and its consumer in one lane and tick) */
+    int32_t chain;        /* node slots per lane */
+    int32_t reserved;
 } mc_plan_info;
 
 /* Thread-local description of the last error (never NULL). */
@@ -79,11 +82,11 @@ int mc_plan_get_info(const void* plan, mc_plan_info* info);
 int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
                    int64_t* slot_reach);
 /* Schedule links (test / inspection): flags, up_cnt, up4 [nslots] (at most 4 input codes per
- * slot: workgroup-local slot, 0x8000 | external input, or 0x7fff = the lane's low slot in the
- * same tick (fused pair); flags 3 = partial-sum slot); ext_off [nwg+1]; ext_src, ext_g [n_ext]
- * (ext_src is the source's output row: its reach index, or n + slot for a partial-sum slot).
- * Node slot d of workgroup w = w * 2 * slots + lane (+ slots for a lane's high slot).  Any
- * pointer may be NULL. */
+ * slot: workgroup-local slot, 0x8000 | external input, or 0x7fff = the lane's previous position
+ * in the same tick (chained edge); flags 3 = partial-sum slot); ext_off [nwg+1]; ext_src, ext_g
+ * [n_ext] (ext_src is the source's output row: its reach index, or n + slot for a partial-sum
+ * slot).  Node slot d of workgroup w, lane l, position p = w * chain * slots + p * slots + l.
+ * Any pointer may be NULL. */
 int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint64_t* up4,
                          int32_t* ext_off, int64_t* ext_src, int32_t* ext_g);
 /* Launch schedule for a horizon of T steps: launch k covers ticks [k*tile, (k+1)*tile) and

@@ -14,7 +14,7 @@ for rep in 1 2; do
       python - "gpurun_out/ab_${v}_$s.log" "$v" "$s" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(sys.argv[2], "slots", sys.argv[3], "ms", round(d["ms_per_step"], 4), "ticks",
+print(sys.argv[2], "slots", sys.argv[3], "ms", round(d["ms_per_step"], 4), "kern_us", d["roofline"]["avg_launch_us"], "ticks",
       d["config"]["schedule_ticks"], "nwg", d["config"]["nwg"], "kernel", d["roofline"]["kernel"])
 PY
     done

@@ -74,9 +74,10 @@ def summarize_flow(rec, khz, gmin, gmax, T):
 
 
 def wg_windows(plan):
-    """G range of every workgroup's node slots (2 * slots per workgroup, padding excluded)."""
+    """G range of every workgroup's node slots (chain * slots per workgroup, padding
+    excluded)."""
     ex, ln = plan.export(), plan.export_links()
-    rs = 2 * plan.info["slots"]
+    rs = plan.info["chain"] * plan.info["slots"]
     G = ex["G"].reshape(-1, rs)
     used = ln["flags"].reshape(G.shape) != 0
     return np.where(used, G, 1 << 30).min(1), np.where(used, G, -1).max(1)
@@ -106,7 +107,7 @@ def main():
         from tx_fast_hydrology_amd import engine
         heads = np.flatnonzero(wl.indeg == 0)
         plan = engine.Plan(wl.end, wl.indeg, heads, slots=net.info["slots"],
-                           tile=net.info["tile"])
+                           tile=net.info["tile"], chain=net.info["chain"])
         gmin, gmax = wg_windows(plan)
         summarize_flow(rec, khz, gmin, gmax, len(wl.x))
     else:

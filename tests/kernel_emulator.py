@@ -41,14 +41,16 @@ def step_tables(x, xp):
 def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
     """Route len(x) steps exactly as the device does.  Returns (O [n][T], I [n][T]).
 
-    A workgroup has `slots` lanes and 2 * slots node slots: lane l owns slot l (low, computed
-    first in a tick) and slot slots + l (high).  A high node may read its lane's low output of
-    the same tick (SELF code); every other in-workgroup code reads the previous tick."""
+    A workgroup has `slots` lanes and chain * slots node slots: lane l owns slots p * slots + l
+    for positions p = 0 .. chain-1, computed in that order within a tick.  A node may read the
+    output of its lane's previous position in the same tick (SELF code); every other
+    in-workgroup code reads the previous tick."""
     info = plan.info
     ex = plan.export()
     ln = plan.export_links()
     C, tile, nslots = info["slots"], info["tile"], info["nslots"]
-    RS = 2 * C
+    K = info["chain"]
+    RS = K * C
     n = info["n"]
     T = len(x)
     off, wlist = plan.schedule(T)
@@ -115,7 +117,7 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
                 q = np.where(hi[tc] < 0, qlo, w0[tc] * qlo + w1[tc] * qhi)
                 prev = xb[(kk - 1) & 1]
                 cur = xb[kk & 1]
-                for half in (slice(0, C), slice(C, RS)):
+                for half in (slice(p * C, (p + 1) * C) for p in range(K)):
                     Iv = np.zeros(RS)
                     for c in range(4):
                         m = act & (c < cn)

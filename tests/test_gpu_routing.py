@@ -44,6 +44,7 @@ def _model(endnodes, K, X, dt, o0=None, seed=0):
 
 
 def _net(endnodes, indeg, heads, coef, o0, i0, **kw):
+    """Session with coefficients and initial state loaded."""
     net = engine.RoutingNet(endnodes, indeg, heads, **kw)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
@@ -324,3 +325,66 @@ def test_dataflow_rejects_what_does_not_fit():
     net.set_mode("auto")
     net.run(xp[0] + 300e9 * np.arange(1, 11))
     assert net.mode()[1] == "launches"
+
+
+# ---------------------------------------------------------------- lane chains (plan chain > 2)
+@pytest.mark.parametrize("chain,slots,tile,n,p_chain,T", [
+    (3, 64, 16, 3000, 0.95, 50), (4, 64, 16, 3000, 0.95, 37), (3, 192, 16, 6000, 0.98, 96),
+    (4, 128, 32, 6000, 0.98, 60), (4, 256, 16, 5000, 0.5, 20), (4, 192, 16, 2, 1.0, 5)])
+def test_lane_chains_random_vs_oracle(chain, slots, tile, n, p_chain, T):
+    """Lanes of 3 / 4 node slots (a run of consecutive reaches in one lane and one tick):
+    bit-identical to the serial oracle in both execution paths."""
+    end, K, X = _random_case(n, n + T + chain, p_chain, max(1, n // 500))
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=n)
+    xp, fp = synthetic.forcing(n, rows=5, seed=n)
+    xp = xp.astype(float)
+    x = xp[0] - 600e9 + 300e9 * np.arange(1, T + 1)
+    want_o, want_i, fo, fi = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=tile, chain=chain)
+    assert net.info["chain"] == chain
+    got_o, got_i = net.simulate(x, xp, fp)
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+    so, si = net.get_state()
+    assert np.array_equal(so, fo) and np.array_equal(si, fi)
+
+
+@pytest.mark.parametrize("chain", [3, 4])
+def test_lane_chains_high_fan_in_and_step_api(chain):
+    rng = np.random.default_rng(40 + chain)
+    end = synthetic.fan_in_forest(4000, rng, hubs=12)
+    n = end.size
+    K, X = rng.uniform(1800.0, 7200.0, n), rng.uniform(0.1, 0.4, n)
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=chain)
+    xp, fp = synthetic.forcing(n, rows=4, seed=chain)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 41)
+    want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=64, tile=16, chain=chain)
+    assert net.info["n_partial"] > 0
+    got_o, got_i = net.simulate(x, xp, fp)
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+    q = np.random.default_rng(1).uniform(0, 2, n)
+    i_n, o_n = net.step(q, o0, i0)
+    i_w, o_w = orc.ax_bu(heads, end, *coef, i0, o0, q, indeg)
+    assert np.array_equal(o_n, o_w) and np.array_equal(i_n, i_w)
+
+
+@pytest.mark.parametrize("chain,slots", [(3, 192), (3, 256), (4, 192)])
+def test_texas_scale_lane_chains_bitexact(exec_mode, chain, slots):
+    """Full Texas network, 24 h @ 300 s, lanes of 3 / 4 node slots (the deterministic default
+    is chain 4): every output bit-identical to the serial oracle, one resident dataflow launch
+    in auto mode."""
+    end = synthetic.texas(seed=0)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=0)
+    indeg, heads, coef, _, i0 = _model(end, K, X, 300.0)
+    i0 = orc.init_inflows(np.arange(n), end, o0)
+    xp, fp = synthetic.forcing(n, rows=25, seed=1)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 289)
+    want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=16, chain=chain)
+    got_o, got_i = net.simulate(x, xp, fp)
+    assert net.mode()[1] == ("launches" if exec_mode == "launches" else "dataflow")
+    assert np.array_equal(got_o, want_o)
+    assert np.array_equal(got_i, want_i)

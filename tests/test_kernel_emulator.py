@@ -18,11 +18,12 @@ def _case(end, K, X, dt, o0):
     return start, indeg, coef, i0
 
 
+@pytest.mark.parametrize("chain", [2, 1, 3, 4])
 @pytest.mark.parametrize("n,p_chain,slots,tile,T,rows", [
     (1, 0.0, 64, 32, 7, 3), (2, 1.0, 64, 1, 3, 2), (300, 0.9, 64, 4, 50, 5),
     (1500, 0.95, 128, 16, 40, 4), (900, 0.5, 64, 8, 13, 1), (700, 0.99, 64, 64, 1, 2),
     (2000, 0.97, 256, 32, 70, 7)])
-def test_emulator_matches_oracle(n, p_chain, slots, tile, T, rows):
+def test_emulator_matches_oracle(n, p_chain, slots, tile, T, rows, chain):
     rng = np.random.default_rng(n * 7 + T)
     end = synthetic.random_forest(n, max(1, n // 400), rng, p_chain=p_chain)
     K = rng.uniform(1800, 7200, n)
@@ -33,14 +34,15 @@ def test_emulator_matches_oracle(n, p_chain, slots, tile, T, rows):
     xp = xp.astype(float)
     x = xp[0] - 600e9 + 300e9 * np.arange(1, T + 1)
     want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
-    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile, chain=chain)
     O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
     assert np.array_equal(O.T, want_o)
     assert np.array_equal(I.T, want_i)
 
 
-@pytest.mark.parametrize("slots,tile", [(64, 1), (64, 8), (128, 16)])
-def test_emulator_partial_sums_high_fan_in(slots, tile):
+@pytest.mark.parametrize("slots,tile,chain", [(64, 1, 2), (64, 8, 2), (128, 16, 2), (64, 8, 3),
+                                              (128, 16, 4)])
+def test_emulator_partial_sums_high_fan_in(slots, tile, chain):
     """Reaches with up to 30 routed upstreams read chains of partial-sum slots; the fold must
     stay bit-identical to the reference's rank-ordered accumulation."""
     rng = np.random.default_rng(slots + tile)
@@ -53,13 +55,14 @@ def test_emulator_partial_sums_high_fan_in(slots, tile):
     xp = xp.astype(float)
     x = xp[0] + 300e9 * np.arange(1, 41)
     want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
-    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile, chain=chain)
     assert plan.info["n_partial"] > 0
     O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
     assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
 
 
-def test_emulator_river_network_and_golden_edges(golden):
+@pytest.mark.parametrize("chain", [2, 4])
+def test_emulator_river_network_and_golden_edges(golden, chain):
     end = synthetic.river_network(4000, 6, 150, np.random.default_rng(9))
     n = end.size
     K, X, o0 = synthetic.model_arrays(n, seed=3)
@@ -68,14 +71,14 @@ def test_emulator_river_network_and_golden_edges(golden):
     xp = xp.astype(float)
     x = xp[0] + 300e9 * np.arange(1, 31)
     want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
-    plan = engine.Plan(end, indeg, start[indeg == 0], slots=128, tile=8)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=128, tile=8, chain=chain)
     O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
     assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
     g = golden("g8_ax_bu_edge.npz")
     for name in g["names"]:
         a = g[f"{name}_args"]
         plan = engine.Plan(g[f"{name}_endnodes"], g[f"{name}_indegree"], g[f"{name}_heads"],
-                           slots=64, tile=4)
+                           slots=64, tile=4, chain=chain)
         O, I = emu.run(plan, a[0], a[1], a[2], a[3], a[5], a[4], np.array([0.0]),
                        np.array([0.0]), a[6][None, :])
         assert np.array_equal(O[:, 0], g[f"{name}_o"]), name

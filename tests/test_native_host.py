@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(nat.SIGNATURES), set(syms) ^ set(nat.SIGNATURES)
-    assert L.mc_version() == 100
+    assert L.mc_version() == 101
 
 
 def _replay_rank(heads, endnodes, indegree):
@@ -72,12 +72,13 @@ def _check_plan(endnodes, indegree, heads, **kw):
     assert (ln["up_cnt"] <= 4).all()
     assert int((ln["flags"] == 3).sum()) == info["n_partial"]
     assert (ex["slot_reach"][ln["flags"] == 3] == -1).all()
+    rs = info["chain"] * slots
     for d in np.flatnonzero(ln["up_cnt"]):
-        w = d // (2 * slots)
+        w = d // rs
         for c in range(int(ln["up_cnt"][d])):
             code = int((ln["up4"][d] >> np.uint64(16 * c)) & np.uint64(0xFFFF))
-            if code == 0x7FFF:                      # fused pair: the lane's low slot
-                assert d % (2 * slots) >= slots
+            if code == 0x7FFF:                      # chained edge: the lane's previous position
+                assert d % rs >= slots
                 assert Gs[d] == Gs[d - slots] and ln["flags"][d - slots] != 0
             elif code & 0x8000:
                 row = int(ln["ext_src"][ln["ext_off"][w] + (code & 0x7FFF)])
@@ -85,30 +86,34 @@ def _check_plan(endnodes, indegree, heads, **kw):
                 assert Gs[d] - Gs[src] >= tile, (d, src)
                 assert ln["ext_g"][ln["ext_off"][w] + (code & 0x7FFF)] == Gs[d]
             else:
-                src = w * 2 * slots + code
-                assert code < 2 * slots and Gs[d] - Gs[src] == 1, (d, src)
+                src = w * rs + code
+                assert code < rs and Gs[d] - Gs[src] == 1, (d, src)
     assert info["gmax"] == G.max() if n else True
     return info, ex
 
 
-@pytest.mark.parametrize("slots,tile", [(64, 1), (64, 8), (256, 32), (512, 64)])
-def test_plan_invariants_random(slots, tile):
+@pytest.mark.parametrize("slots,tile,chain", [(64, 1, 2), (64, 8, 2), (256, 32, 2), (512, 64, 2),
+                                              (64, 8, 1), (64, 16, 3), (128, 16, 4),
+                                              (256, 32, 4)])
+def test_plan_invariants_random(slots, tile, chain):
     rng = np.random.default_rng(slots + tile)
     for trial in range(3):
         n = int(rng.integers(1, 3000))
         end = synthetic.random_forest(n, int(rng.integers(1, 5)), rng, p_chain=0.9)
         deg = orc.compute_indegree(np.arange(n), end)
         heads = np.flatnonzero(deg == 0)
-        _check_plan(end, deg, heads, slots=slots, tile=tile)
+        _check_plan(end, deg, heads, slots=slots, tile=tile, chain=chain)
 
 
-@pytest.mark.parametrize("slots,tile", [(64, 1), (64, 8), (128, 16), (256, 32)])
-def test_plan_partial_sums_high_fan_in(slots, tile):
+@pytest.mark.parametrize("slots,tile,chain", [(64, 1, 2), (64, 8, 2), (128, 16, 2), (256, 32, 2),
+                                              (64, 16, 3), (128, 16, 4)])
+def test_plan_partial_sums_high_fan_in(slots, tile, chain):
     rng = np.random.default_rng(slots * 3 + tile)
     end = synthetic.fan_in_forest(2500, rng)
     deg = orc.compute_indegree(np.arange(end.size), end)
     assert deg.max() > 4
-    info, ex = _check_plan(end, deg, np.flatnonzero(deg == 0), slots=slots, tile=tile)
+    info, ex = _check_plan(end, deg, np.flatnonzero(deg == 0), slots=slots, tile=tile,
+                           chain=chain)
     assert info["n_partial"] > 0
 
 
@@ -118,17 +123,23 @@ def test_plan_golden_edge_topologies(golden):
         _check_plan(g[f"{name}_endnodes"], g[f"{name}_indegree"], g[f"{name}_heads"])
 
 
-def test_plan_deep_chain_and_capacity():
+@pytest.mark.parametrize("chain", [1, 2, 3, 4])
+def test_plan_deep_chain_and_capacity(chain):
     n = 5000
     end = np.arange(1, n + 1)
     end[-1] = n - 1                       # one 5000-reach chain
     deg = orc.compute_indegree(np.arange(n), end)
-    info, ex = _check_plan(end, deg, np.flatnonzero(deg == 0), slots=256, tile=16)
-    assert info["max_height"] == n - 1
-    assert info["nwg"] >= n // 512                  # 2 node slots per lane
-    # fused lane pairs halve the chain: one tick per pair, plus the cross-cluster slack
-    assert info["n_pairs"] >= n // 2 - info["nwg"]
-    assert (n - 1) // 2 <= info["gmax"] < (n - 1) // 2 + 16 * (info["nwg"] + 1)
+    info, ex = _check_plan(end, deg, np.flatnonzero(deg == 0), slots=256, tile=16, chain=chain)
+    assert info["max_height"] == n - 1 and info["chain"] == chain
+    assert info["nwg"] >= n // (256 * chain)        # `chain` node slots per lane
+    # lane chains divide the chain: one tick per lane, plus the cross-cluster slack
+    assert info["n_pairs"] >= n - n // chain - chain * info["nwg"]
+    assert (n - 1) // chain <= info["gmax"] < (n - 1) // chain + 16 * (info["nwg"] + 1)
+
+
+def test_plan_chain_rejects_out_of_range():
+    with pytest.raises(nat.TopologyError):
+        Plan(np.array([0]), np.array([0]), np.array([0]), chain=5)
 
 
 def test_plan_rejects_bad_input():

@@ -32,6 +32,7 @@ mcr::PlanParams to_params(const mc_plan_params* pp) {
         if (pp->slots) p.slots = pp->slots;
         if (pp->tile) p.tile = pp->tile;
         if (pp->ext_cap) p.ext_cap = pp->ext_cap;
+        if (pp->chain) p.chain = pp->chain;
     }
     return p;
 }
@@ -51,6 +52,8 @@ void fill_info(const mcr::Plan& P, mc_plan_info* info) {
     info->n_partial = P.n_partial;
     info->n_ext = (int64_t)P.ext_src.size();
     info->n_pairs = P.n_pairs;
+    info->chain = P.p.chain;
+    info->reserved = 0;
 }
 
 void check_topology_args(int64_t n, const int64_t* endnodes, const int64_t* indegree,
@@ -71,7 +74,9 @@ int64_t searchsorted_left(const double* xp, int64_t n, double x) {
     return lo;
 }
 
-// {row_lo, row_hi (-1: copy row_lo), frac as two 32-bit halves (lo, hi)}
+// {row_lo, row_hi, frac as two 32-bit halves (lo, hi)}; a step clamped to the first / last
+// forcing row (nutils.py:24-27 copies that row) is {row, row, 0}: (1 - 0) f + 0 f = f exactly
+// for finite forcing
 int4 step_entry(int lo, int hi, double frac) {
     uint64_t bits;
     std::memcpy(&bits, &frac, sizeof(bits));
@@ -183,6 +188,10 @@ struct Net {
         if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
         if (plan.p.tile % mcr::kChunk != 0)
             throw Fail(MC_E_INVALID, "tile must be a multiple of 16 for the device sweep");
+        if (!mcr::wavefront_shape_ok(plan.p.slots, plan.p.chain))
+            throw Fail(MC_E_INVALID, "no device kernel for this (slots, chain): chain 2 takes "
+                                     "slots 64..512 (multiples of 64 up to 448, and 512), chain "
+                                     "3 slots 64/192/256, chain 4 slots 64/128/192/256");
         HIPC(hipGetDevice(&device));
         HIPC(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
         stream = own;
@@ -285,15 +294,15 @@ struct Net {
     // Can the whole horizon run as one dataflow launch?  Every workgroup must be resident.
     bool flow_fits(int64_t T, bool dense, size_t& lds) {
         if (mode == 1) return false;
-        const int S = plan.p.slots;
+        const int S = plan.p.slots, Kc = plan.p.chain;
         const size_t xg = plan.ext_src.size() * (size_t)T * 16;
-        lds = mcr::flow_lds_bytes(S, (int)T, plan.max_ext_wg);
-        bool ok = (S == 64 || S == 128 || S == 192 || S == 256 || S == 384 || S == 448) &&
+        lds = mcr::flow_lds_bytes(S, Kc, (int)T, plan.max_ext_wg);
+        bool ok = mcr::flow_shape_ok(S, Kc) &&
                   plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
                   T <= mcr::kFlowMaxT && xg < (size_t(1) << 31) && lds <= 160 * 1024;
         if (ok) {
             int bpc = 0;
-            HIPC(mcr::flow_occupancy(S, dense, lds, &bpc));
+            HIPC(mcr::flow_occupancy(S, Kc, dense, lds, &bpc));
             ok = (int64_t)bpc * cu_count >= plan.nwg;
         }
         if (mode == 2 && !ok)
@@ -305,15 +314,15 @@ struct Net {
     // Can one step of all E members run as one member-dataflow launch?
     bool members_fit(size_t& lds) {
         if (mode == 1) return false;
-        const int S = plan.p.slots;
+        const int S = plan.p.slots, Kc = plan.p.chain;
         const size_t xg = plan.ext_src.size() * (size_t)E * 16;
-        lds = mcr::flow_lds_bytes(S, 0, plan.max_ext_wg);
-        bool ok = (S == 64 || S == 128 || S == 192 || S == 256 || S == 384 || S == 448) &&
+        lds = mcr::flow_lds_bytes(S, Kc, 0, plan.max_ext_wg);
+        bool ok = mcr::flow_shape_ok(S, Kc) &&
                   plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
                   E < (1 << 24) && xg < (size_t(1) << 31) && lds <= 160 * 1024;
         if (ok) {
             int bpc = 0;
-            HIPC(mcr::flow_members_occupancy(S, lds, &bpc));
+            HIPC(mcr::flow_members_occupancy(S, Kc, lds, &bpc));
             ok = (int64_t)bpc * cu_count >= plan.nwg;
         }
         return ok;
@@ -409,7 +418,7 @@ struct Net {
     // single-GPU mc_enkf_analysis.  Stage buffers are device pointers owned by the caller.
     int64_t slice_size(int64_t N) const { return (plan.nslots + N - 1) / N; }
     // values per tick row of an output window: the node slots of a workgroup
-    int row_width() const { return 2 * plan.p.slots; }
+    int row_width() const { return plan.p.chain * plan.p.slots; }
 
     void upload_gauges(int64_t m, const int64_t* gauges) {
         REQUIRE(m >= 1 && m < (1ll << 31) && gauges, "bad gauge arguments");
@@ -591,6 +600,9 @@ struct Net {
         to_slots(b, beta);
         to_slots(c, chi);
         to_slots(g, gamma);
+        // partial sums pass their fold through, unrouted reaches and padding output 0
+        HIPC(mcr::launch_set_slot_coeffs(flags.p, alpha.p, beta.p, chi.p, gamma.p, plan.nslots,
+                                         stream));
         sync();  // `stage` is reused by the next call
         coeffs_set = true;
     }
@@ -741,7 +753,8 @@ struct Net {
                 for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
             }
             if (timing) HIPC(hipEventRecord(events[0], stream));
-            HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, flds, stream));
+            HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, plan.p.chain, flds,
+                                          stream));
             if (timing) HIPC(hipEventRecord(events[1], stream));
             HIPC(mcr::launch_member_unpack(IOp, flags.p, G.p, wg_gmin.p, cur->wbase.p,
                                            row_width(), O.p, cur->Otot, st_o.p, st_i.p,
@@ -779,7 +792,8 @@ struct Net {
                 for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
             }
             if (timing) HIPC(hipEventRecord(events[0], stream));
-            HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, flds, dense, stream));
+            HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, plan.p.chain, flds, dense,
+                                  stream));
             if (timing) HIPC(hipEventRecord(events[1], stream));
             HIPC(hipMemcpyAsync(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost,
                                 stream));
@@ -788,8 +802,8 @@ struct Net {
             last_path = 2;
         }
         a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
-        const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, a.table_cap, a.ext_cap,
-                                                    a.tile);
+        const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, plan.p.chain, a.table_cap,
+                                                    a.ext_cap, a.tile);
         if (launched == 0 && trace) {
             trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(cur->off[nl], 1));
             trace_wg = cur->list;
@@ -804,7 +818,8 @@ struct Net {
             }
             a.kappa0 = (int32_t)(k * plan.p.tile);
             if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, lds, dense, (int)E, stream));
+            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, plan.p.chain, lds, dense,
+                                       (int)E, stream));
             if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
             ++launched;
             last_path = 1;
@@ -852,9 +867,9 @@ struct Net {
             const double xt = x[t];
             const int64_t ix = searchsorted_left(xp.data(), n_rows, xt);
             if (ix == 0) {
-                tab[t] = step_entry(0, -1, 0.0);
+                tab[t] = step_entry(0, 0, 0.0);
             } else if (ix >= n_rows) {
-                tab[t] = step_entry((int)(n_rows - 1), -1, 0.0);
+                tab[t] = step_entry((int)(n_rows - 1), (int)(n_rows - 1), 0.0);
             } else {
                 // the device forms (1 - frac) * f[ix-1] + frac * f[ix] exactly as numpy does
                 const double dx0 = xt - xp[ix - 1];
@@ -870,7 +885,7 @@ struct Net {
         const int64_t n = plan.n;
         Fstep.reserve((size_t)(std::max<int64_t>(plan.nslots, 1) * E));
         if (n) to_slots(q, Fstep, E);
-        run_tables(1, Fstep.p, 1, std::vector<int4>(1, step_entry(0, -1, 0.0)));
+        run_tables(1, Fstep.p, 1, std::vector<int4>(1, step_entry(0, 0, 0.0)));
         if (n) {  // the new state is the output of the step
             from_slots(st_o, o_out, E);
             from_slots(st_i, i_out, E);
@@ -936,7 +951,7 @@ extern "C" {
 
 const char* mc_last_error(void) { return g_err.c_str(); }
 
-int mc_version(void) { return 100; }
+int mc_version(void) { return 101; }
 
 int mc_plan_create(int64_t n, const int64_t* endnodes, const int64_t* indegree,
                    const int64_t* headwaters, int64_t n_head, const mc_plan_params* params,

@@ -45,7 +45,7 @@ struct Slot {
     double al, be, ch, ga, op, ip;
     int cnt;
     unsigned ubase[kUpInline], uinc[kUpInline];
-    bool self[kUpInline];  // code reads the lane's low output of this tick (fused pair)
+    bool chained;          // the last input is the lane's previous position of this tick
     int64_t xs0;           // XS address of tick 0 when the slot feeds another cluster
 };
 
@@ -82,28 +82,49 @@ __device__ __forceinline__ void decode_codes(Slot& s, uint64_t up4, unsigned XB,
 #pragma unroll
     for (int u = 0; u < kUpInline; ++u) {
         unsigned code = u < s.cnt ? (unsigned)((up4 >> (16 * u)) & 0xffffu) : (unsigned)RS;
-        s.self[u] = code == kSelfCode;
-        if (s.self[u]) code = RS;
+        if (u == 0) s.chained = false;
+        if (code == kSelfCode) {      // the chained (last) input: read the zero slot, added last
+            s.chained = true;
+            code = RS;
+        }
         const bool ext = (code & kExtBit) != 0;
         s.ubase[u] = ext ? XE + (code & 0x7fffu) * ext_stride : XB + code * 16;
         s.uinc[u] = ext ? 16u : 0u;
     }
 }
 
-// inflow fold in reference finalisation order.  Every value a lane publishes is 0 + (...) or
-// such a sum, never -0.0, so the reference's leading 0 + is exact without an add.  HIGH: the
-// slot may read its lane's low output of this tick (`low`) in place of a code.
-template <bool HIGH>
-__device__ __forceinline__ double fold(const char* lds, const unsigned* m, const bool* self,
-                                       unsigned rd, bool any3, double low) {
-    const double v0 = lds_f64(lds, m[0] + rd), v1 = lds_f64(lds, m[1] + rd);
-    double I = HIGH && self[0] ? low : v0;
-    I = I + (HIGH && self[1] ? low : v1);
+// The input values of one slot for this tick (previous-tick outputs in the LDS double buffer,
+// parity rd).  A lane reads the inputs of ALL its positions before it writes any output: the
+// compiler cannot prove that a position's LDS write does not alias the next position's reads,
+// so reads issued after it would wait for it (one LDS round trip per position per tick).
+// any3 (wave-uniform): some slot of the wave has more than 2 inputs.
+__device__ __forceinline__ void read_inputs(const char* lds, const unsigned* m, unsigned rd,
+                                            bool any3, double* v) {
+    v[0] = lds_f64(lds, m[0] + rd);
+    v[1] = lds_f64(lds, m[1] + rd);
     if (any3) {
-        const double v2 = lds_f64(lds, m[2] + rd), v3 = lds_f64(lds, m[3] + rd);
-        I = I + (HIGH && self[2] ? low : v2);
-        I = I + (HIGH && self[3] ? low : v3);
+        v[2] = lds_f64(lds, m[2] + rd);
+        v[3] = lds_f64(lds, m[3] + rd);
+    } else {
+        v[2] = v[3] = 0.0;
     }
+}
+
+// inflow fold in reference finalisation order.  Every value a lane publishes is 0 + (...) or
+// such a sum, never -0.0, so the reference's leading 0 + is exact without an add, and so is
+// adding the zero slot's +0.0 for an unused code.  The chained input of a slot is its LAST
+// input (plan.cpp); its code reads the zero slot and the value, the lane's previous position
+// output of this tick (`prev`), is added after the others: the same left fold bit for bit.
+// first: position 0 (compile-time at every call site), which has no previous position.
+__device__ __forceinline__ double fold_values(const double* v, bool chained, bool any3,
+                                              double prev, bool first) {
+    double I = v[0];
+    I = I + v[1];
+    if (any3) {
+        I = I + v[2];
+        I = I + v[3];
+    }
+    if (!first) I = I + (chained ? prev : 0.0);
     return I;
 }
 

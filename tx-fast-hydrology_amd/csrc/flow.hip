@@ -37,9 +37,6 @@
 #ifndef MCR_EXP_NO_HELPER
 #define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
 #endif
-#ifndef MCR_EXP_EXTRA_CHAIN
-#define MCR_EXP_EXTRA_CHAIN 0    // diagnostic: n dependent node updates chained after the high slot
-#endif
 
 namespace mcr {
 
@@ -51,13 +48,12 @@ using dev::lds_f64;
 using dev::Slot;
 using dev::load_slot;
 using dev::decode_codes;
-using dev::fold;
+using dev::fold_values;
+using dev::read_inputs;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kHelperLanes = 64;                      // one helper wave per workgroup
-// dataflow instantiations: compute waves + the helper fill whole wave slots on the SIMDs
-#define MCR_SLOT_LIST_FLOW(X) X(64) X(128) X(192) X(256) X(384) X(448)
 constexpr int kBatch = 8;                             // granules per helper lane per batch
 constexpr int kBatchItems = kHelperLanes * kBatch;    // (external input, tick) items per batch
 constexpr int64_t kGiveUpTicks = 200000000;           // 2 s of the 100 MHz wall clock
@@ -156,17 +152,21 @@ struct Helper {
     }
 };
 
-// LDS layout (bytes), RS = 2 * SLOTS node slots (lane l: slots l and SLOTS + l):
+// LDS layout (bytes), RS = K * SLOTS node slots (lane l: slots p * SLOTS + l, p < K):
 //   XB [RS + 1][2] f64 | FR [RS][3] f64 | TAB [T] int4 (whole step table)
 //   | XE [2][ext_cap][kChunk] f64 (ring of external inputs, one slot per chunk parity)
 //   | EG [kFlowMaxExt] i32 (consumer G)
-// Each tick a lane routes its low slot, then its high slot (fused pairs: kernels.hip).
+// Each tick a lane routes its K positions in order; position p may take the output of position
+// p - 1 of the same tick (a chained edge, plan.hpp "lane chains").
 // MEMB: member dataflow (kernels.hpp, launch_flow_members): T = E members in place of steps.
-template <int SLOTS, bool DENSE, bool MEMB>
-__global__ __launch_bounds__(SLOTS + kHelperLanes) __attribute__((amdgpu_waves_per_eu(2)))
+// Register budget: two waves per SIMD (256 VGPRs) up to 3 positions per lane; lanes of 4
+// positions need more (one wave per SIMD, so at most 3 compute waves + the helper).
+template <int SLOTS, int K, bool DENSE, bool MEMB>
+__global__ __launch_bounds__(SLOTS + kHelperLanes)
+__attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
 void wavefront_flow(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    constexpr int RS = 2 * SLOTS;
+    constexpr int RS = K * SLOTS;
     constexpr unsigned XB = 0;
     constexpr unsigned FR = XB + (RS + 1) * 16;
     constexpr unsigned TAB = FR + RS * 24;
@@ -240,19 +240,25 @@ void wavefront_flow(WaveArgs a) {
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
     const int64_t wb = a.wbase[w];
-    Slot A, B;                                          // every real slot runs steps 0 .. T-1
-    load_slot(A, a, (int64_t)w * RS + lid, 0, kb, wend - kb, T);
-    load_slot(B, a, (int64_t)w * RS + SLOTS + lid, 0, kb, wend - kb, T);
-    const uint64_t up4A = a.up4[A.d], up4B = a.up4[B.d];
-    xbp[lid * 2 + ((kb - 1) & 1)] = A.op;
-    xbp[(SLOTS + lid) * 2 + ((kb - 1) & 1)] = B.op;
+    Slot S[K];                                          // every real slot runs steps 0 .. T-1
+    uint64_t up[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + lid, 0, kb, wend - kb, T);
+        up[p] = a.up4[S[p].d];
+        xbp[(p * SLOTS + lid) * 2 + ((kb - 1) & 1)] = S[p].op;
+    }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();                                    // LDS tables staged
 
-    decode_codes<RS>(A, up4A, XB, XE, kChunk * 8);
-    decode_codes<RS>(B, up4B, XB, XE, kChunk * 8);
-    const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);
-    const unsigned ownA = XB + (unsigned)lid * 16, ownB = XB + (unsigned)(SLOTS + lid) * 16;
+    bool any3[K];
+    unsigned own[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        decode_codes<RS>(S[p], up[p], XB, XE, kChunk * 8);
+        any3[p] = __any(S[p].cnt > 2);
+        own[p] = XB + (unsigned)(p * SLOTS + lid) * 16;
+    }
 
     const unsigned epoch = a.epoch;
     int64_t t_loop = 0, c_loop = 0;
@@ -266,218 +272,210 @@ void wavefront_flow(WaveArgs a) {
         static_assert(kChunk % kRing == 0, "ring slots must be static in the unrolled chunk");
         const double* __restrict__ Qm = a.Qm;
         double2* __restrict__ IO = reinterpret_cast<double2*>(const_cast<double*>(a.IO));
-        double2 rA_[kRing], rB_[kRing];
-        double rQA[kRing], rQB[kRing];
+        double2 rIO[K][kRing];
+        double rQ[K][kRing];
 #pragma unroll
-        for (int r = 0; r < kRing; ++r) {
-            int eA = kb + r - A.G, eB = kb + r - B.G;
-            eA = eA < 0 ? 0 : (eA >= E ? E - 1 : eA);
-            eB = eB < 0 ? 0 : (eB >= E ? E - 1 : eB);
-            const int64_t pa = (int64_t)eA * mS + A.d, pb = (int64_t)eB * mS + B.d;
-            rA_[r] = IO[pa];
-            rQA[r] = Qm[pa];
-            rB_[r] = IO[pb];
-            rQB[r] = Qm[pb];
-        }
+        for (int r = 0; r < kRing; ++r)
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                int e = kb + r - S[p].G;
+                e = e < 0 ? 0 : (e >= E ? E - 1 : e);
+                const int64_t pa = (int64_t)e * mS + S[p].d;
+                rIO[p][r] = IO[pa];
+                rQ[p][r] = Qm[pa];
+            }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();                                // prologue barrier (helper staged XE)
         t_loop = a.trace ? wall_clock64() : 0;
         c_loop = a.trace ? clock64() : 0;
         for (int kc = kb; kc < wend; kc += kChunk) {
             const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;
-            unsigned mA[kUpInline], mB[kUpInline];
+            unsigned m[K][kUpInline];
 #pragma unroll
-            for (int u = 0; u < kUpInline; ++u) {
-                mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
-                mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
-            }
+            for (int p = 0; p < K; ++p)
+#pragma unroll
+                for (int u = 0; u < kUpInline; ++u)
+                    m[p][u] = S[p].uinc[u] ? S[p].ubase[u] + sb - 8u : S[p].ubase[u];
 #pragma unroll
             for (int i = 0; i < kChunk; ++i) {
                 if (i & 1) {
 #pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) {
-                        mA[u] += A.uinc[u];
-                        mB[u] += B.uinc[u];
-                    }
+                    for (int p = 0; p < K; ++p)
+#pragma unroll
+                        for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uinc[u];
                 }
                 const unsigned rd = 8u * ((i + 1) & 1);
                 const int k = kc + i;
                 const int r = i % kRing;
-                const int eA = k - A.G, eB = k - B.G;
-                const bool actA = (unsigned)eA < (unsigned)E;
-                const bool actB = (unsigned)eB < (unsigned)E;
-                const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
-                const double rA =
-                    0.0 + (((A.al * IA + A.be * rA_[r].y) + A.ch * rA_[r].x) + A.ga * rQA[r]);
-                const double oA = A.psum ? IA : rA;
-                const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
-                const double rB =
-                    0.0 + (((B.al * IB + B.be * rB_[r].y) + B.ch * rB_[r].x) + B.ga * rQB[r]);
-                const double oB = B.psum ? IB : rB;
-                *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
-                {   // refill this ring slot with the inputs of tick k + kRing
-                    int fA = k + kRing - A.G, fB = k + kRing - B.G;
-                    fA = fA < 0 ? 0 : (fA >= E ? E - 1 : fA);
-                    fB = fB < 0 ? 0 : (fB >= E ? E - 1 : fB);
-                    const int64_t pa = (int64_t)fA * mS + A.d, pb = (int64_t)fB * mS + B.d;
-                    rA_[r] = IO[pa];
-                    rQA[r] = Qm[pa];
-                    rB_[r] = IO[pb];
-                    rQB[r] = Qm[pb];
+                double vin[K][kUpInline];
+#pragma unroll
+                for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
+                double ov[K], Iv[K];
+                double prev = 0.0;
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
+                    const double rr = 0.0 + (((S[p].al * I + S[p].be * rIO[p][r].y) +
+                                              S[p].ch * rIO[p][r].x) + S[p].ga * rQ[p][r]);
+                    const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
+                    ov[p] = o;
+                    Iv[p] = I;
+                    prev = o;
+                }
+#pragma unroll
+                for (int p = 0; p < K; ++p)
+                    *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
+#pragma unroll
+                for (int p = 0; p < K; ++p) {   // refill this ring slot with tick k + kRing
+                    int f = k + kRing - S[p].G;
+                    f = f < 0 ? 0 : (f >= E ? E - 1 : f);
+                    const int64_t pa = (int64_t)f * mS + S[p].d;
+                    rIO[p][r] = IO[pa];
+                    rQ[p][r] = Qm[pa];
                 }
                 // the member's new state, in place of its inputs (read kRing ticks ago by this
                 // lane); launch_member_unpack forms the session state and output windows
-                if (actA)
-                    IO[(int64_t)eA * mS + A.d] = make_double2(A.routed || A.psum ? oA : 0.0, IA);
-                if (actB)
-                    IO[(int64_t)eB * mS + B.d] = make_double2(B.routed || B.psum ? oB : 0.0, IB);
-                if (A.xsrc && actA) {
-                    const uint64_t bits = (uint64_t)__double_as_longlong(oA);
-                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16),
-                                                           0, 16);
-                }
-                if (B.xsrc && actB) {
-                    const uint64_t bits = (uint64_t)__double_as_longlong(oB);
-                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16),
-                                                           0, 16);
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    const int e = k - S[p].G;
+                    const bool act = (unsigned)e < (unsigned)E;
+                    if (act)
+                        IO[(int64_t)e * mS + S[p].d] =
+                            make_double2(ov[p], Iv[p]);
+                    if (S[p].xsrc && act) {
+                        const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
+                        const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
+                    }
                 }
                 __syncthreads();
             }
         }
     } else {
-        int rbA, nrA, rbB, nrB;
-        chunk_rows(tab, 0, kb, A.G, T, rbA, nrA);
-        chunk_rows(tab, 0, kb, B.G, T, rbB, nrB);
-        double fA0 = a.F[(int64_t)clamp_row(rbA, nrow) * ns + A.d];
-        double fA1 = a.F[(int64_t)clamp_row(rbA + 1, nrow) * ns + A.d];
-        double fA2 = a.F[(int64_t)clamp_row(rbA + 2, nrow) * ns + A.d];
-        double fB0 = a.F[(int64_t)clamp_row(rbB, nrow) * ns + B.d];
-        double fB1 = a.F[(int64_t)clamp_row(rbB + 1, nrow) * ns + B.d];
-        double fB2 = a.F[(int64_t)clamp_row(rbB + 2, nrow) * ns + B.d];
+        int rb[K], nr[K];
+        double f0[K], f1[K], f2[K];
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            chunk_rows(tab, 0, kb, S[p].G, T, rb[p], nr[p]);
+            f0[p] = a.F[(int64_t)clamp_row(rb[p], nrow) * ns + S[p].d];
+            f1[p] = a.F[(int64_t)clamp_row(rb[p] + 1, nrow) * ns + S[p].d];
+            f2[p] = a.F[(int64_t)clamp_row(rb[p] + 2, nrow) * ns + S[p].d];
+        }
         __builtin_amdgcn_s_waitcnt(0);                      // nothing pending may enter the loop
         __syncthreads();                                    // prologue barrier (helper staged XE)
         t_loop = a.trace ? wall_clock64() : 0;
         c_loop = a.trace ? clock64() : 0;
 
-        double* frA = reinterpret_cast<double*>(lds + FR) + lid * 3;
-        double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + lid) * 3;
-#if MCR_EXP_EXTRA_CHAIN
-        double xop[MCR_EXP_EXTRA_CHAIN], xip[MCR_EXP_EXTRA_CHAIN];
-#pragma unroll
-        for (int r = 0; r < MCR_EXP_EXTRA_CHAIN; ++r) {
-            xop[r] = B.op;
-            xip[r] = B.ip;
-        }
-#endif
+        // lateral inflow of a position at tick i of the chunk, interpolate_sample
+        // (nutils.py:23-33); it does not depend on the routing state (off the tick's chain).
+        // K <= 2 forms the whole chunk's values up front; longer lanes form them per tick
+        // (register budget)
+        constexpr bool kBatchQ = K <= 2;
         for (int kc = kb; kc < wend; kc += kChunk) {
             const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
-            frA[0] = fA0;
-            frA[1] = fA1;
-            frA[2] = fA2;
-            frB[0] = fB0;
-            frB[1] = fB1;
-            frB[2] = fB2;
-            const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
-            const unsigned frpA = FR + (unsigned)lid * 24 - (unsigned)rbA * 8;
-            const unsigned frpB = FR + (unsigned)(SLOTS + lid) * 24 - (unsigned)rbB * 8;
+            unsigned frp[K], tp[K];
+            bool slow = false;
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                double* fr = reinterpret_cast<double*>(lds + FR) + (p * SLOTS + lid) * 3;
+                fr[0] = f0[p];
+                fr[1] = f1[p];
+                fr[2] = f2[p];
+                slow = slow || (DENSE && __any(nr[p] > 3));
+                frp[p] = FR + (unsigned)(p * SLOTS + lid) * 24 - (unsigned)rb[p] * 8;
+                tp[p] = TAB + (unsigned)(kc - S[p].G) * 16u;
+            }
             const int Tn = kc + kChunk < wend ? T : 0;
-            int rbAn, nrAn, rbBn, nrBn;
-            chunk_rows(tab, 0, kc + kChunk, A.G, Tn, rbAn, nrAn);
-            chunk_rows(tab, 0, kc + kChunk, B.G, Tn, rbBn, nrBn);
-            const double gA0 = a.F[(int64_t)clamp_row(rbAn, nrow) * ns + A.d];
-            const double gA1 = a.F[(int64_t)clamp_row(rbAn + 1, nrow) * ns + A.d];
-            const double gA2 = a.F[(int64_t)clamp_row(rbAn + 2, nrow) * ns + A.d];
-            const double gB0 = a.F[(int64_t)clamp_row(rbBn, nrow) * ns + B.d];
-            const double gB1 = a.F[(int64_t)clamp_row(rbBn + 1, nrow) * ns + B.d];
-            const double gB2 = a.F[(int64_t)clamp_row(rbBn + 2, nrow) * ns + B.d];
-            unsigned mA[kUpInline], mB[kUpInline];
-    #pragma unroll
-            for (int u = 0; u < kUpInline; ++u) {
-                mA[u] = A.uinc[u] ? A.ubase[u] + sb - 8u : A.ubase[u];
-                mB[u] = B.uinc[u] ? B.ubase[u] + sb - 8u : B.ubase[u];
+            int rbn[K], nrn[K];
+            double g0[K], g1[K], g2[K];
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                chunk_rows(tab, 0, kc + kChunk, S[p].G, Tn, rbn[p], nrn[p]);
+                g0[p] = a.F[(int64_t)clamp_row(rbn[p], nrow) * ns + S[p].d];
+                g1[p] = a.F[(int64_t)clamp_row(rbn[p] + 1, nrow) * ns + S[p].d];
+                g2[p] = a.F[(int64_t)clamp_row(rbn[p] + 2, nrow) * ns + S[p].d];
             }
-            const unsigned tpA = TAB + (unsigned)(kc - A.G) * 16u;
-            const unsigned tpB = TAB + (unsigned)(kc - B.G) * 16u;
-            double qA[kChunk], qB[kChunk];
-    #pragma unroll
-            for (int j = 0; j < kChunk; ++j) {
-                const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
-                const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
-                double aLo, aHi, bLo, bHi;
+            unsigned m[K][kUpInline];
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+#pragma unroll
+                for (int u = 0; u < kUpInline; ++u)
+                    m[p][u] = S[p].uinc[u] ? S[p].ubase[u] + sb - 8u : S[p].ubase[u];
+            auto q_of = [&](int p, int j) -> double {
+                const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
+                double lo, hi;
                 if (DENSE && slow) {
-                    aLo = a.F[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
-                    aHi = a.F[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
-                    bLo = a.F[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
-                    bHi = a.F[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
+                    lo = a.F[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
+                    hi = a.F[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
                 } else {
-                    aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
-                    aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
-                    bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
-                    bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
+                    lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
+                    hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
                 }
-                const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
-                const double qa = (1.0 - fa) * aLo + fa * aHi;
-                const double qb = (1.0 - fb) * bLo + fb * bHi;
-                qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
-                qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
+                const double f = __hiloint2double(e.w, e.z);
+                const double qq = (1.0 - f) * lo + f * hi;
+                return MCR_EXP_NO_Q ? 0.0 : qq;   // clamped steps: hi = lo, frac = 0
+            };
+            double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
+            if constexpr (kBatchQ) {
+#pragma unroll
+                for (int j = 0; j < kChunk; ++j)
+#pragma unroll
+                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j);
+                if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
             }
-            if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
-    #pragma unroll
+#pragma unroll
             for (int i = 0; i < kChunk; ++i) {
                 if (i & 1) {
-    #pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) {
-                        mA[u] += A.uinc[u];
-                        mB[u] += B.uinc[u];
-                    }
+#pragma unroll
+                    for (int p = 0; p < K; ++p)
+#pragma unroll
+                        for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uinc[u];
                 }
                 const unsigned rd = 8u * ((i + 1) & 1);
                 const int k = kc + i;
-                const bool actA = (unsigned)(k - A.G) < (unsigned)T;
-                const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
-                const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
-                const double oA = A.psum ? IA : rA;
-                const bool actB = (unsigned)(k - B.G) < (unsigned)T;
-                const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
-                const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
-                const double oB = B.psum ? IB : rB;
-                double oX = oB;
-#if MCR_EXP_EXTRA_CHAIN
+                double qv[K];
 #pragma unroll
-                for (int r = 0; r < MCR_EXP_EXTRA_CHAIN; ++r) {
-                    const double IX = oX + lds_f64(lds, mB[r & 1] + rd);
-                    oX = 0.0 + (((B.al * IX + B.be * xip[r]) + B.ch * xop[r]) + B.ga * qB[i]);
-                    xop[r] = actB ? oX : xop[r];
-                    xip[r] = actB ? IX : xip[r];
-                    __builtin_nontemporal_store(oX, a.dummy + ((lid + 64 * r) & 1023));
+                for (int p = 0; p < K; ++p) {
+                    if constexpr (kBatchQ) qv[p] = qb[p][i];
+                    else qv[p] = q_of(p, i);
                 }
-#endif
-                *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-                *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oX;
-                A.op = actA ? oA : A.op;
-                A.ip = actA ? IA : A.ip;
-                B.op = actB ? oB : B.op;
-                B.ip = actB ? IB : B.ip;
+                double vin[K][kUpInline];
+#pragma unroll
+                for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
+                double ov[K];
+                double prev = 0.0;
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    const bool act = (unsigned)(k - S[p].G) < (unsigned)T;
+                    const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
+                    const double rr =
+                        0.0 + (((S[p].al * I + S[p].be * S[p].ip) + S[p].ch * S[p].op) +
+                               S[p].ga * qv[p]);
+                    const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
+                    S[p].op = act ? o : S[p].op;
+                    S[p].ip = act ? I : S[p].ip;
+                    ov[p] = o;
+                    prev = o;
+                }
+#pragma unroll
+                for (int p = 0; p < K; ++p)
+                    *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
                 const bool inwin = k >= gminw && k < wend;
                 double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
-                if (!MCR_EXP_NO_STORES) {
-                    // non-temporal: rows are written once and read only by later fetches
-                    // (measured: Texas det horizon 0.734 -> 0.656 ms)
-                    __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + lid);
-                    __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + lid);
-                }
-                if (A.xsrc && actA) {
-                    const uint64_t bits = (uint64_t)__double_as_longlong(oA);
-                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((A.xs0 + k) * 16), 0, 16);
-                }
-                if (B.xsrc && actB) {
-                    const uint64_t bits = (uint64_t)__double_as_longlong(oB);
-                    const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                    __builtin_amdgcn_raw_buffer_store_b128(gv, xg, (unsigned)((B.xs0 + k) * 16), 0, 16);
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    if (!MCR_EXP_NO_STORES) {
+                        // non-temporal: rows are written once and read only by later fetches
+                        // (measured: Texas det horizon 0.734 -> 0.656 ms)
+                        __builtin_nontemporal_store(ov[p], orow + p * SLOTS + lid);
+                    }
+                    if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T) {
+                        const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
+                        const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
+                    }
                 }
 #if MCR_EXP_BARRIER_CLOCK
                 const int64_t tb0 = clock64();
@@ -487,22 +485,21 @@ void wavefront_flow(WaveArgs a) {
                 if (!MCR_EXP_CHUNK_BARRIER || i == kChunk - 1) __syncthreads();
 #endif
             }
-            rbA = rbAn;
-            nrA = nrAn;
-            rbB = rbBn;
-            nrB = nrBn;
-            fA0 = gA0;
-            fA1 = gA1;
-            fA2 = gA2;
-            fB0 = gB0;
-            fB1 = gB1;
-            fB2 = gB2;
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                rb[p] = rbn[p];
+                nr[p] = nrn[p];
+                f0[p] = g0[p];
+                f1[p] = g1[p];
+                f2[p] = g2[p];
+            }
         }
         // session state after the horizon; never-processed reaches hold o = 0
-        a.st_o[A.d] = A.routed || A.psum ? A.op : 0.0;
-        a.st_i[A.d] = A.ip;
-        a.st_o[B.d] = B.routed || B.psum ? B.op : 0.0;
-        a.st_i[B.d] = B.ip;
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            a.st_o[S[p].d] = S[p].op;
+            a.st_i[S[p].d] = S[p].ip;
+        }
     }
     if (a.trace && tid == 0) {
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
@@ -516,14 +513,27 @@ void wavefront_flow(WaveArgs a) {
 }
 
 template <bool DENSE, bool MEMB>
-const void* flow_fn(int slots) {
-    switch (slots) {
-#define MCR_CASE(S) \
-    case S: return reinterpret_cast<const void*>(&wavefront_flow<S, DENSE, MEMB>);
-        MCR_SLOT_LIST_FLOW(MCR_CASE)
+const void* flow_fn(int slots, int chain);
+
+}  // namespace
+
+bool flow_shape_ok(int slots, int chain) {
+#define MCR_CASE(S, K) if (slots == S && chain == K) return true;
+    MCR_FLOW_SHAPES(MCR_CASE)
 #undef MCR_CASE
-        default: return nullptr;
-    }
+    return false;
+}
+
+namespace {
+
+template <bool DENSE, bool MEMB>
+const void* flow_fn(int slots, int chain) {
+#define MCR_CASE(S, K)                 \
+    if (slots == S && chain == K)      \
+        return reinterpret_cast<const void*>(&wavefront_flow<S, K, DENSE, MEMB>);
+    MCR_FLOW_SHAPES(MCR_CASE)
+#undef MCR_CASE
+    return nullptr;
 }
 
 hipError_t occupancy_of(const void* fn, int slots, size_t lds, int* blocks_per_cu) {
@@ -570,26 +580,27 @@ __global__ void member_inputs(const double* __restrict__ F, int64_t mF, int64_t 
 
 }  // namespace
 
-hipError_t flow_occupancy(int slots, bool dense, size_t lds, int* blocks_per_cu) {
-    return occupancy_of(dense ? flow_fn<true, false>(slots) : flow_fn<false, false>(slots), slots,
-                        lds, blocks_per_cu);
+hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds, int* blocks_per_cu) {
+    return occupancy_of(dense ? flow_fn<true, false>(slots, chain)
+                              : flow_fn<false, false>(slots, chain),
+                        slots, lds, blocks_per_cu);
 }
 
-hipError_t flow_members_occupancy(int slots, size_t lds, int* blocks_per_cu) {
-    return occupancy_of(flow_fn<false, true>(slots), slots, lds, blocks_per_cu);
+hipError_t flow_members_occupancy(int slots, int chain, size_t lds, int* blocks_per_cu) {
+    return occupancy_of(flow_fn<false, true>(slots, chain), slots, lds, blocks_per_cu);
 }
 
-hipError_t launch_flow(const WaveArgs& a, int grid, int slots, size_t lds, bool dense,
+hipError_t launch_flow(const WaveArgs& a, int grid, int slots, int chain, size_t lds, bool dense,
                        hipStream_t s) {
-    const void* fn = dense ? flow_fn<true, false>(slots) : flow_fn<false, false>(slots);
+    const void* fn = dense ? flow_fn<true, false>(slots, chain) : flow_fn<false, false>(slots, chain);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<WaveArgs*>(&a)};
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);
 }
 
-hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, size_t lds,
+hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain, size_t lds,
                                hipStream_t s) {
-    const void* fn = flow_fn<false, true>(slots);
+    const void* fn = flow_fn<false, true>(slots, chain);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<WaveArgs*>(&a)};
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);

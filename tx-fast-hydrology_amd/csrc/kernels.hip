@@ -42,24 +42,26 @@ using dev::lds_f64;
 using dev::Slot;
 using dev::load_slot;
 using dev::decode_codes;
-using dev::fold;
+using dev::fold_values;
+using dev::read_inputs;
 
-// LDS layout of one workgroup (bytes), RS = 2 * SLOTS node slots (lane l: slots l and
-// SLOTS + l):
+// LDS layout of one workgroup (bytes), RS = K * SLOTS node slots (lane l: slots p * SLOTS + l
+// for positions p < K):
 //   XB  [RS + 1][2] f64   output of each node slot at tick parity 0/1; slot RS stays 0.0
 //   FR  [RS][3]     f64   each slot's forcing rows rb .. rb + 2 of the current chunk
 //   TAB [table_cap] int4  step-table window {row_lo, row_hi, frac}
 //   XE  [ext_cap][tile] f64 external inputs of this launch
-// Each tick a lane routes its low slot, then its high slot; a fused pair's high node takes the
-// low output of the same tick from a register (SELF code), so a fused edge costs no tick.
+// Each tick a lane routes its K positions in order; position p may take the output of position
+// p - 1 of the same tick from a register (SELF code), so a chained edge costs no tick.
 // DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
-template <int SLOTS, bool DENSE>
-__global__ __launch_bounds__(SLOTS) __attribute__((amdgpu_waves_per_eu(2)))
+template <int SLOTS, int K, bool DENSE>
+__global__ __launch_bounds__(SLOTS)
+__attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
 void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    constexpr int RS = 2 * SLOTS;
+    constexpr int RS = K * SLOTS;
     const int tile = a.tile;
     constexpr unsigned XB = 0;
     constexpr unsigned FR = XB + (RS + 1) * 16;
@@ -86,10 +88,13 @@ void wavefront_det(WaveArgs a) {
     const int64_t wb = a.wbase[w];
 
     // ---- per-slot registers (issued first: longest latency)
-    Slot A, B;
-    load_slot(A, a, (int64_t)w * RS + tid, mem, k0, tile, T);
-    load_slot(B, a, (int64_t)w * RS + SLOTS + tid, mem, k0, tile, T);
-    const uint64_t up4A = a.up4[A.d], up4B = a.up4[B.d];
+    Slot S[K];
+    uint64_t up[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + tid, mem, k0, tile, T);
+        up[p] = a.up4[S[p].d];
+    }
 
     // ---- step-table window of this workgroup -> LDS
     int tw0 = k0 - gmaxw, tw1 = k0 + tile - gminw;
@@ -123,153 +128,165 @@ void wavefront_det(WaveArgs a) {
             if (base + k * SLOTS < ntot) xe[base + k * SLOTS] = v[k];
     }
     // the consumer (one tick behind) reads step t_first - 1 at the first tick
-    xbp[tid * 2 + ((k0 - 1) & 1)] = A.op;
-    xbp[(SLOTS + tid) * 2 + ((k0 - 1) & 1)] = B.op;
+#pragma unroll
+    for (int p = 0; p < K; ++p) xbp[(p * SLOTS + tid) * 2 + ((k0 - 1) & 1)] = S[p].op;
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;               // zero slot for unused codes
     // drain every prologue load: otherwise the wait-count pass carries "pending" state into
     // the tick loop and waits for each chunk's stores at every tick
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 
-    decode_codes<RS>(A, up4A, XB, XE, (unsigned)tile * 8);
-    decode_codes<RS>(B, up4B, XB, XE, (unsigned)tile * 8);
-    const bool any3A = __any(A.cnt > 2), any3B = __any(B.cnt > 2);   // wave-uniform
-    const unsigned ownA = XB + (unsigned)tid * 16, ownB = XB + (unsigned)(SLOTS + tid) * 16;
+    bool any3[K];
+    unsigned own[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        decode_codes<RS>(S[p], up[p], XB, XE, (unsigned)tile * 8);
+        any3[p] = __any(S[p].cnt > 2);                  // wave-uniform
+        own[p] = XB + (unsigned)(p * SLOTS + tid) * 16;
+    }
 
     // forcing rows of the first chunk
-    int rbA, nrA, rbB, nrB;
-    chunk_rows(tab, tw0, k0, A.G, T, rbA, nrA);
-    chunk_rows(tab, tw0, k0, B.G, T, rbB, nrB);
-    double fA0 = Fm[(int64_t)clamp_row(rbA, nrow) * ns + A.d];
-    double fA1 = Fm[(int64_t)clamp_row(rbA + 1, nrow) * ns + A.d];
-    double fA2 = Fm[(int64_t)clamp_row(rbA + 2, nrow) * ns + A.d];
-    double fB0 = Fm[(int64_t)clamp_row(rbB, nrow) * ns + B.d];
-    double fB1 = Fm[(int64_t)clamp_row(rbB + 1, nrow) * ns + B.d];
-    double fB2 = Fm[(int64_t)clamp_row(rbB + 2, nrow) * ns + B.d];
+    int rb[K], nr[K];
+    double f0[K], f1[K], f2[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        chunk_rows(tab, tw0, k0, S[p].G, T, rb[p], nr[p]);
+        f0[p] = Fm[(int64_t)clamp_row(rb[p], nrow) * ns + S[p].d];
+        f1[p] = Fm[(int64_t)clamp_row(rb[p] + 1, nrow) * ns + S[p].d];
+        f2[p] = Fm[(int64_t)clamp_row(rb[p] + 2, nrow) * ns + S[p].d];
+    }
     __builtin_amdgcn_s_waitcnt(0);   // same reason: nothing pending may enter the loop
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
     const int wend = gmaxw + T;                         // end of this workgroup's window
-    double* frA = reinterpret_cast<double*>(lds + FR) + tid * 3;
-    double* frB = reinterpret_cast<double*>(lds + FR) + (SLOTS + tid) * 3;
+    constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         // this chunk's forcing rows -> the slots' LDS rows (private: no barrier needed)
-        frA[0] = fA0;
-        frA[1] = fA1;
-        frA[2] = fA2;
-        frB[0] = fB0;
-        frB[1] = fB1;
-        frB[2] = fB2;
-        const bool slow = DENSE && (__any(nrA > 3) || __any(nrB > 3));
-        const unsigned frpA = FR + (unsigned)tid * 24 - (unsigned)rbA * 8;
-        const unsigned frpB = FR + (unsigned)(SLOTS + tid) * 24 - (unsigned)rbB * 8;
+        unsigned frp[K], tp[K];
+        bool slow = false;
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            double* fr = reinterpret_cast<double*>(lds + FR) + (p * SLOTS + tid) * 3;
+            fr[0] = f0[p];
+            fr[1] = f1[p];
+            fr[2] = f2[p];
+            slow = slow || (DENSE && __any(nr[p] > 3));
+            frp[p] = FR + (unsigned)(p * SLOTS + tid) * 24 - (unsigned)rb[p] * 8;
+            tp[p] = TAB + (unsigned)(kc - S[p].G - tw0) * 16u;
+        }
         // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
         const int Tn = c + kChunk < tile ? T : 0;
-        int rbAn, nrAn, rbBn, nrBn;
-        chunk_rows(tab, tw0, kc + kChunk, A.G, Tn, rbAn, nrAn);
-        chunk_rows(tab, tw0, kc + kChunk, B.G, Tn, rbBn, nrBn);
-        const double gA0 = Fm[(int64_t)clamp_row(rbAn, nrow) * ns + A.d];
-        const double gA1 = Fm[(int64_t)clamp_row(rbAn + 1, nrow) * ns + A.d];
-        const double gA2 = Fm[(int64_t)clamp_row(rbAn + 2, nrow) * ns + A.d];
-        const double gB0 = Fm[(int64_t)clamp_row(rbBn, nrow) * ns + B.d];
-        const double gB1 = Fm[(int64_t)clamp_row(rbBn + 1, nrow) * ns + B.d];
-        const double gB2 = Fm[(int64_t)clamp_row(rbBn + 2, nrow) * ns + B.d];
+        int rbn[K], nrn[K];
+        double g0[K], g1[K], g2[K];
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            chunk_rows(tab, tw0, kc + kChunk, S[p].G, Tn, rbn[p], nrn[p]);
+            g0[p] = Fm[(int64_t)clamp_row(rbn[p], nrow) * ns + S[p].d];
+            g1[p] = Fm[(int64_t)clamp_row(rbn[p] + 1, nrow) * ns + S[p].d];
+            g2[p] = Fm[(int64_t)clamp_row(rbn[p] + 2, nrow) * ns + S[p].d];
+        }
         // per-chunk LDS cursors: input value of tick i at m[u] + 8 * ((i + 1) & 1)
-        unsigned mA[kUpInline], mB[kUpInline];
+        unsigned m[K][kUpInline];
 #pragma unroll
-        for (int u = 0; u < kUpInline; ++u) {
-            mA[u] = A.uinc[u] ? A.ubase[u] + 8u * c - 8u : A.ubase[u];
-            mB[u] = B.uinc[u] ? B.ubase[u] + 8u * c - 8u : B.ubase[u];
-        }
-        const unsigned tpA = TAB + (unsigned)(kc - A.G - tw0) * 16u;
-        const unsigned tpB = TAB + (unsigned)(kc - B.G - tw0) * 16u;
-        // lateral inflow of the chunk's ticks, interpolate_sample (nutils.py:23-33); it does
-        // not depend on the routing state, so it is formed off the tick's critical path
-        double qA[kChunk], qB[kChunk];
+        for (int p = 0; p < K; ++p)
 #pragma unroll
-        for (int j = 0; j < kChunk; ++j) {
-            const int4 ea = *reinterpret_cast<const int4*>(lds + tpA + 16u * j);
-            const int4 eb = *reinterpret_cast<const int4*>(lds + tpB + 16u * j);
-            double aLo, aHi, bLo, bHi;
+            for (int u = 0; u < kUpInline; ++u)
+                m[p][u] = S[p].uinc[u] ? S[p].ubase[u] + 8u * c - 8u : S[p].ubase[u];
+        // lateral inflow of position p at tick j of the chunk, interpolate_sample
+        // (nutils.py:23-33); it does not depend on the routing state (off the tick's chain)
+        auto q_of = [&](int p, int j) -> double {
+            const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
+            double lo, hi;
             if (DENSE && slow) {
-                aLo = Fm[(int64_t)clamp_row(ea.x < 0 ? 0 : ea.x, nrow) * ns + A.d];
-                aHi = Fm[(int64_t)clamp_row(ea.y < 0 ? 0 : ea.y, nrow) * ns + A.d];
-                bLo = Fm[(int64_t)clamp_row(eb.x < 0 ? 0 : eb.x, nrow) * ns + B.d];
-                bHi = Fm[(int64_t)clamp_row(eb.y < 0 ? 0 : eb.y, nrow) * ns + B.d];
+                lo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
+                hi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
             } else {
-                aLo = lds_f64(lds, frpA + 8u * (unsigned)ea.x);
-                aHi = lds_f64(lds, frpA + 8u * (unsigned)ea.y);
-                bLo = lds_f64(lds, frpB + 8u * (unsigned)eb.x);
-                bHi = lds_f64(lds, frpB + 8u * (unsigned)eb.y);
+                lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
+                hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
             }
-            const double fa = __hiloint2double(ea.w, ea.z), fb = __hiloint2double(eb.w, eb.z);
-            const double qa = (1.0 - fa) * aLo + fa * aHi;
-            const double qb = (1.0 - fb) * bLo + fb * bHi;
-            qA[j] = MCR_EXP_NO_Q ? 0.0 : (ea.y < 0 ? aLo : qa);
-            qB[j] = MCR_EXP_NO_Q ? 0.0 : (eb.y < 0 ? bLo : qb);
+            const double f = __hiloint2double(e.w, e.z);
+            const double qq = (1.0 - f) * lo + f * hi;
+            return MCR_EXP_NO_Q ? 0.0 : qq;   // clamped steps: hi = lo, frac = 0
+        };
+        double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
+        if constexpr (kBatchQ) {
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j)
+#pragma unroll
+                for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j);
+            if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
         }
-        if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
 #pragma unroll
         for (int i = 0; i < kChunk; ++i) {
             if (i & 1) {
 #pragma unroll
-                for (int u = 0; u < kUpInline; ++u) {
-                    mA[u] += A.uinc[u];
-                    mB[u] += B.uinc[u];
-                }
+                for (int p = 0; p < K; ++p)
+#pragma unroll
+                    for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uinc[u];
             }
             const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
             const int k = kc + i;
-            // low slot
-            const bool actA = (unsigned)(k - A.G) < (unsigned)T;
-            const double IA = fold<false>(lds, mA, A.self, rd, any3A, 0.0);
-            const double rA = 0.0 + (((A.al * IA + A.be * A.ip) + A.ch * A.op) + A.ga * qA[i]);
-            const double oA = A.psum ? IA : rA;
-            // high slot (may read oA of this tick)
-            const bool actB = (unsigned)(k - B.G) < (unsigned)T;
-            const double IB = fold<true>(lds, mB, B.self, rd, any3B, oA);
-            const double rB = 0.0 + (((B.al * IB + B.be * B.ip) + B.ch * B.op) + B.ga * qB[i]);
-            const double oB = B.psum ? IB : rB;
+            double qv[K];
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                if constexpr (kBatchQ) qv[p] = qb[p][i];
+                else qv[p] = q_of(p, i);
+            }
+            double vin[K][kUpInline];
+#pragma unroll
+            for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
+            double ov[K];
+            double prev = 0.0;
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                const bool act = (unsigned)(k - S[p].G) < (unsigned)T;
+                const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
+                const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
+                                          S[p].ch * S[p].op) + S[p].ga * qv[p]);
+                const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
+                S[p].op = act ? o : S[p].op;
+                S[p].ip = act ? I : S[p].ip;
+                ov[p] = o;
+                prev = o;
+            }
             // inactive ticks write garbage that no active node reads (its consumer is inactive
             // one tick later); never-processed reaches (no consumer) output 0
-            *reinterpret_cast<double*>(lds + ownA + 8u * (i & 1)) = oA;
-            *reinterpret_cast<double*>(lds + ownB + 8u * (i & 1)) = oB;
-            A.op = actA ? oA : A.op;
-            A.ip = actA ? IA : A.ip;
-            B.op = actB ? oB : B.op;
-            B.ip = actB ? IB : B.ip;
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+                *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
             // one contiguous row of RS values per tick; ticks outside the window: dummy row
             const bool inwin = k >= gminw && k < wend;
             double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
             if (!MCR_EXP_NO_STORES) {
-                // non-temporal: rows are written once and read only by later fetches
-                __builtin_nontemporal_store(A.routed ? oA : 0.0, orow + tid);
-                __builtin_nontemporal_store(B.routed ? oB : 0.0, orow + SLOTS + tid);
-                if (A.xsrc && actA) XSm[A.xs0 + k] = oA;
-                if (B.xsrc && actB) XSm[B.xs0 + k] = oB;
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    // non-temporal: rows are written once and read only by later fetches
+                    __builtin_nontemporal_store(ov[p], orow + p * SLOTS + tid);
+                    if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T)
+                        XSm[S[p].xs0 + k] = ov[p];
+                }
             }
             if (!MCR_EXP_NO_BARRIER) __syncthreads();
         }
-        rbA = rbAn;
-        nrA = nrAn;
-        rbB = rbBn;
-        nrB = nrBn;
-        fA0 = gA0;
-        fA1 = gA1;
-        fA2 = gA2;
-        fB0 = gB0;
-        fB1 = gB1;
-        fB2 = gB2;
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            rb[p] = rbn[p];
+            nr[p] = nrn[p];
+            f0[p] = g0[p];
+            f1[p] = g1[p];
+            f2[p] = g2[p];
+        }
     }
     // state for the next launch (slots that did not run keep theirs); never-processed reaches
     // hold o = 0 as in the reference's fresh o_t_next
     const int64_t sb = (int64_t)blockIdx.y * a.mS;
-    a.st_o[sb + A.d] = A.routed || A.psum ? A.op : 0.0;
-    a.st_i[sb + A.d] = A.ip;
-    a.st_o[sb + B.d] = B.routed || B.psum ? B.op : 0.0;
-    a.st_i[sb + B.d] = B.ip;
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        a.st_o[sb + S[p].d] = S[p].op;
+        a.st_i[sb + S[p].d] = S[p].ip;
+    }
     if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
@@ -279,6 +296,24 @@ void wavefront_det(WaveArgs a) {
         rec[3] = (int64_t)__smid();
         rec[4] = c_loop;
         rec[5] = c_end;
+    }
+}
+
+// Device coefficients by slot kind, so that the tick needs no per-slot selects: a partial-sum
+// node computes 0 + (((1 I + 0 Ip) + 0 Op) + 0 q) = I, an unrouted reach (never processed by
+// the reference walk) and a padding slot 0 + (((0 I + 0 Ip) + 0 Op) + 0 q) = +0 -- exact for
+// finite values (the reference keeps o = 0 for unrouted reaches, nutils.py:68)
+__global__ void set_slot_coeffs(const uint8_t* __restrict__ flags, double* __restrict__ alpha,
+                                double* __restrict__ beta, double* __restrict__ chi,
+                                double* __restrict__ gamma, int64_t ns) {
+    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < ns;
+         d += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t f = flags[d];
+        if (f == kSlotRouted) continue;
+        alpha[d] = f == kSlotSum ? 1.0 : 0.0;
+        beta[d] = 0.0;
+        chi[d] = 0.0;
+        gamma[d] = 0.0;
     }
 }
 
@@ -416,23 +451,38 @@ inline int grid_for(int64_t work, int block) {
 }  // namespace
 
 template <bool DENSE>
-hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, size_t lds, int members,
-                              hipStream_t s) {
+hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, int chain, size_t lds,
+                              int members, hipStream_t s) {
     const dim3 g(grid, members);
-    switch (slots) {
-#define MCR_CASE(S) \
-    case S: hipLaunchKernelGGL((wavefront_det<S, DENSE>), g, S, lds, s, a); break;
-        MCR_SLOT_LIST(MCR_CASE)
-#undef MCR_CASE
-        default: return hipErrorInvalidValue;
+#define MCR_CASE(S, K)                                                              \
+    if (slots == S && chain == K) {                                                 \
+        hipLaunchKernelGGL((wavefront_det<S, K, DENSE>), g, S, lds, s, a);          \
+        return hipGetLastError();                                                   \
     }
-    return hipGetLastError();
+    MCR_SLOT_SHAPES(MCR_CASE)
+#undef MCR_CASE
+    return hipErrorInvalidValue;
 }
 
-hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds, bool dense,
-                            int members, hipStream_t s) {
-    return dense ? launch_wavefront_t<true>(a, grid, slots, lds, members, s)
-                 : launch_wavefront_t<false>(a, grid, slots, lds, members, s);
+bool wavefront_shape_ok(int slots, int chain) {
+#define MCR_CASE(S, K) if (slots == S && chain == K) return true;
+    MCR_SLOT_SHAPES(MCR_CASE)
+#undef MCR_CASE
+    return false;
+}
+
+hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, int chain, size_t lds,
+                            bool dense, int members, hipStream_t s) {
+    return dense ? launch_wavefront_t<true>(a, grid, slots, chain, lds, members, s)
+                 : launch_wavefront_t<false>(a, grid, slots, chain, lds, members, s);
+}
+
+hipError_t launch_set_slot_coeffs(const uint8_t* flags, double* alpha, double* beta, double* chi,
+                                  double* gamma, int64_t nslots, hipStream_t s) {
+    if (nslots > 0)
+        hipLaunchKernelGGL(set_slot_coeffs, grid_for(nslots, 256), 256, 0, s, flags, alpha, beta,
+                           chi, gamma, nslots);
+    return hipGetLastError();
 }
 
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,

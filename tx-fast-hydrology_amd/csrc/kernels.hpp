@@ -20,14 +20,22 @@
 
 namespace mcr {
 
-// Workgroup sizes (plan slots) the kernels are instantiated for.
-#define MCR_SLOT_LIST(X) X(64) X(128) X(192) X(256) X(384) X(448) X(512)
+// (lanes, node slots per lane) the kernels are instantiated for (plan slots, chain).
+// Multi-launch sweep:
+#define MCR_SLOT_SHAPES(X)                                                             \
+    X(64, 2) X(128, 2) X(192, 2) X(256, 2) X(384, 2) X(448, 2) X(512, 2) X(64, 3) X(128, 3) \
+    X(192, 3) X(256, 3) X(64, 4) X(128, 4) X(192, 4) X(256, 4)
+// Dataflow kernels (compute waves + the helper wave fill whole wave slots on the SIMDs):
+// (4 positions per lane take one wave per SIMD: at most 192 lanes + the helper)
+#define MCR_FLOW_SHAPES(X)                                                             \
+    X(64, 2) X(128, 2) X(192, 2) X(256, 2) X(384, 2) X(448, 2) X(64, 3) X(128, 3) X(192, 3) \
+    X(256, 3) X(64, 4) X(128, 4) X(192, 4)
 
 // Ticks whose lateral inflow is formed in one burst (and whose forcing rows are prefetched
 // together).  Launch lengths (`tile`) are multiples of it.
 constexpr int kChunk = 8;
 
-// doubles of the out-of-window dummy row per ensemble member (>= 2 * largest slots)
+// doubles of the out-of-window dummy row per ensemble member (>= the widest chain * slots)
 constexpr int64_t kDummyPerMember = 2048;
 
 // Dataflow kernel (flow.hip): external inputs per workgroup it supports, longest step table it
@@ -62,7 +70,7 @@ struct WaveArgs {
     double* st_o;
     double* st_i;
     const double* F;              // forcing rows in slot order [n_rows][nslots]
-    const int4* stab;             // per step {row_lo, row_hi (-1 = copy row_lo), frac (f64)}
+    const int4* stab;             // per step {row_lo, row_hi, frac (f64)}; clamped: {r, r, 0}
     const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
     const int32_t* wg_gmax;
     const int64_t* wbase;         // [nwg] window base of each workgroup in O / I
@@ -89,36 +97,35 @@ struct WaveArgs {
     int32_t ext_cap;              // LDS rows reserved for external inputs
 };
 
-// LDS bytes for `slots` lanes (2 * slots node slots)
-inline size_t wavefront_lds_bytes(int slots, int table_cap, int ext_cap, int tile) {
-    const size_t rs = 2 * (size_t)slots;
+// LDS bytes for `slots` lanes (chain * slots node slots)
+inline size_t wavefront_lds_bytes(int slots, int chain, int table_cap, int ext_cap, int tile) {
+    const size_t rs = (size_t)chain * slots;
     return 16 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
 }
 
-inline size_t flow_lds_bytes(int slots, int T, int ext_cap) {
-    const size_t rs = 2 * (size_t)slots;
+inline size_t flow_lds_bytes(int slots, int chain, int T, int ext_cap) {
+    const size_t rs = (size_t)chain * slots;
     return 16 * (rs + 1) + 24 * rs + 16 * (size_t)T + 2 * (size_t)ext_cap * kChunk * 8 +
            4 * kFlowMaxExt;
 }
 
 // One launch for the whole horizon; grid = every workgroup (all must be co-resident).
-hipError_t launch_flow(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
-                       hipStream_t s);
+hipError_t launch_flow(const WaveArgs& a, int grid, int slots, int chain, size_t lds_bytes,
+                       bool dense, hipStream_t s);
 // Resident workgroups per CU of the dataflow kernel at this LDS size.
-hipError_t flow_occupancy(int slots, bool dense, size_t lds_bytes, int* blocks_per_cu);
+hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds_bytes, int* blocks_per_cu);
 
 // Member dataflow (flow.hip): ONE step of E ensemble members as one resident launch.  Member e
 // of node slot d runs at tick G[d] + e (the members take the place of the steps of a horizon;
 // a.T = E), reading its state from a.IO and its lateral inflow from a.Qm (launch_member_inputs)
 // and writing the member's step-0 outputs into the T = 1 output windows (member stride a.mO);
 // the new session state is then formed from those outputs (launch_state_from_step).
-hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, size_t lds_bytes,
-                               hipStream_t s);
-hipError_t flow_members_occupancy(int slots, size_t lds_bytes, int* blocks_per_cu);
+hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain,
+                               size_t lds_bytes, hipStream_t s);
+hipError_t flow_members_occupancy(int slots, int chain, size_t lds_bytes, int* blocks_per_cu);
 // Inputs of a member-dataflow step, member-major [E][nslots]: IO = {o, i} of the session state
 // (16 B per slot, one load per slot and tick) and Qm = the step's interpolated lateral inflow of
-// the member (the kernels' formula: F[e][lo][d] when ent.y < 0, else
-// (1 - frac) F[e][lo][d] + frac F[e][hi][d]).
+// the member (the kernels' formula: (1 - frac) F[e][lo][d] + frac F[e][hi][d]).
 hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t nslots, int n_rows,
                                 int4 ent, const double* st_o, const double* st_i, double* IO,
                                 double* Qm, int64_t E, hipStream_t s);
@@ -137,9 +144,16 @@ hipError_t launch_state_from_step(const double* O, int64_t mO, const int64_t* jb
 
 // dense: the step table has a kChunk-step window spanning more than 3 forcing rows.
 // members: ensemble members (grid y); member strides are in `a`.
-hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, size_t lds_bytes, bool dense,
-                            int members, hipStream_t s);
+hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, int chain, size_t lds_bytes,
+                            bool dense, int members, hipStream_t s);
+// Is (slots, chain) instantiated for the multi-launch sweep / the dataflow kernels?
+bool wavefront_shape_ok(int slots, int chain);
+bool flow_shape_ok(int slots, int chain);
 
+// Device coefficients by slot kind (partial sums alpha = 1, unrouted reaches and padding 0;
+// kernels.hip set_slot_coeffs), applied after every coefficient upload
+hipError_t launch_set_slot_coeffs(const uint8_t* flags, double* alpha, double* beta, double* chi,
+                                  double* gamma, int64_t nslots, hipStream_t s);
 // Layout conversions between the caller (reach order, member innermost: [n][E]) and the device
 // (slot order, member-major: [E][nslots]).  E = 1 is the deterministic case.
 // dst[e][d] = src[slot_reach[d]][e]  (0 for padding slots)

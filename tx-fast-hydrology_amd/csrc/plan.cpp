@@ -3,6 +3,7 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <array>
 #include <numeric>
 #include <sstream>
 
@@ -17,7 +18,28 @@ struct Cluster {
     int64_t wg = -1;
     int32_t off = 0;        // G offset
     int32_t dmax = 0;       // deepest in-cluster distance to the root
+    int64_t cnt[kMaxChain + 1] = {};   // lane chains by length
 };
+
+// Lanes of `chain` positions needed for chains of the given lengths (cnt[L] chains of length
+// L), packed first-fit decreasing: the packing slot assignment (step 8) performs.
+int64_t lanes_needed(const int64_t* c, int K) {
+    switch (K) {
+        case 1: return c[1];
+        case 2: return c[2] + (c[1] + 1) / 2;
+        case 3: return c[3] + c[2] + (std::max<int64_t>(0, c[1] - c[2]) + 2) / 3;
+        default: {   // 4: a 3-chain leaves one free position, an odd 2-chain two
+            const int64_t free1 = c[3] + (c[2] & 1) * 2;
+            return c[4] + c[3] + (c[2] + 1) / 2 + (std::max<int64_t>(0, c[1] - free1) + 3) / 4;
+        }
+    }
+}
+
+int64_t lanes_sum(const int64_t* a, const int64_t* b, int K) {
+    int64_t s[kMaxChain + 1];
+    for (int L = 0; L <= kMaxChain; ++L) s[L] = a[L] + b[L];
+    return lanes_needed(s, K);
+}
 
 }  // namespace
 
@@ -33,10 +55,12 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     if (C < 64 || C > 512 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 512]";
     if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
     if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";
+    const int K = params.chain;
+    if (K < 1 || K > kMaxChain) return "chain must be in [1, 4]";
     // hard cap of external inputs: what is left of the LDS after the outflow double buffer and
-    // forcing rows of the 2 * slots node slots and the step-table window
+    // forcing rows of the chain * slots node slots and the step-table window
     {
-        const int64_t left = kLdsBudget - 40 * (2 * C + 1) - kTableEntryBytes * table_entries(C, B);
+        const int64_t left = kLdsBudget - 40 * (K * C + 1) - kTableEntryBytes * table_entries(C, B);
         const int64_t hard = std::min<int64_t>(left / (8 * (int64_t)B), 0x7fff);
         if (hard < 1) return "slots/tile too large for the 160 KiB LDS of a workgroup";
         P.ext_hard = (int32_t)hard;
@@ -211,74 +235,99 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (int64_t k = gin_off[x]; k < gin_off[x + 1]; ++k) cons[gin_list[k]] = x;
     for (int64_t x = 0; x < N; ++x) P.max_height = std::max(P.max_height, h[x]);
 
-    // ---- 4. lane pairs -----------------------------------------------------------------
-    // A lane owns two node slots, low (computed first in a tick) and high.  When the high node
-    // consumes the low one the pair is fused: both run step t at the same tick and the high
-    // node takes low's output from a register, so the fused edge costs no tick.  Fusing
-    // alternate edges of a chain halves its depth.  DP over the forest in topological order:
-    // Sx = height of x when it is not the high node of a pair, Fx = height when it is (fused
-    // with its best input fch).  A node is low for at most one pair (it has one consumer).
-    std::vector<int32_t> Sx(N, 0), Fx(N, INT32_MAX), bx(N, 0);
-    std::vector<int64_t> fch(N, -1);
+    // ---- 4. lane chains ----------------------------------------------------------------
+    // A lane owns K = chain node slots (positions), computed in order within a tick.  A node at
+    // position p >= 1 may consume the output of position p - 1 in the same tick (a chained
+    // edge, no tick); every other input arrives from an earlier tick.  A run of up to K
+    // consecutive nodes along a flow path therefore costs one tick (K = 2: fused lane pairs).
+    // Only a node's LAST input in fold order may be chained: the device then folds the other
+    // inputs (the chained code reads the zero slot) and adds the chained value last, which is
+    // the reference's left fold bit for bit and needs no per-input selects (measured on the
+    // Texas network: the same schedule length as chaining any input).
+    // DP over the forest in topological order: F[x][k] = height (ticks) of x at position k of
+    // its chain (k = 0: no chained input), fc[x][k] the chained input achieving it, bx = min
+    // over k.  A node has one consumer, so it is chained into at most one node and the choices
+    // of different consumers never conflict.
+    std::vector<int32_t> F((size_t)N * K, INT32_MAX), bx(N, 0);
+    std::vector<int64_t> fc((size_t)N * K, -1);
     for (int64_t x : nodes) {
         const int64_t k0 = gin_off[x], k1 = gin_off[x + 1];
-        int32_t sx = 0;
-        for (int64_t k = k0; k < k1; ++k) sx = std::max(sx, bx[gin_list[k]] + 1);
-        Sx[x] = sx;
-        for (int64_t k = k0; k < k1; ++k) {
-            int32_t m = Sx[gin_list[k]];
-            for (int64_t q = k0; q < k1; ++q)
-                if (q != k) m = std::max(m, bx[gin_list[q]] + 1);
-            if (m < Fx[x]) {
-                Fx[x] = m;
-                fch[x] = gin_list[k];
+        int32_t* Fx = &F[(size_t)x * K];
+        int32_t s = 0;
+        for (int64_t q = k0; q < k1; ++q) s = std::max(s, bx[gin_list[q]] + 1);
+        Fx[0] = s;
+        for (int k = 1; k < K && k1 > k0; ++k) {
+            const int64_t c = gin_list[k1 - 1];
+            int32_t m = F[(size_t)c * K + k - 1];
+            if (m == INT32_MAX) continue;
+            for (int64_t r = k0; r < k1 - 1; ++r) m = std::max(m, bx[gin_list[r]] + 1);
+            if (m < Fx[k]) {
+                Fx[k] = m;
+                fc[(size_t)x * K + k] = c;
             }
         }
-        bx[x] = std::min(Sx[x], Fx[x]);
+        int32_t b = Fx[0];
+        for (int k = 1; k < K; ++k) b = std::min(b, Fx[k]);
+        bx[x] = b;
     }
-    std::vector<int8_t> role(N, 0);         // 0 single, 1 low of a fused pair, 2 high
-    std::vector<int64_t> mate(N, -1);
+    // positions, downstream first: a node its consumer did not chain takes its best position
+    // (the lowest on ties); below[x] = its chained input, above[x] = the node it is chained into
+    std::vector<int8_t> cpos(N, -1);
+    std::vector<int64_t> below(N, -1), above(N, -1), top(N, -1);
     for (auto it = nodes.rbegin(); it != nodes.rend(); ++it) {
         const int64_t x = *it;
-        if (role[x] == 1 || Fx[x] >= Sx[x]) continue;
-        role[x] = 2;
-        role[fch[x]] = 1;
-        mate[x] = fch[x];
-        mate[fch[x]] = x;
-        P.n_pairs++;
+        int k = cpos[x];
+        if (k < 0) {
+            const int32_t* Fx = &F[(size_t)x * K];
+            k = 0;
+            for (int j = 1; j < K; ++j)
+                if (Fx[j] < Fx[k]) k = j;
+            cpos[x] = (int8_t)k;
+        }
+        if (F[(size_t)x * K + k] == INT32_MAX) return "internal: lane chain position";
+        if (k > 0) {
+            const int64_t c = fc[(size_t)x * K + k];
+            below[x] = c;
+            above[c] = x;
+            cpos[c] = (int8_t)(k - 1);
+            P.n_pairs++;
+        }
+        top[x] = above[x] >= 0 ? top[above[x]] : x;
     }
-    // lane node of every node (a fused pair is represented by its high node), its inputs and
-    // its consumer; a pair's inputs are low's inputs then high's other inputs
-    auto lane_of = [&](int64_t x) { return role[x] == 1 ? mate[x] : x; };
-    std::vector<int64_t> lin_off(N + 1, 0), lin_list;
+    std::vector<int32_t>().swap(F);
+    std::vector<int64_t>().swap(fc);
+    // lane node of every node = the top (most downstream node) of its chain; a lane node's
+    // inputs are the inputs of its chain members, bottom first, without the chained edges.
+    // Every such input is itself the top of its chain (its one consumer did not chain it).
+    auto lane_of = [&](int64_t x) { return top[x]; };
+    std::vector<int64_t> lin_off(N + 1, 0), lin_list, chain_nodes;
     lin_list.reserve(gin_list.size());
     for (int64_t x = 0; x < N; ++x) {
-        if (role[x] != 1) {
-            if (role[x] == 2) {
-                const int64_t u = mate[x];
-                for (int64_t k = gin_off[u]; k < gin_off[u + 1]; ++k)
-                    lin_list.push_back(gin_list[k]);
-            }
-            for (int64_t k = gin_off[x]; k < gin_off[x + 1]; ++k)
-                if (gin_list[k] != mate[x] || role[x] != 2) lin_list.push_back(lane_of(gin_list[k]));
-            if (role[x] == 2)
-                for (int64_t k = lin_off[x]; k < (int64_t)lin_list.size(); ++k)
-                    lin_list[k] = lane_of(lin_list[k]);
+        if (top[x] == x) {
+            chain_nodes.clear();
+            for (int64_t y = x; y >= 0; y = below[y]) chain_nodes.push_back(y);
+            for (auto it = chain_nodes.rbegin(); it != chain_nodes.rend(); ++it)
+                for (int64_t q = gin_off[*it]; q < gin_off[*it + 1]; ++q)
+                    if (gin_list[q] != below[*it]) {
+                        if (top[gin_list[q]] != gin_list[q]) return "internal: lane input";
+                        lin_list.push_back(gin_list[q]);
+                    }
         }
         lin_off[x + 1] = (int64_t)lin_list.size();
     }
     std::vector<int64_t> lnodes;            // lane nodes in topological order
     lnodes.reserve(N);
     for (int64_t x : nodes)
-        if (role[x] != 1) lnodes.push_back(x);
+        if (top[x] == x) lnodes.push_back(x);
     auto lcons = [&](int64_t x) { return cons[x] < 0 ? -1 : lane_of(cons[x]); };
-    auto weight = [&](int64_t x) -> int64_t { return role[x] == 2 ? 2 : 1; };
+    auto weight = [&](int64_t x) -> int64_t { return (int64_t)cpos[x] + 1; };
 
     // ---- 5. clustering (bottom-up greedy) -------------------------------------------------
-    // Each lane node starts a cluster that absorbs the clusters of its inputs while the slot
-    // (2 * slots node slots per workgroup) and external-input budgets allow.  The deepest input
-    // is tried first; a shallow input whose value can arrive `tile` ticks late is cut for free.
-    const int64_t RS = 2 * C;
+    // Each lane node starts a cluster that absorbs the clusters of its inputs while the lane
+    // (`slots` lanes of K positions per workgroup) and external-input budgets allow.  The
+    // deepest input is tried first; a shallow input whose value can arrive `tile` ticks late is
+    // cut for free.
+    const int64_t RS = (int64_t)K * C;
     const int64_t scap = span_cap(C);
     std::vector<int64_t> cl(N, -1);
     std::vector<Cluster> clusters;
@@ -293,6 +342,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         Cluster c;
         c.root = j;
         c.size = weight(j);
+        c.cnt[weight(j)] = 1;
         std::vector<int64_t> absorb;
         int32_t best = ups.empty() ? -1 : eh[ups[0]];
         int32_t ehj = 0;
@@ -304,9 +354,10 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             const bool want = first || (eh[u] + B > best + 1) || (c.ext + 1 > soft);
             first = false;
             // the cluster's tick span (in-cluster depth) must fit one workgroup's window
-            if (want && c.size + cu.size <= RS && c.ext + cu.ext <= hard &&
+            if (want && lanes_sum(c.cnt, cu.cnt, K) <= C && c.ext + cu.ext <= hard &&
                 cu.dmax + 1 <= scap) {
                 c.size += cu.size;
+                for (int L = 1; L <= kMaxChain; ++L) c.cnt[L] += cu.cnt[L];
                 c.ext += cu.ext;
                 c.dmax = std::max(c.dmax, cu.dmax + 1);
                 absorb.push_back(cl[u]);
@@ -382,9 +433,9 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (int64_t v : members[id]) G[v] = c.off + c.dmax - dist[v];
     }
     for (int64_t x = 0; x < N; ++x) {
-        if (role[x] == 1) {
-            G[x] = G[mate[x]];
-            cl[x] = cl[mate[x]];
+        if (top[x] != x) {
+            G[x] = G[top[x]];
+            cl[x] = cl[top[x]];
         }
         P.gmax = std::max(P.gmax, G[x]);
     }
@@ -397,6 +448,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         return clusters[a].off < clusters[b].off;
     });
     std::vector<int64_t> wg_fill, wg_ext, bin_lo, bin_hi;
+    std::vector<std::array<int64_t, kMaxChain + 1>> wg_cnt;
     const int kProbe = 64;  // bounded first fit over the most recent bins keeps packing O(n)
     for (int64_t id : by_off) {
         Cluster& c = clusters[id];
@@ -404,7 +456,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         int64_t w = -1;
         const int64_t nb = (int64_t)wg_fill.size();
         for (int64_t b = std::max<int64_t>(0, nb - kProbe); b < nb; ++b)
-            if (wg_fill[b] + c.size <= RS && wg_ext[b] + c.ext <= std::max<int64_t>(soft, c.ext) &&
+            if (lanes_sum(wg_cnt[b].data(), c.cnt, K) <= C &&
+                wg_ext[b] + c.ext <= std::max<int64_t>(soft, c.ext) &&
                 std::max(bin_hi[b], hi) - std::min(bin_lo[b], lo) <= scap) {
                 w = b;
                 break;
@@ -413,11 +466,13 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             w = nb;
             wg_fill.push_back(0);
             wg_ext.push_back(0);
+            wg_cnt.push_back({});
             bin_lo.push_back(lo);
             bin_hi.push_back(hi);
         }
         wg_fill[w] += c.size;
         wg_ext[w] += c.ext;
+        for (int L = 1; L <= kMaxChain; ++L) wg_cnt[w][L] += c.cnt[L];
         bin_lo[w] = std::min(bin_lo[w], lo);
         bin_hi[w] = std::max(bin_hi[w], hi);
         c.wg = w;
@@ -426,13 +481,13 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     P.nslots = (int64_t)P.nwg * RS;
 
     // ---- 8. slot assignment ----------------------------------------------------------------
-    // node slot of a workgroup: lane + (high ? slots : 0).  Fused pairs take whole lanes, the
-    // other nodes fill the remaining low then high slots; both in order of G, so a wave holds
-    // nodes that are active at the same ticks.
-    std::vector<std::vector<int64_t>> wg_pairs(P.nwg), wg_single(P.nwg);
+    // node slot of a workgroup: position * slots + lane.  The workgroup's chains are packed
+    // into lanes first-fit decreasing (longest first, best fit on the free positions: the
+    // packing lanes_needed counts), a chain on consecutive positions bottom first; lanes are
+    // then ordered by their earliest G, so a wave holds nodes that are active at the same ticks.
+    std::vector<std::vector<int64_t>> wg_chains(P.nwg);
     for (int64_t id : live)
-        for (int64_t v : members[id])
-            (role[v] == 2 ? wg_pairs : wg_single)[clusters[id].wg].push_back(v);
+        for (int64_t v : members[id]) wg_chains[clusters[id].wg].push_back(v);
     P.slot_reach.assign(P.nslots, -1);
     P.G.assign(P.nslots, 0);
     P.flags.assign(P.nslots, kSlotPad);
@@ -453,23 +508,49 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             P.flags[d] = kSlotSum;
         }
     };
-    auto byG = [&](int64_t a, int64_t b) { return G[a] < G[b]; };
+    std::vector<std::vector<int64_t>> lanes;         // nodes of each lane, position order
+    std::vector<int64_t> open[kMaxChain];            // lanes with f free positions
+    std::vector<int64_t> lane_order;
     for (int32_t w = 0; w < P.nwg; ++w) {
-        auto& pr = wg_pairs[w];
-        auto& sg = wg_single[w];
-        std::stable_sort(pr.begin(), pr.end(), byG);
-        std::stable_sort(sg.begin(), sg.end(), byG);
-        const int64_t base = (int64_t)w * RS;
-        int64_t lane = 0;
-        for (int64_t x : pr) {
-            place(mate[x], base + lane);
-            place(x, base + C + lane);
-            ++lane;
+        auto& ch = wg_chains[w];
+        std::stable_sort(ch.begin(), ch.end(), [&](int64_t a, int64_t b) {
+            return weight(a) != weight(b) ? weight(a) > weight(b) : G[a] < G[b];
+        });
+        lanes.clear();
+        for (auto& o : open) o.clear();
+        for (int64_t t : ch) {
+            const int L = (int)weight(t);
+            int64_t ln = -1;
+            for (int f = L; f < K && ln < 0; ++f)
+                if (!open[f].empty()) {
+                    ln = open[f].back();
+                    open[f].pop_back();
+                }
+            if (ln < 0) {
+                ln = (int64_t)lanes.size();
+                lanes.emplace_back();
+            }
+            const size_t at = lanes[ln].size();
+            for (int64_t y = t; y >= 0; y = below[y]) lanes[ln].push_back(y);
+            std::reverse(lanes[ln].begin() + at, lanes[ln].end());   // bottom first
+            const int f = K - (int)lanes[ln].size();
+            if (f > 0) open[f].push_back(ln);
         }
-        if ((int64_t)pr.size() * 2 + (int64_t)sg.size() > RS) return "internal: workgroup overfull";
-        size_t k = 0;
-        for (int64_t l = lane; l < C && k < sg.size(); ++l) place(sg[k++], base + l);
-        for (int64_t l = lane; l < C && k < sg.size(); ++l) place(sg[k++], base + C + l);
+        if ((int64_t)lanes.size() > C) return "internal: workgroup overfull";
+        lane_order.resize(lanes.size());
+        std::vector<int32_t> lane_g(lanes.size(), INT32_MAX);
+        for (size_t l = 0; l < lanes.size(); ++l) {
+            lane_order[l] = (int64_t)l;
+            for (int64_t x : lanes[l]) lane_g[l] = std::min(lane_g[l], G[x]);
+        }
+        std::stable_sort(lane_order.begin(), lane_order.end(),
+                         [&](int64_t a, int64_t b) { return lane_g[a] < lane_g[b]; });
+        const int64_t base = (int64_t)w * RS;
+        for (size_t l = 0; l < lane_order.size(); ++l) {
+            const auto& nodes_l = lanes[lane_order[l]];
+            for (size_t p = 0; p < nodes_l.size(); ++p)
+                place(nodes_l[p], base + (int64_t)p * C + (int64_t)l);
+        }
         int32_t lo = INT32_MAX, hi = INT32_MIN;
         for (int64_t d = base; d < base + RS; ++d)
             if (P.flags[d] != kSlotPad) {
@@ -497,8 +578,9 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         for (int64_t k = k0; k < k1; ++k) {
             const int64_t u = gin_list[k];
             uint16_t code;
-            if (role[j] == 2 && u == mate[j]) {
-                if (npos[u] != d - C || G[u] != G[j]) return "internal: fused pair layout";
+            if (u == below[j]) {
+                if (npos[u] != d - C || G[u] != G[j]) return "internal: lane chain layout";
+                if (k != k1 - 1) return "internal: chained input is not the last input";
                 code = kSelfCode;
             } else if (cl[u] == cl[j]) {
                 if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";

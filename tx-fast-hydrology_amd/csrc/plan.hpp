@@ -27,10 +27,17 @@
 namespace mcr {
 
 struct PlanParams {
-    int32_t slots = 256;       // reaches (threads) per workgroup
+    int32_t slots = 256;       // lanes (threads) per workgroup
     int32_t tile = 32;         // ticks per launch; also the slack of a cross-cluster edge
     int32_t ext_cap = 64;      // preferred max cross-cluster inputs per workgroup (soft)
+    int32_t chain = 2;         // node slots per lane (positions 0 .. chain-1, see "lane chains")
 };
+
+// Lane chains: a lane owns `chain` node slots (positions), computed in order within one tick;
+// a node at position p >= 1 may take the output of position p - 1 of the SAME tick (a chained
+// edge, no tick), so a run of up to `chain` consecutive reaches along a flow path costs one
+// tick.  Node slot of (workgroup w, position p, lane l) = w * chain * slots + p * slots + l.
+constexpr int kMaxChain = 4;
 
 // LDS of one workgroup (bytes): outflow double buffer, step-table window, external inputs.
 constexpr int64_t kLdsBudget = 160 * 1024;
@@ -41,7 +48,7 @@ constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 
 // upstream code: bit 15 set -> index into the workgroup's external-input list, else the
 // workgroup-local slot of the upstream reach.
 constexpr uint16_t kExtBit = 0x8000;
-// code of a fused pair's low node in its high node's list: low's output of the same tick
+// code of a chained input: the output of the lane's previous position in the same tick
 constexpr uint16_t kSelfCode = 0x7fff;
 constexpr int kUpInline = 4;  // upstream values one lane reads per tick (codes in registers)
 
@@ -63,7 +70,7 @@ struct Plan {
     int64_t n_cross = 0;           // cross-cluster edges
     int32_t max_height = 0;        // longest upstream path (levels - 1, partial sums included)
     int64_t n_partial = 0;         // partial-sum nodes
-    int64_t n_pairs = 0;           // fused lane pairs
+    int64_t n_pairs = 0;           // chained edges (chain = 2: fused lane pairs)
     int32_t max_ext_wg = 0;
     int32_t ext_hard = 0;          // LDS-derived hard cap of cross-cluster inputs per workgroup
     int32_t max_span = 0;          // max G span inside one workgroup

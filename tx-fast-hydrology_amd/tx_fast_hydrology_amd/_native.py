@@ -38,7 +38,7 @@ class TopologyError(RoutingError, ValueError):
 
 class PlanParams(ctypes.Structure):
     _fields_ = [("slots", ctypes.c_int32), ("tile", ctypes.c_int32),
-                ("ext_cap", ctypes.c_int32)]
+                ("ext_cap", ctypes.c_int32), ("chain", ctypes.c_int32)]
 
 
 class PlanInfo(ctypes.Structure):
@@ -48,7 +48,8 @@ class PlanInfo(ctypes.Structure):
                 ("tile", ctypes.c_int32), ("gmax", ctypes.c_int32),
                 ("max_height", ctypes.c_int32), ("max_ext_wg", ctypes.c_int32),
                 ("n_partial", ctypes.c_int64), ("n_ext", ctypes.c_int64),
-                ("n_pairs", ctypes.c_int64)]
+                ("n_pairs", ctypes.c_int64), ("chain", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -16,14 +16,14 @@ from . import _native as nat
 from ._native import f64, i64, ptr
 
 
-def _params(slots=0, tile=0, ext_cap=0):
-    return nat.PlanParams(int(slots), int(tile), int(ext_cap))
+def _params(slots=0, tile=0, ext_cap=0, chain=0):
+    return nat.PlanParams(int(slots), int(tile), int(ext_cap), int(chain))
 
 
 class Plan:
     """Compiled schedule of a network (no device memory)."""
 
-    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0):
+    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, chain=0):
         L = nat.lib()
         self._end = i64(endnodes)
         self._deg = i64(indegree)
@@ -32,7 +32,7 @@ class Plan:
         if self._deg.size != self.n:
             raise ValueError("indegree and endnodes must have the same length")
         h = ctypes.c_void_p()
-        p = _params(slots, tile, ext_cap)
+        p = _params(slots, tile, ext_cap, chain)
         nat.check(L.mc_plan_create(self.n, ptr(self._end), ptr(self._deg), ptr(self._heads),
                                    self._heads.size, ctypes.byref(p), ctypes.byref(h)))
         self._h = h
@@ -97,7 +97,8 @@ class RoutingNet:
     (member innermost), forcing [n_rows, n, E], step-major outputs [T, n, E] (mcroute.h).
     """
 
-    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, members=1):
+    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, members=1,
+                 chain=0):
         L = nat.lib()
         end = i64(endnodes)
         deg = i64(indegree)
@@ -110,7 +111,7 @@ class RoutingNet:
             # 3 compute waves + the dataflow helper: one wave per SIMD (Texas det horizon 0.61 ms
             # vs 0.66 at 384 lanes and 0.82 through the multi-launch path at 256)
             slots = 192
-        p = _params(slots, tile, ext_cap)
+        p = _params(slots, tile, ext_cap, chain)
         nat.check(L.mc_net_create(self.n, ptr(end), ptr(deg), ptr(heads), heads.size,
                                   ctypes.byref(p), ctypes.byref(h)))
         self._h = h
