@@ -44,7 +44,8 @@ struct Slot {
     bool routed, psum, xsrc;
     double al, be, ch, ga, op, ip;
     int cnt;
-    unsigned ubase[kUpInline], uinc[kUpInline];
+    unsigned ubase[kUpInline];  // LDS byte base of each input
+    bool uext[kUpInline];       // input from another cluster (XE region)
     bool chained;          // the last input is the lane's previous position of this tick
     int64_t xs0;           // XS address of tick 0 when the slot feeds another cluster
 };
@@ -75,9 +76,11 @@ __device__ __forceinline__ void load_slot(Slot& s, const WaveArgs& a, int64_t d,
 }
 
 // input codes -> LDS byte bases; unused codes read the zero slot (adding +0.0 to a sum that
-// started as a published value is exact, so the sum needs no predicate)
+// started as a published value is exact, so the sum needs no predicate).  xb_stride: bytes
+// between consecutive node slots' outputs; ext_stride: between external inputs.
 template <int RS>
-__device__ __forceinline__ void decode_codes(Slot& s, uint64_t up4, unsigned XB, unsigned XE,
+__device__ __forceinline__ void decode_codes(Slot& s, uint64_t up4, unsigned XB,
+                                             unsigned xb_stride, unsigned XE,
                                              unsigned ext_stride) {
 #pragma unroll
     for (int u = 0; u < kUpInline; ++u) {
@@ -88,23 +91,23 @@ __device__ __forceinline__ void decode_codes(Slot& s, uint64_t up4, unsigned XB,
             code = RS;
         }
         const bool ext = (code & kExtBit) != 0;
-        s.ubase[u] = ext ? XE + (code & 0x7fffu) * ext_stride : XB + code * 16;
-        s.uinc[u] = ext ? 16u : 0u;
+        s.ubase[u] = ext ? XE + (code & 0x7fffu) * ext_stride : XB + code * xb_stride;
+        s.uext[u] = ext;
     }
 }
 
-// The input values of one slot for this tick (previous-tick outputs in the LDS double buffer,
-// parity rd).  A lane reads the inputs of ALL its positions before it writes any output: the
-// compiler cannot prove that a position's LDS write does not alias the next position's reads,
-// so reads issued after it would wait for it (one LDS round trip per position per tick).
-// any3 (wave-uniform): some slot of the wave has more than 2 inputs.
-__device__ __forceinline__ void read_inputs(const char* lds, const unsigned* m, unsigned rd,
+// The input values of one slot for this tick (byte offset `off` from the bases m).  A lane reads the inputs of ALL its
+// positions before it writes any output: the compiler cannot prove that a position's LDS
+// write does not alias the next position's reads, so reads issued after it would wait for it
+// (one LDS round trip per position per tick).  any3 (wave-uniform): some slot of the wave has
+// more than 2 inputs.
+__device__ __forceinline__ void read_inputs(const char* lds, const unsigned* m, unsigned off,
                                             bool any3, double* v) {
-    v[0] = lds_f64(lds, m[0] + rd);
-    v[1] = lds_f64(lds, m[1] + rd);
+    v[0] = lds_f64(lds, m[0] + off);
+    v[1] = lds_f64(lds, m[1] + off);
     if (any3) {
-        v[2] = lds_f64(lds, m[2] + rd);
-        v[3] = lds_f64(lds, m[3] + rd);
+        v[2] = lds_f64(lds, m[2] + off);
+        v[3] = lds_f64(lds, m[3] + off);
     } else {
         v[2] = v[3] = 0.0;
     }

@@ -75,7 +75,7 @@ __device__ __forceinline__ void sleep_backoff(int& sl) {
 struct Helper {
     const char* lds;
     __amdgpu_buffer_rsrc_t xg;
-    unsigned XE, XSLOT, EG;
+    unsigned XE, XSLOT, EG, PL;   // XE: first external column byte; XSLOT: one ring slot's columns
     int lane, e0, nitems, T;
     unsigned epoch;
     int32_t* status;
@@ -100,6 +100,8 @@ struct Helper {
         }
     }
     // write the batch to LDS; returns the first (lane-local) item whose tag is stale, or -1
+    // item idx = (external input e = idx / kChunk, chunk tick j = idx % kChunk) is staged in
+    // tick plane (j + 7) & 7, column e of the ring slot (tick planes, see wavefront_flow)
     __device__ __forceinline__ int consume(int b, int kn, unsigned slot,
                                            const u32x4 (&g)[kBatch]) const {
         int bad = -1;
@@ -112,7 +114,9 @@ struct Helper {
             const uint64_t bits = ((uint64_t)g[k].z << 32) | g[k].x;
             const double v = need ? __longlong_as_double((long long)bits) : 0.0;
             if (idx < nitems)
-                *reinterpret_cast<double*>(const_cast<char*>(lds) + XE + slot * XSLOT + idx * 8) = v;
+                *reinterpret_cast<double*>(const_cast<char*>(lds) + XE + slot * XSLOT +
+                                           (unsigned)(idx >> 3) * 8u +
+                                           (unsigned)(((idx & 7) + 7) & 7) * PL) = v;
             if (need && !cur && bad < 0) bad = k;
         }
         return bad;
@@ -153,8 +157,14 @@ struct Helper {
 };
 
 // LDS layout (bytes), RS = K * SLOTS node slots (lane l: slots p * SLOTS + l, p < K):
-//   XB [RS + 1][2] f64 | FR [RS][3] f64 | TAB [T] int4 (whole step table)
-//   | XE [2][ext_cap][kChunk] f64 (ring of external inputs, one slot per chunk parity)
+//   PLANES [8][RS + 1 + 2 * kFlowMaxExt] f64 | FR [RS][3] f64 | TAB [T] int4 (whole step
+//   table) | EG [kFlowMaxExt] i32 (consumer G)
+// Tick planes: plane k & 7 holds every node slot's output of tick k (column d; column RS is
+// the zero slot) and, in columns RS + 1 + s * kFlowMaxExt + e, the value external input e
+// delivers at chunk tick i (plane (i + 7) & 7) for chunk ring slot s (chunk parity).  At chunk
+// tick i a slot reads plane (i + 7) & 7 of EVERY input: one compile-time LDS offset per
+// unrolled tick, no per-tick address arithmetic, and consecutive node slots are consecutive
+// 8-byte words (bank-conflict-free neighbour reads).
 //   | EG [kFlowMaxExt] i32 (consumer G)
 // Each tick a lane routes its K positions in order; position p may take the output of position
 // p - 1 of the same tick (a chained edge, plan.hpp "lane chains").
@@ -167,13 +177,15 @@ __attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
 void wavefront_flow(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int RS = K * SLOTS;
-    constexpr unsigned XB = 0;
-    constexpr unsigned FR = XB + (RS + 1) * 16;
+    constexpr unsigned PL = flow_plane_bytes(RS);
+    static_assert(7 * PL < 65536, "tick-plane offsets must fit the 16-bit LDS immediate");
+    constexpr unsigned XB = 0;                          // node-slot columns of plane 0
+    constexpr unsigned XE = XB + (RS + 1) * 8;          // external columns of plane 0
+    constexpr unsigned XSLOT = kFlowMaxExt * 8;         // one chunk ring slot of them
+    constexpr unsigned FR = 8 * PL;
     constexpr unsigned TAB = FR + RS * 24;
     const int T = a.T;
-    const unsigned XE = TAB + (unsigned)a.table_cap * 16;
-    const unsigned XSLOT = (unsigned)a.ext_cap * kChunk * 8;
-    const unsigned EG = XE + 2 * XSLOT;
+    const unsigned EG = TAB + (unsigned)a.table_cap * 16;
     double* xbp = reinterpret_cast<double*>(lds + XB);
     int4* tab = reinterpret_cast<int4*>(lds + TAB);
 
@@ -193,13 +205,13 @@ void wavefront_flow(WaveArgs a) {
         for (int idx = tid; idx < T; idx += nthr) tab[idx] = a.stab[idx];
     for (int idx = tid; idx < next; idx += nthr)
         reinterpret_cast<int*>(lds + EG)[idx] = a.ext_g[e0 + idx];
-    if (tid < 2) xbp[RS * 2 + tid] = 0.0;
+    if (tid < 8) xbp[(tid * PL) / 8 + RS] = 0.0;       // zero slot of every plane
 
     const int wave = tid >> 6;
     constexpr int kHW = SLOTS / 64;                     // the helper is the last wave
     if (wave == kHW) {
         // ================================ helper wave ================================
-        Helper h{lds, xg, XE, XSLOT, EG, tid & 63, e0, next * kChunk, T, a.epoch, a.status,
+        Helper h{lds, xg, XE, XSLOT, EG, PL, tid & 63, e0, next * kChunk, T, a.epoch, a.status,
                  false};
         const int nb = (h.nitems + kBatchItems - 1) / kBatchItems;   // <= 2 (host-checked)
         __builtin_amdgcn_s_waitcnt(0);
@@ -246,7 +258,7 @@ void wavefront_flow(WaveArgs a) {
     for (int p = 0; p < K; ++p) {
         load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + lid, 0, kb, wend - kb, T);
         up[p] = a.up4[S[p].d];
-        xbp[(p * SLOTS + lid) * 2 + ((kb - 1) & 1)] = S[p].op;
+        xbp[(((kb - 1) & 7) * PL) / 8 + p * SLOTS + lid] = S[p].op;
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();                                    // LDS tables staged
@@ -255,9 +267,9 @@ void wavefront_flow(WaveArgs a) {
     unsigned own[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        decode_codes<RS>(S[p], up[p], XB, XE, kChunk * 8);
+        decode_codes<RS>(S[p], up[p], XB, 8u, XE, 8u);
         any3[p] = __any(S[p].cnt > 2);
-        own[p] = XB + (unsigned)(p * SLOTS + lid) * 16;
+        own[p] = XB + (unsigned)(p * SLOTS + lid) * 8u;
     }
 
     const unsigned epoch = a.epoch;
@@ -295,16 +307,10 @@ void wavefront_flow(WaveArgs a) {
             for (int p = 0; p < K; ++p)
 #pragma unroll
                 for (int u = 0; u < kUpInline; ++u)
-                    m[p][u] = S[p].uinc[u] ? S[p].ubase[u] + sb - 8u : S[p].ubase[u];
+                    m[p][u] = S[p].uext[u] ? S[p].ubase[u] + sb : S[p].ubase[u];
 #pragma unroll
             for (int i = 0; i < kChunk; ++i) {
-                if (i & 1) {
-#pragma unroll
-                    for (int p = 0; p < K; ++p)
-#pragma unroll
-                        for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uinc[u];
-                }
-                const unsigned rd = 8u * ((i + 1) & 1);
+                const unsigned rd = (unsigned)((i + 7) & 7) * PL;   // plane of tick k - 1
                 const int k = kc + i;
                 const int r = i % kRing;
                 double vin[K][kUpInline];
@@ -324,7 +330,7 @@ void wavefront_flow(WaveArgs a) {
                 }
 #pragma unroll
                 for (int p = 0; p < K; ++p)
-                    *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
+                    *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
 #pragma unroll
                 for (int p = 0; p < K; ++p) {   // refill this ring slot with tick k + kRing
                     int f = k + kRing - S[p].G;
@@ -401,7 +407,7 @@ void wavefront_flow(WaveArgs a) {
             for (int p = 0; p < K; ++p)
 #pragma unroll
                 for (int u = 0; u < kUpInline; ++u)
-                    m[p][u] = S[p].uinc[u] ? S[p].ubase[u] + sb - 8u : S[p].ubase[u];
+                    m[p][u] = S[p].uext[u] ? S[p].ubase[u] + sb : S[p].ubase[u];
             auto q_of = [&](int p, int j) -> double {
                 const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
                 double lo, hi;
@@ -426,13 +432,7 @@ void wavefront_flow(WaveArgs a) {
             }
 #pragma unroll
             for (int i = 0; i < kChunk; ++i) {
-                if (i & 1) {
-#pragma unroll
-                    for (int p = 0; p < K; ++p)
-#pragma unroll
-                        for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uinc[u];
-                }
-                const unsigned rd = 8u * ((i + 1) & 1);
+                const unsigned rd = (unsigned)((i + 7) & 7) * PL;   // plane of tick k - 1
                 const int k = kc + i;
                 double qv[K];
 #pragma unroll
@@ -460,7 +460,7 @@ void wavefront_flow(WaveArgs a) {
                 }
 #pragma unroll
                 for (int p = 0; p < K; ++p)
-                    *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
+                    *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
                 const bool inwin = k >= gminw && k < wend;
                 double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
 #pragma unroll

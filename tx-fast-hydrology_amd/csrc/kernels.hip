@@ -140,7 +140,7 @@ void wavefront_det(WaveArgs a) {
     unsigned own[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        decode_codes<RS>(S[p], up[p], XB, XE, (unsigned)tile * 8);
+        decode_codes<RS>(S[p], up[p], XB, 16u, XE, (unsigned)tile * 8);
         any3[p] = __any(S[p].cnt > 2);                  // wave-uniform
         own[p] = XB + (unsigned)(p * SLOTS + tid) * 16;
     }
@@ -193,7 +193,7 @@ void wavefront_det(WaveArgs a) {
         for (int p = 0; p < K; ++p)
 #pragma unroll
             for (int u = 0; u < kUpInline; ++u)
-                m[p][u] = S[p].uinc[u] ? S[p].ubase[u] + 8u * c - 8u : S[p].ubase[u];
+                m[p][u] = S[p].uext[u] ? S[p].ubase[u] + 8u * c - 8u : S[p].ubase[u];
         // lateral inflow of position p at tick j of the chunk, interpolate_sample
         // (nutils.py:23-33); it does not depend on the routing state (off the tick's chain)
         auto q_of = [&](int p, int j) -> double {
@@ -224,7 +224,7 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
                 for (int p = 0; p < K; ++p)
 #pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uinc[u];
+                    for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uext[u] ? 16u : 0u;
             }
             const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
             const int k = kc + i;

@@ -100,13 +100,17 @@ struct WaveArgs {
 // LDS bytes for `slots` lanes (chain * slots node slots)
 inline size_t wavefront_lds_bytes(int slots, int chain, int table_cap, int ext_cap, int tile) {
     const size_t rs = (size_t)chain * slots;
-    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
+    return 64 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
 }
 
+// dataflow kernel tick plane (flow.hip): every node slot, the zero slot and two chunk ring
+// slots of external inputs, 8 bytes each
+constexpr unsigned flow_plane_bytes(int rs) { return (unsigned)(rs + 1 + 2 * kFlowMaxExt) * 8u; }
+
 inline size_t flow_lds_bytes(int slots, int chain, int T, int ext_cap) {
+    (void)ext_cap;                               // external columns are sized for kFlowMaxExt
     const size_t rs = (size_t)chain * slots;
-    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)T + 2 * (size_t)ext_cap * kChunk * 8 +
-           4 * kFlowMaxExt;
+    return 8 * (size_t)flow_plane_bytes((int)rs) + 24 * rs + 16 * (size_t)T + 4 * kFlowMaxExt;
 }
 
 // One launch for the whole horizon; grid = every workgroup (all must be co-resident).
