@@ -210,6 +210,13 @@ int mc_reset_timing(void* net);
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);
 
+/* How long a dataflow wait polls a stale upstream value before it gives up, in ticks of the
+ * device's 100 MHz wall clock (0 = the default 2 s; < 0 = give up at once, for tests).  A run
+ * whose wait gave up is detected at the next synchronising call: when it was the only
+ * dataflow run since the previous one, the library routes the same horizon again from its
+ * input state with launches (last_path then reads 1); otherwise that call fails (MC_E_HIP). */
+int mc_set_flow_patience(void* net, int64_t wall_ticks);
+
 /* Launch trace of the last mc_run (off by default; diagnostic).  One record of 8 int64 per
  * workgroup per launch: {launch, workgroup, t_start, t_loop, t_end, hw_id, c_loop, c_end}.
  * t_* are ticks of the device's constant wall clock (clock_khz); t_loop is the end of the launch

@@ -388,3 +388,39 @@ def test_texas_scale_lane_chains_bitexact(exec_mode, chain, slots):
     assert net.mode()[1] == ("launches" if exec_mode == "launches" else "dataflow")
     assert np.array_equal(got_o, want_o)
     assert np.array_equal(got_i, want_i)
+
+
+def test_dataflow_give_up_reroutes_with_launches():
+    """A dataflow run whose waits give up (forced here: patience < 0 gives up at the first stale
+    upstream value) is re-routed from its input state with launches at the next synchronising
+    call -- outputs and final state stay bit-exact; two such runs before a synchronisation
+    cannot be recovered and raise."""
+    from tx_fast_hydrology_amd import _native as nat
+    end = synthetic.texas(seed=0)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=0)
+    indeg, heads, coef, _, i0 = _model(end, K, X, 300.0, o0=o0)
+    xp, fp = synthetic.forcing(n, rows=25, seed=1)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 289)
+    want_o, want_i, fo, fi = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=192, tile=16)
+    net.set_mode("auto")
+    net.set_flow_patience(-1)
+    net.load_forcing(xp, fp)
+    net.run(x)
+    got_o, got_i = net.fetch_outputs()
+    assert net.mode()[1] == "launches"             # the give-up was detected and re-routed
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+    so, si = net.get_state()
+    assert np.array_equal(so, fo) and np.array_equal(si, fi)
+    net.set_state(o0, i0)
+    net.run(x)
+    net.run(x)
+    with pytest.raises(nat.RoutingError):
+        net.fetch_outputs()
+    net.set_flow_patience(0)
+    net.set_state(o0, i0)
+    net.run(x)
+    got_o, _ = net.fetch_outputs()
+    assert net.mode()[1] == "dataflow" and np.array_equal(got_o, want_o)

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -96,6 +97,7 @@ struct Net {
     DBuf<int64_t> slot_reach, pos;
     // coefficients / state (slot order)
     DBuf<double> alpha, beta, chi, gamma, st_o, st_i;
+    DBuf<double> st_o2, st_i2;     // input state of the last dataflow horizon (re-run source)
     // forcing (slot order) and single-step forcing
     DBuf<double> F, Fstep, stage, Qm;   // Qm: member lateral inflows of a member-dataflow step
     int64_t n_rows = 0;
@@ -160,8 +162,19 @@ struct Net {
     size_t xg_words = 0;
     uint32_t epoch = 0;
     DBuf<int32_t> status;
-    int32_t* status_host = nullptr;  // pinned mirror, valid after a sync
-    bool status_pending = false;
+    int32_t* status_host = nullptr;  // pinned mirror, read at sync()
+    int flow_runs = 0;               // dataflow launches since the status word was last read
+    // the last dataflow horizon of one member, re-routed with launches when its waits gave up
+    // (st_o2 / st_i2 hold its input state until the next dataflow run)
+    struct FlowRun {
+        bool valid = false;
+        int64_t T = 0, rows = 0;
+        const double* F = nullptr;
+        std::vector<int4> tab;
+    } last_flow;
+    std::vector<int4> stab_host;     // step table last uploaded to stab
+    int force_mode = -1;             // >= 0: mode override during a re-run
+    int64_t patience = mcr::kFlowPatience;   // dataflow waits (mc_set_flow_patience)
 
     // launch trace (mc_set_trace)
     bool trace = false;
@@ -280,20 +293,43 @@ struct Net {
                                          "unchanged by that analysis");
             }
         }
-        if (status_pending) {
-            status_pending = false;
+        if (flow_runs > 0) {
+            // the status word is sticky: read once per sync, not once per run
+            const int runs = flow_runs;
+            flow_runs = 0;
+            HIPC(hipMemcpy(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost));
             if (*status_host != 0) {
                 *status_host = 0;
                 HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
+                if (runs == 1 && last_flow.valid) {
+                    // the device was shared (another stream held CUs the resident launch
+                    // needed): route the same horizon again from its input state with launches
+                    st_o.swap(st_o2);
+                    st_i.swap(st_i2);
+                    last_flow.valid = false;
+                    std::fprintf(stderr, "[mcroute] dataflow launch gave up waiting for upstream "
+                                         "workgroups; the horizon was re-routed with launches\n");
+                    force_mode = 1;
+                    try {
+                        run_tables(last_flow.T, last_flow.F, last_flow.rows, last_flow.tab);
+                    } catch (...) {
+                        force_mode = -1;
+                        throw;
+                    }
+                    force_mode = -1;
+                    HIPC(hipStreamSynchronize(stream));
+                    return;
+                }
                 throw Fail(MC_E_HIP, "dataflow kernel: a wait for upstream results gave up "
-                                     "(outputs of the last run are invalid)");
+                                     "(outputs of the runs since the last synchronisation are "
+                                     "invalid)");
             }
         }
     }
 
     // Can the whole horizon run as one dataflow launch?  Every workgroup must be resident.
     bool flow_fits(int64_t T, bool dense, size_t& lds) {
-        if (mode == 1) return false;
+        if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
         const size_t xg = plan.ext_src.size() * (size_t)T * 16;
         lds = mcr::flow_lds_bytes(S, Kc, (int)T, plan.max_ext_wg);
@@ -313,7 +349,7 @@ struct Net {
 
     // Can one step of all E members run as one member-dataflow launch?
     bool members_fit(size_t& lds) {
-        if (mode == 1) return false;
+        if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
         const size_t xg = plan.ext_src.size() * (size_t)E * 16;
         lds = mcr::flow_lds_bytes(S, Kc, 0, plan.max_ext_wg);
@@ -337,9 +373,15 @@ struct Net {
                             stream));
         HIPC(mcr::launch_scatter_to_slots(stage.p, dst.p, slot_reach.p, plan.nslots, m, stream));
     }
+    // Resolve pending dataflow runs (status word, re-run on give-up) before results are read.
+    void settle() {
+        if (flow_runs > 0) sync();
+    }
+
     void from_slots(const DBuf<double>& src, double* host, int64_t m = 1) {
         const int64_t n = plan.n;
         if (n == 0) return;
+        settle();
         stage.reserve((size_t)(n * m));
         HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, plan.nslots, m, stream));
         HIPC(hipMemcpyAsync(host, stage.p, n * m * sizeof(double), hipMemcpyDeviceToHost,
@@ -678,7 +720,10 @@ struct Net {
             const int last = std::max(tabh[t2].x, tabh[t2].y);
             dense = last - tabh[t].x + 1 > 3;
         }
-        upload_async(stab, tabh.data(), tabh.size());
+        if (tabh != stab_host) {           // repeated horizons reuse the uploaded table
+            upload_async(stab, tabh.data(), tabh.size());
+            stab_host = tabh;
+        }
         last_path = 0;
         ensure_schedule(T);
         const int64_t nl = (int64_t)cur->off.size() - 1;
@@ -744,6 +789,7 @@ struct Net {
             a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
             a.epoch = epoch;
             a.status = status.p;
+            a.patience = patience;
             a.table_cap = 0;
             a.active = all_wg.p;
             if (trace) {
@@ -759,9 +805,8 @@ struct Net {
             HIPC(mcr::launch_member_unpack(IOp, flags.p, G.p, wg_gmin.p, cur->wbase.p,
                                            row_width(), O.p, cur->Otot, st_o.p, st_i.p,
                                            plan.nslots, E, stream));
-            HIPC(hipMemcpyAsync(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                stream));
-            status_pending = true;
+            ++flow_runs;
+            last_flow.valid = false;       // member runs update the state in place
             launched = 1;
             last_path = 2;
             a.T = (int32_t)T;
@@ -783,6 +828,7 @@ struct Net {
             a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
             a.epoch = epoch;
             a.status = status.p;
+            a.patience = patience;
             a.table_cap = (int32_t)T;
             a.active = all_wg.p;
             if (trace) {
@@ -791,13 +837,24 @@ struct Net {
                 trace_launch.assign(plan.nwg, 0);
                 for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
             }
+            // the horizon's final state goes to the spare buffers, which then become the
+            // session state; the input state stays in the old ones (re-run source, sync())
+            st_o2.reserve(st_o.cap);
+            st_i2.reserve(st_i.cap);
+            a.st_o_out = st_o2.p;
+            a.st_i_out = st_i2.p;
             if (timing) HIPC(hipEventRecord(events[0], stream));
             HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, plan.p.chain, flds, dense,
                                   stream));
             if (timing) HIPC(hipEventRecord(events[1], stream));
-            HIPC(hipMemcpyAsync(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                stream));
-            status_pending = true;
+            st_o.swap(st_o2);
+            st_i.swap(st_i2);
+            ++flow_runs;
+            last_flow.valid = true;
+            last_flow.T = T;
+            last_flow.F = Fsrc;
+            last_flow.rows = rows;
+            last_flow.tab = tabh;
             launched = 1;
             last_path = 2;
         }
@@ -894,6 +951,7 @@ struct Net {
     }
 
     void fetch(int64_t t0, int64_t t1, double* oo, double* io) {
+        settle();
         REQUIRE(T_out > 0, "no outputs: call mc_run first");
         REQUIRE(0 <= t0 && t0 <= t1 && t1 <= T_out, "step range out of bounds");
         const int64_t n = plan.n;
@@ -912,6 +970,7 @@ struct Net {
     }
 
     void fetch_series(double* oo, double* io) {
+        settle();
         REQUIRE(T_out > 0, "no outputs: call mc_run first");
         const int64_t n = plan.n;
         if (n == 0) return;
@@ -1130,6 +1189,7 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         REQUIRE(D->E == S->E, "sessions hold different member counts");
         const int64_t n = D->plan.n, E = D->E;
         if (n == 0) return;
+        S->settle();
         // order: after the source's pending work, on the destination's stream; the source waits
         // for the copy before it may overwrite its state again
         hipEvent_t ev;
@@ -1219,6 +1279,13 @@ int mc_set_mode(void* net, int mode) {
     return guarded([&] {
         REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
         as_net(net)->mode = mode;
+    });
+}
+
+int mc_set_flow_patience(void* net, int64_t wall_ticks) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        N->patience = wall_ticks == 0 ? mcr::kFlowPatience : std::max<int64_t>(wall_ticks, 0);
     });
 }
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -77,6 +78,10 @@ struct DBuf {
     void upload(const T* src, size_t k, hipStream_t s) {
         reserve(k);
         if (k) HIPC(hipMemcpyAsync(p, src, k * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    void swap(DBuf& o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
     }
 };
 

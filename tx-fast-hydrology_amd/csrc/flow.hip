@@ -34,6 +34,12 @@
 #ifndef MCR_EXP_BARRIER_CLOCK
 #define MCR_EXP_BARRIER_CLOCK 0  // diagnostic: the trace's CU-id word holds tick-barrier cycles
 #endif
+#ifndef MCR_EXP_NO_ZERO_ADD
+#define MCR_EXP_NO_ZERO_ADD 0    // diagnostic: drop the reference's leading 0 + of the update
+#endif
+#ifndef MCR_EXP_NO_ACT
+#define MCR_EXP_NO_ACT 0         // diagnostic (wrong results): every slot active at every tick
+#endif
 #ifndef MCR_EXP_NO_HELPER
 #define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
 #endif
@@ -56,7 +62,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kHelperLanes = 64;                      // one helper wave per workgroup
 constexpr int kBatch = 8;                             // granules per helper lane per batch
 constexpr int kBatchItems = kHelperLanes * kBatch;    // (external input, tick) items per batch
-constexpr int64_t kGiveUpTicks = 200000000;           // 2 s of the 100 MHz wall clock
 static_assert(kFlowMaxExt * kChunk == 2 * kBatchItems, "two helper batches per chunk");
 
 // poll back-off: s_sleep 32 (x 64 clocks) per unit, at most 16 units (1-64 clocks per unit
@@ -79,6 +84,7 @@ struct Helper {
     int lane, e0, nitems, T;
     unsigned epoch;
     int32_t* status;
+    int64_t patience;             // wall-clock ticks a stale granule is polled before giving up
     bool dead;
 
     __device__ __forceinline__ bool item(int idx, int kn, unsigned& voff) const {
@@ -135,7 +141,7 @@ struct Helper {
                 const u32x4 p = __builtin_amdgcn_raw_buffer_load_b128(xg, voff, 0, 16);
                 if (p.y == epoch && p.w == epoch) break;
                 const int st = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (st != 0 || wall_clock64() - t0 > kGiveUpTicks) {
+                if (st != 0 || wall_clock64() - t0 > patience) {
                     if (st == 0 && lane == 0)
                         __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     dead = true;
@@ -212,7 +218,7 @@ void wavefront_flow(WaveArgs a) {
     if (wave == kHW) {
         // ================================ helper wave ================================
         Helper h{lds, xg, XE, XSLOT, EG, PL, tid & 63, e0, next * kChunk, T, a.epoch, a.status,
-                 false};
+                 a.patience, false};
         const int nb = (h.nitems + kBatchItems - 1) / kBatchItems;   // <= 2 (host-checked)
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();                     // EG staged (LDS) before the helper reads it
@@ -447,11 +453,11 @@ void wavefront_flow(WaveArgs a) {
                 double prev = 0.0;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    const bool act = (unsigned)(k - S[p].G) < (unsigned)T;
+                    const bool act = MCR_EXP_NO_ACT || (unsigned)(k - S[p].G) < (unsigned)T;
                     const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                    const double rr =
-                        0.0 + (((S[p].al * I + S[p].be * S[p].ip) + S[p].ch * S[p].op) +
-                               S[p].ga * qv[p]);
+                    const double xx = ((S[p].al * I + S[p].be * S[p].ip) + S[p].ch * S[p].op) +
+                                      S[p].ga * qv[p];
+                    const double rr = MCR_EXP_NO_ZERO_ADD ? xx : 0.0 + xx;
                     const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
                     S[p].op = act ? o : S[p].op;
                     S[p].ip = act ? I : S[p].ip;
@@ -497,8 +503,8 @@ void wavefront_flow(WaveArgs a) {
         // session state after the horizon; never-processed reaches hold o = 0
 #pragma unroll
         for (int p = 0; p < K; ++p) {
-            a.st_o[S[p].d] = S[p].op;
-            a.st_i[S[p].d] = S[p].ip;
+            a.st_o_out[S[p].d] = S[p].op;
+            a.st_i_out[S[p].d] = S[p].ip;
         }
     }
     if (a.trace && tid == 0) {

@@ -44,6 +44,7 @@ constexpr int64_t kDummyPerMember = 2048;
 constexpr int kFlowMaxExt = 128;
 constexpr int kFlowMaxT = 1024;
 constexpr int kFlowMinSlack = 2 * kChunk;
+constexpr int64_t kFlowPatience = 200000000;   // default: 2 s of the 100 MHz wall clock
 
 // launch trace record of one workgroup: wall clock at start / loop start / end, hw id, shader
 // clock at loop start / end
@@ -69,6 +70,10 @@ struct WaveArgs {
     // final state after the horizon (the session state, no separate gather)
     double* st_o;
     double* st_i;
+    // dataflow horizon (flow.hip, one member): the state after the horizon goes here (the
+    // session keeps its input state until the run is known to have completed)
+    double* st_o_out;
+    double* st_i_out;
     const double* F;              // forcing rows in slot order [n_rows][nslots]
     const int4* stab;             // per step {row_lo, row_hi, frac (f64)}; clamped: {r, r, 0}
     const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
@@ -86,6 +91,7 @@ struct WaveArgs {
     uint32_t xg_bytes;            // size of XG in bytes (< 2^31)
     uint32_t epoch;               // tag of this run's granules (never 0)
     int32_t* status;              // set to 1 when a wait gave up
+    int64_t patience;             // wall-clock (100 MHz) ticks a wait polls before giving up
     const double* Qm;             // member dataflow: lateral inflow [E][nslots] of the step
     const double* IO;             // member dataflow: state {o, i} [E][nslots][2]
     int64_t nslots;

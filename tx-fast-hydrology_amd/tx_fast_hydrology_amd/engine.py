@@ -293,6 +293,11 @@ class RoutingNet:
         """Execution path: "auto" (default), "launches" or "dataflow" (see mcroute.h)."""
         nat.check(nat.lib().mc_set_mode(self._h, self.MODES[mode]))
 
+    def set_flow_patience(self, wall_ticks: int):
+        """Dataflow wait limit in 100 MHz wall-clock ticks (0 = default 2 s, < 0 = give up at
+        once; a horizon whose wait gave up is re-routed with launches, mcroute.h)."""
+        nat.check(nat.lib().mc_set_flow_patience(self._h, int(wall_ticks)))
+
     def mode(self) -> tuple:
         """(requested mode, path of the last run: "launches" / "dataflow" / None)."""
         m = ctypes.c_int()
