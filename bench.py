@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--chain", type=int, default=0,
                     help="node slots per lane (plan.hpp lane chains); 0 = per workload")
+    ap.add_argument("--vec-shape", default="",
+                    help="route with the member-vector sweep at shape H:W (node slots per wave "
+                         "instruction, waves per workgroup; 0 = automatic)")
     ap.add_argument("--conus", action="store_true",
                     help="BASELINE configs[4]: CONUS NWM-scale synthetic network (2.7M reaches, "
                          "4000 outlets, deepest path ~7000 reaches); --members per GPU (default "
@@ -162,6 +165,9 @@ def build_workload(args, rank=0, world=1):
     tile = args.tile or (64 if E > 1 and enkf is None else 16)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E,
                             chain=args.chain)
+    if args.vec_shape:         # the member-vector sweep (mcroute.h mode 3) at this shape
+        net.set_mode("vector")
+        net.set_vector_shape(*(int(v) for v in args.vec_shape.split(":")))
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
@@ -327,7 +333,14 @@ def main():
                 # measured HBM bytes per launch / launch time: the DRAM rate the kernel drives
                 "traffic_gbs": (round(traffic["traffic_bytes_per_launch"] / (launch_ms * 1e-3)
                                       / 1e9, 3) if traffic else None),
-                "kernel": "wavefront_flow" if net.mode()[1] == "dataflow" else "wavefront_det",
+                # the same DRAM rate as a fraction of the HBM peak: the routing recurrence keeps
+                # coefficients and state in registers / LDS and is bound by its dependency chain
+                # (schedule ticks x per-tick latency), not by DRAM bandwidth
+                "dram_frac": (round(traffic["traffic_bytes_per_launch"] / (launch_ms * 1e-3)
+                                    / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
+                "algorithmic_bytes_per_unit": per_unit,
+                "kernel": {"dataflow": "wavefront_flow", "vector": "wavefront_vec"}.get(
+                    net.mode()[1], "wavefront_det"),
                 "launches_per_step": tm["launches"] / args.timing_runs,
                 "avg_launch_us": round(launch_ms * 1e3, 3),
                 "kernel_ms_per_step": round(tm["kernel_ms"] / args.timing_runs, 4)}
@@ -382,7 +395,10 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            # one bench step = one whole T-step horizon (module docstring)
             "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_horizon": elapsed / args.steps * 1e3,
+            "us_per_timestep": elapsed / args.steps / args.T * 1e6,
             "higher_is_better": True,
             "scaling": "strong" if wl.enkf is not None else "weak",
             "vs_baseline": None,

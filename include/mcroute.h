@@ -205,10 +205,17 @@ int mc_reset_timing(void* net);
 
 /* Execution path of mc_run / mc_step.  mode 0 (default): one resident dataflow launch for the
  * whole horizon when the network fits the device at once, else launches of `tile` ticks;
- * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit).
- * last_path: 1 or 2 = the path the last run took (0 before any run). */
+ * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit);
+ * 3: the member-vector sweep (ensembles of E = a multiple of 16 members on a 64-lane plan:
+ * lanes are members, launches of `tile` ticks; MC_E_STATE for a session it cannot route).
+ * last_path: 1, 2 or 3 = the path the last run took (0 before any run). */
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);
+/* Shape of the member-vector sweep: node slots per wave instruction (1, 2 or 4: 64, 32 or 16
+ * members each) and waves per workgroup (4, 8 or 16); 0 = automatic.  A shape without a kernel
+ * instantiation (or whose member width does not divide E) makes the session fall back to the
+ * other paths (mode 3: MC_E_STATE). */
+int mc_set_vector_shape(void* net, int nodes_per_instr, int waves);
 
 /* How long a dataflow wait polls a stale upstream value before it gives up, in ticks of the
  * device's 100 MHz wall clock (0 = the default 2 s; < 0 = give up at once, for tests).  A run

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -34,6 +35,9 @@ mcr::PlanParams to_params(const mc_plan_params* pp) {
         if (pp->tile) p.tile = pp->tile;
         if (pp->ext_cap) p.ext_cap = pp->ext_cap;
         if (pp->chain) p.chain = pp->chain;
+        // 64-lane plans serve the member-vector ensemble kernel, which stages at most
+        // kVecMaxExt external inputs per workgroup
+        if (!pp->ext_cap && p.slots == 64) p.ext_cap = mcr::kVecMaxExt / 2;
     }
     return p;
 }
@@ -176,6 +180,18 @@ struct Net {
     int force_mode = -1;             // >= 0: mode override during a re-run
     int64_t patience = mcr::kFlowPatience;   // dataflow waits (mc_set_flow_patience)
 
+    // member-vector ensemble sweep (vector.hip): node records, external-input sources,
+    // member-minor forcing / state, and whether the last run's outputs are in its layout
+    // OM[slot][t][e] (fetches then read them through vjbase[j] = pos[j] * T * E)
+    bool vec_plan = false;           // 64-lane plan within the kernel's external-input cap
+    int vec_waves = 8;               // waves per workgroup
+    DBuf<mcr::VecMeta> vmeta;
+    DBuf<int64_t> vext_slot, vjbase;
+    DBuf<double> FMv, SMo, SMi;
+    bool fm_valid = false;
+    int64_t vjbase_E = 0, vjbase_T = 0;
+    bool out_vec = false;
+
     // launch trace (mc_set_trace)
     bool trace = false;
     DBuf<int64_t> trace_buf;
@@ -202,9 +218,10 @@ struct Net {
         if (plan.p.tile % mcr::kChunk != 0)
             throw Fail(MC_E_INVALID, "tile must be a multiple of 16 for the device sweep");
         if (!mcr::wavefront_shape_ok(plan.p.slots, plan.p.chain))
-            throw Fail(MC_E_INVALID, "no device kernel for this (slots, chain): chain 2 takes "
-                                     "slots 64..512 (multiples of 64 up to 448, and 512), chain "
-                                     "3 slots 64/192/256, chain 4 slots 64/128/192/256");
+            throw Fail(MC_E_INVALID, "no device kernel for this (slots, chain): chain 1 takes "
+                                     "slots 64, chain 2 slots 64..512 (multiples of 64 up to "
+                                     "448, and 512), chain 3 slots 64/192/256, chain 4 slots "
+                                     "64/128/192/256");
         HIPC(hipGetDevice(&device));
         HIPC(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
         stream = own;
@@ -250,6 +267,7 @@ struct Net {
             for (size_t w = 0; w < ids.size(); ++w) ids[w] = (int32_t)w;
             all_wg.upload(ids.data(), ids.size(), stream);
         }
+        init_vec();
         status.reserve(1);
         HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
         HIPC(hipHostMalloc(reinterpret_cast<void**>(&status_host), sizeof(int32_t),
@@ -257,6 +275,134 @@ struct Net {
         *status_host = 0;
         sync();
     }
+
+    // Node records of the member-vector kernel (codes -> plane columns; coefficients are filled
+    // in by set_coeffs).  Only 64-lane plans whose workgroups stay within kVecMaxExt external
+    // inputs qualify.
+    void init_vec() {
+        const int64_t RS = (int64_t)plan.p.chain * plan.p.slots;
+        vec_plan = plan.p.slots == 64 && plan.max_ext_wg <= mcr::kVecMaxExt && plan.nslots > 0 &&
+                   plan.nslots < (1ll << 31);
+        if (!vec_plan) return;
+        std::vector<mcr::VecMeta> m((size_t)plan.nslots);
+        for (int64_t d = 0; d < plan.nslots; ++d) {
+            mcr::VecMeta& r = m[d];
+            r.al = r.be = r.ch = r.ga = 0.0;
+            r.cnt = r.chained = r.pad = 0;
+            for (int u = 0; u < 4; ++u) r.in[u] = (int32_t)RS;
+            if (plan.flags[d] == mcr::kSlotPad) {
+                r.G = 1 << 29;
+                continue;
+            }
+            r.G = plan.G[d];
+            int k = 0;
+            for (int u = 0; u < plan.up_cnt[d]; ++u) {
+                const unsigned code = (unsigned)((plan.up4[d] >> (16 * u)) & 0xffffu);
+                if (code == mcr::kSelfCode) {
+                    r.chained = 1;
+                } else if (code & mcr::kExtBit) {
+                    r.in[k++] = (int32_t)(RS + 1 + (code & 0x7fffu));
+                } else {
+                    r.in[k++] = (int32_t)code;
+                }
+            }
+            r.cnt = k;
+        }
+        vmeta.upload(m.data(), m.size(), stream);
+        std::vector<int64_t> xs(plan.ext_src.size());
+        for (size_t x = 0; x < xs.size(); ++x) {
+            const int64_t src = plan.ext_src[x];
+            xs[x] = src < plan.n ? plan.pos[src] : src - plan.n;
+        }
+        vext_slot.upload(xs.data(), xs.size(), stream);
+        vext_slot.reserve(1);
+        sync();
+    }
+
+    // nodes per wave instruction (64 / H members each) of the member-vector kernel for this
+    // ensemble, and its waves per workgroup (H = 0: not eligible).  mc_set_vector_shape pins
+    // either; by default the first instantiated shape in the order below (measured: Texas
+    // ens64, 4 nodes x 16 members per instruction in 16-wave workgroups is the fastest)
+    int vec_pin_h = 0, vec_pin_w = 0;
+    int vec_H() {
+        if (!vec_plan || E < 2) return 0;
+        for (int H : {4, 2, 1}) {
+            if (vec_pin_h && H != vec_pin_h) continue;
+            if (E % (64 / H) != 0) continue;
+            for (int W : {16, 8, 4}) {
+                if (vec_pin_w && W != vec_pin_w) continue;
+                if (mcr::vec_shape_ok(plan.p.slots, plan.p.chain, W, H)) {
+                    vec_waves = W;
+                    return H;
+                }
+            }
+        }
+        return 0;
+    }
+
+    // T steps of all members with the member-vector kernel (vector.hip): node-major
+    // member-minor layouts FM [ns][rows][E], SM [ns][E], outputs [ns][T][E]
+    void run_vec(int64_t T, int H) {
+        const int64_t ns = plan.nslots, rows = n_rows;
+        const int Ew = 64 / H;
+        REQUIRE((int64_t)H * std::max(T, rows) * E * 8 < (1ll << 31),
+                "horizon x members too large for the member-vector path");
+        if (!fm_valid) {            // forcing [E][rows][ns] -> [ns][rows][E], row by row
+            FMv.reserve((size_t)(rows * ns * E));
+            for (int64_t r = 0; r < rows; ++r)
+                HIPC(mcr::launch_transpose_ld(F.p + r * ns, rows * ns, FMv.p + r * E, rows * E,
+                                              E, ns, stream));
+            fm_valid = true;
+        }
+        SMo.reserve((size_t)(ns * E));
+        SMi.reserve((size_t)(ns * E));
+        HIPC(mcr::launch_transpose(st_o.p, SMo.p, E, ns, 1, stream));
+        HIPC(mcr::launch_transpose(st_i.p, SMi.p, E, ns, 1, stream));
+        O.reserve((size_t)(T * ns * E));
+        if (vjbase_E != E || vjbase_T != T) {
+            std::vector<int64_t> jb((size_t)std::max<int64_t>(plan.n, 1));
+            for (int64_t j = 0; j < plan.n; ++j) jb[j] = plan.pos[j] * T * E;
+            vjbase.upload(jb.data(), jb.size(), stream);
+            vjbase_E = E;
+            vjbase_T = T;
+        }
+        mcr::VecArgs a{};
+        a.meta = vmeta.p;
+        a.wg_gmin = wg_gmin.p;
+        a.wg_gmax = wg_gmax.p;
+        a.ext_off = ext_off.p;
+        a.ext_slot = vext_slot.p;
+        a.ext_g = ext_g.p;
+        a.stab = stab.p;
+        a.FM = FMv.p;
+        a.SM_o = SMo.p;
+        a.SM_i = SMi.p;
+        a.OM = O.p;
+        a.nslots = ns;
+        a.E = E;
+        a.n_rows = (int32_t)rows;
+        a.T = (int32_t)T;
+        a.tile = plan.p.tile;
+        const int64_t nl = (int64_t)cur->off.size() - 1;
+        int64_t launched = 0;
+        for (int64_t k = 0; k < nl; ++k) {
+            const int64_t grid = cur->off[k + 1] - cur->off[k];
+            if (grid == 0) continue;
+            a.active = cur->active.p + cur->off[k];
+            a.kappa0 = (int32_t)(k * plan.p.tile);
+            if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
+            HIPC(mcr::launch_vec(a, (int)grid, (int)(E / Ew), plan.p.chain, vec_waves, H,
+                                 stream));
+            if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
+            ++launched;
+        }
+        HIPC(mcr::launch_transpose(SMo.p, st_o.p, ns, E, 1, stream));
+        HIPC(mcr::launch_transpose(SMi.p, st_i.p, ns, E, 1, stream));
+        out_vec = true;
+        last_path = 3;
+        vec_launched = launched;
+    }
+    int64_t vec_launched = 0;
 
     // Copy k elements host -> device without waiting for the stream: the source is staged in a
     // pinned slot whose previous copy (8 uploads ago) must have completed.
@@ -633,6 +779,7 @@ struct Net {
         dummy.reserve(mcr::kDummyPerMember * m);
         n_rows = 0;                    // forcing and outputs are per member: load again
         T_out = 0;
+        fm_valid = false;
         sync();
     }
 
@@ -645,6 +792,9 @@ struct Net {
         // partial sums pass their fold through, unrouted reaches and padding output 0
         HIPC(mcr::launch_set_slot_coeffs(flags.p, alpha.p, beta.p, chi.p, gamma.p, plan.nslots,
                                          stream));
+        if (vec_plan)
+            HIPC(mcr::launch_vec_meta_coeffs(alpha.p, beta.p, chi.p, gamma.p, vmeta.p,
+                                             plan.nslots, stream));
         sync();  // `stage` is reused by the next call
         coeffs_set = true;
     }
@@ -764,122 +914,142 @@ struct Net {
         int64_t launched = 0;
         trace_launch.clear();
         trace_wg.clear();
+        out_vec = false;
         size_t flds = 0;
-        if (E > 1 && mode == 2 && T != 1)
-            throw Fail(MC_E_STATE, "dataflow mode routes one member, or one step of an ensemble");
-        if (E > 1 && T == 1 && members_fit(flds)) {
-            // ---- one step of all members as one dataflow launch (flow.hip, MEMB): member e
-            // of slot d at tick G[d] + e
-            const size_t words = plan.ext_src.size() * (size_t)E * 4;
-            if (words > xg_words || epoch == 0xffffffffu) {
-                XG.reserve(std::max<size_t>(words, 4));
-                HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(words, 4) * 4, stream));
-                xg_words = std::max(xg_words, words);
-                epoch = 0;
+        {
+            // ---- the member-vector sweep (vector.hip), on request: bit-identical to the other
+            // paths, but measured slower than the multi-launch sweep on Texas ens64 (DESIGN.md
+            // §6), so mode 0 does not choose it
+            const int H = mode == 3 ? vec_H() : 0;
+            const bool want = mode == 3;
+            if (mode == 3 && (H == 0 || Fsrc != F.p))
+                throw Fail(MC_E_STATE, "member-vector mode needs an ensemble (E a multiple of 16) "
+                                       "on a 64-lane plan within the kernel's external-input "
+                                       "cap, routed with mc_run");
+            if (want && H > 0 && Fsrc == F.p && !trace) {
+                run_vec(T, H);
+                launched = vec_launched;
             }
-            ++epoch;
-            Qm.reserve((size_t)(plan.nslots * E * 3));     // IO [E][nslots][2] + Qm [E][nslots]
-            double* IOp = Qm.p + plan.nslots * E;
-            HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
-                                           st_i.p, IOp, Qm.p, E, stream));
-            a.Qm = Qm.p;
-            a.IO = IOp;
-            a.T = (int32_t)E;
-            a.XG = XG.p;
-            a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
-            a.epoch = epoch;
-            a.status = status.p;
-            a.patience = patience;
-            a.table_cap = 0;
-            a.active = all_wg.p;
-            if (trace) {
-                trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int32_t>(plan.nwg, 1));
-                a.trace = trace_buf.p;
-                trace_launch.assign(plan.nwg, 0);
-                for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
-            }
-            if (timing) HIPC(hipEventRecord(events[0], stream));
-            HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, plan.p.chain, flds,
-                                          stream));
-            if (timing) HIPC(hipEventRecord(events[1], stream));
-            HIPC(mcr::launch_member_unpack(IOp, flags.p, G.p, wg_gmin.p, cur->wbase.p,
-                                           row_width(), O.p, cur->Otot, st_o.p, st_i.p,
-                                           plan.nslots, E, stream));
-            ++flow_runs;
-            last_flow.valid = false;       // member runs update the state in place
-            launched = 1;
-            last_path = 2;
-            a.T = (int32_t)T;
-        } else if (E > 1 && mode == 2) {
-            throw Fail(MC_E_STATE, "member dataflow requested but the network does not fit one "
-                                   "resident launch");
         }
-        if (E == 1 && flow_fits(T, dense, flds)) {
-            // ---- one dataflow launch for the whole horizon (flow.hip)
-            const size_t words = plan.ext_src.size() * (size_t)T * 4;
-            if (words > xg_words || epoch == 0xffffffffu) {
-                XG.reserve(std::max<size_t>(words, 4));
-                HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(words, 4) * 4, stream));
-                xg_words = std::max(xg_words, words);
-                epoch = 0;                 // granules of earlier runs can never match again
+        if (last_path == 3) {
+            // outputs and state are complete; timing below
+        } else {
+            if (E > 1 && mode == 2 && T != 1)
+                throw Fail(MC_E_STATE, "dataflow mode routes one member, or one step of an ensemble");
+            if (E > 1 && T == 1 && members_fit(flds)) {
+                // ---- one step of all members as one dataflow launch (flow.hip, MEMB): member e
+                // of slot d at tick G[d] + e
+                const size_t words = plan.ext_src.size() * (size_t)E * 4;
+                if (words > xg_words || epoch == 0xffffffffu) {
+                    XG.reserve(std::max<size_t>(words, 4));
+                    HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(words, 4) * 4, stream));
+                    xg_words = std::max(xg_words, words);
+                    epoch = 0;
+                }
+                ++epoch;
+                Qm.reserve((size_t)(plan.nslots * E * 3));     // IO [E][nslots][2] + Qm [E][nslots]
+                double* IOp = Qm.p + plan.nslots * E;
+                HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
+                                               st_i.p, IOp, Qm.p, E, stream));
+                a.Qm = Qm.p;
+                a.IO = IOp;
+                a.T = (int32_t)E;
+                a.XG = XG.p;
+                a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
+                a.epoch = epoch;
+                a.status = status.p;
+                a.patience = patience;
+                a.table_cap = 0;
+                a.active = all_wg.p;
+                if (trace) {
+                    trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int32_t>(plan.nwg, 1));
+                    a.trace = trace_buf.p;
+                    trace_launch.assign(plan.nwg, 0);
+                    for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
+                }
+                if (timing) HIPC(hipEventRecord(events[0], stream));
+                HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, plan.p.chain, flds,
+                                              stream));
+                if (timing) HIPC(hipEventRecord(events[1], stream));
+                HIPC(mcr::launch_member_unpack(IOp, flags.p, G.p, wg_gmin.p, cur->wbase.p,
+                                               row_width(), O.p, cur->Otot, st_o.p, st_i.p,
+                                               plan.nslots, E, stream));
+                ++flow_runs;
+                last_flow.valid = false;       // member runs update the state in place
+                launched = 1;
+                last_path = 2;
+                a.T = (int32_t)T;
+            } else if (E > 1 && mode == 2) {
+                throw Fail(MC_E_STATE, "member dataflow requested but the network does not fit one "
+                                       "resident launch");
             }
-            ++epoch;
-            a.XG = XG.p;
-            a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
-            a.epoch = epoch;
-            a.status = status.p;
-            a.patience = patience;
-            a.table_cap = (int32_t)T;
-            a.active = all_wg.p;
-            if (trace) {
-                trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int32_t>(plan.nwg, 1));
-                a.trace = trace_buf.p;
-                trace_launch.assign(plan.nwg, 0);
-                for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
+            if (E == 1 && flow_fits(T, dense, flds)) {
+                // ---- one dataflow launch for the whole horizon (flow.hip)
+                const size_t words = plan.ext_src.size() * (size_t)T * 4;
+                if (words > xg_words || epoch == 0xffffffffu) {
+                    XG.reserve(std::max<size_t>(words, 4));
+                    HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(words, 4) * 4, stream));
+                    xg_words = std::max(xg_words, words);
+                    epoch = 0;                 // granules of earlier runs can never match again
+                }
+                ++epoch;
+                a.XG = XG.p;
+                a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
+                a.epoch = epoch;
+                a.status = status.p;
+                a.patience = patience;
+                a.table_cap = (int32_t)T;
+                a.active = all_wg.p;
+                if (trace) {
+                    trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int32_t>(plan.nwg, 1));
+                    a.trace = trace_buf.p;
+                    trace_launch.assign(plan.nwg, 0);
+                    for (int32_t w = 0; w < plan.nwg; ++w) trace_wg.push_back(w);
+                }
+                // the horizon's final state goes to the spare buffers, which then become the
+                // session state; the input state stays in the old ones (re-run source, sync())
+                st_o2.reserve(st_o.cap);
+                st_i2.reserve(st_i.cap);
+                a.st_o_out = st_o2.p;
+                a.st_i_out = st_i2.p;
+                if (timing) HIPC(hipEventRecord(events[0], stream));
+                HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, plan.p.chain, flds, dense,
+                                      stream));
+                if (timing) HIPC(hipEventRecord(events[1], stream));
+                st_o.swap(st_o2);
+                st_i.swap(st_i2);
+                ++flow_runs;
+                last_flow.valid = true;
+                last_flow.T = T;
+                last_flow.F = Fsrc;
+                last_flow.rows = rows;
+                last_flow.tab = tabh;
+                launched = 1;
+                last_path = 2;
             }
-            // the horizon's final state goes to the spare buffers, which then become the
-            // session state; the input state stays in the old ones (re-run source, sync())
-            st_o2.reserve(st_o.cap);
-            st_i2.reserve(st_i.cap);
-            a.st_o_out = st_o2.p;
-            a.st_i_out = st_i2.p;
-            if (timing) HIPC(hipEventRecord(events[0], stream));
-            HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, plan.p.chain, flds, dense,
-                                  stream));
-            if (timing) HIPC(hipEventRecord(events[1], stream));
-            st_o.swap(st_o2);
-            st_i.swap(st_i2);
-            ++flow_runs;
-            last_flow.valid = true;
-            last_flow.T = T;
-            last_flow.F = Fsrc;
-            last_flow.rows = rows;
-            last_flow.tab = tabh;
-            launched = 1;
-            last_path = 2;
-        }
-        a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
-        const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, plan.p.chain, a.table_cap,
-                                                    a.ext_cap, a.tile);
-        if (launched == 0 && trace) {
-            trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(cur->off[nl], 1));
-            trace_wg = cur->list;
-        }
-        for (int64_t k = 0; k < nl && last_path != 2; ++k) {
-            const int64_t grid = cur->off[k + 1] - cur->off[k];
-            if (grid == 0) continue;
-            a.active = cur->active.p + cur->off[k];
-            if (trace) {
-                a.trace = trace_buf.p + mcr::kTraceWords * cur->off[k];
-                trace_launch.resize(cur->off[k + 1], k);
+            a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
+            const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, plan.p.chain, a.table_cap,
+                                                        a.ext_cap, a.tile);
+            if (launched == 0 && trace) {
+                trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(cur->off[nl], 1));
+                trace_wg = cur->list;
             }
-            a.kappa0 = (int32_t)(k * plan.p.tile);
-            if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-            HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, plan.p.chain, lds, dense,
-                                       (int)E, stream));
-            if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
-            ++launched;
-            last_path = 1;
+            for (int64_t k = 0; k < nl && last_path != 2; ++k) {
+                const int64_t grid = cur->off[k + 1] - cur->off[k];
+                if (grid == 0) continue;
+                a.active = cur->active.p + cur->off[k];
+                if (trace) {
+                    a.trace = trace_buf.p + mcr::kTraceWords * cur->off[k];
+                    trace_launch.resize(cur->off[k + 1], k);
+                }
+                a.kappa0 = (int32_t)(k * plan.p.tile);
+                if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
+                HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, plan.p.chain, lds, dense,
+                                           (int)E, stream));
+                if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
+                ++launched;
+                last_path = 1;
+            }
         }
         if (timing) {
             HIPC(hipEventRecord(events[2 * nl + 1], stream));
@@ -905,6 +1075,7 @@ struct Net {
         const int64_t n = plan.n;
         xp.assign(xps, xps + rows);
         n_rows = rows;
+        fm_valid = false;
         F.reserve((size_t)(rows * plan.nslots * E));
         if (n == 0) return;
         DBuf<double> tmp;
@@ -961,8 +1132,13 @@ struct Net {
         for (int c = 0; c < 2; ++c) {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
-                                          c == 1, row_width(), outT.p, n, t0, t1, E, stream));
+            if (out_vec)
+                HIPC(mcr::launch_gather_steps(O.p, 1, vjbase.p, in_off.p, in_list.p, c == 1,
+                                              (int)E, outT.p, n, t0, t1, E, stream));
+            else
+                HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p,
+                                              in_list.p, c == 1, row_width(), outT.p, n, t0, t1,
+                                              E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             sync();
@@ -979,8 +1155,13 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
-                                           k == 1, row_width(), outT.p, n, T_out, E, stream));
+            if (out_vec)
+                HIPC(mcr::launch_gather_series(O.p, 1, vjbase.p, in_off.p, in_list.p, k == 1,
+                                               (int)E, outT.p, n, T_out, E, stream));
+            else
+                HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p,
+                                               in_list.p, k == 1, row_width(), outT.p, n, T_out,
+                                               E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             sync();
         }
@@ -1277,8 +1458,22 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
+        REQUIRE(mode >= 0 && mode <= 3,
+                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow) or 3 (member-vector)");
         as_net(net)->mode = mode;
+    });
+}
+
+int mc_set_vector_shape(void* net, int nodes_per_instr, int waves) {
+    return guarded([&] {
+        REQUIRE(nodes_per_instr == 0 || nodes_per_instr == 1 || nodes_per_instr == 2 ||
+                    nodes_per_instr == 4,
+                "nodes per instruction must be 0 (auto), 1, 2 or 4");
+        REQUIRE(waves == 0 || waves == 4 || waves == 8 || waves == 16,
+                "waves must be 0 (auto), 4, 8 or 16");
+        Net* N = as_net(net);
+        N->vec_pin_h = nodes_per_instr;
+        N->vec_pin_w = waves;
     });
 }
 

@@ -103,6 +103,7 @@ SIGNATURES = {
     "mc_ens_unpack_apply": (_i32, [_vp, _i64, _vp]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_set_flow_patience": (_i32, [_vp, _i64]),
+    "mc_set_vector_shape": (_i32, [_vp, ctypes.c_int, ctypes.c_int]),
     "mc_get_mode": (_i32, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),
     "mc_get_trace": (_i32, [_vp, _vp, _i64, ctypes.POINTER(ctypes.c_int64),

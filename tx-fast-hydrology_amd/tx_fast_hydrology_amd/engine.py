@@ -287,11 +287,17 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
-    MODES = {"auto": 0, "launches": 1, "dataflow": 2}
+    MODES = {"auto": 0, "launches": 1, "dataflow": 2, "vector": 3}
 
     def set_mode(self, mode: str):
-        """Execution path: "auto" (default), "launches" or "dataflow" (see mcroute.h)."""
+        """Execution path: "auto" (default), "launches", "dataflow" or "vector" (the
+        member-vector ensemble sweep; see mcroute.h)."""
         nat.check(nat.lib().mc_set_mode(self._h, self.MODES[mode]))
+
+    def set_vector_shape(self, nodes_per_instr: int = 0, waves: int = 0):
+        """Member-vector sweep shape: node slots per wave instruction (1, 2, 4) and waves per
+        workgroup (4, 8, 16); 0 = automatic (mcroute.h mc_set_vector_shape)."""
+        nat.check(nat.lib().mc_set_vector_shape(self._h, int(nodes_per_instr), int(waves)))
 
     def set_flow_patience(self, wall_ticks: int):
         """Dataflow wait limit in 100 MHz wall-clock ticks (0 = default 2 s, < 0 = give up at
@@ -304,7 +310,7 @@ class RoutingNet:
         p = ctypes.c_int()
         nat.check(nat.lib().mc_get_mode(self._h, ctypes.byref(m), ctypes.byref(p)))
         names = {v: k for k, v in self.MODES.items()}
-        return names[m.value], {1: "launches", 2: "dataflow"}.get(p.value)
+        return names[m.value], {1: "launches", 2: "dataflow", 3: "vector"}.get(p.value)
 
     def set_trace(self, enable: bool):
         nat.check(nat.lib().mc_set_trace(self._h, 1 if enable else 0))
