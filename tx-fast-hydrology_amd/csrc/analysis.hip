@@ -227,6 +227,44 @@ __global__ void mean_anomalies(const double* __restrict__ X, double* __restrict_
     }
 }
 
+// Increments of a reach slice in one pass, for ensembles of at most MAXE members (the per-GPU
+// shares of the sharded EnKF): per slot d the member mean (mean_anomalies' order), the
+// anomalies A[e] = X[e][d] - mean in registers, and G[e][d] = sum_f A[f] Z[f][e] with Z (Et x Et,
+// column-major) staged in LDS (every lane reads the same coefficient: broadcast).  Replaces
+// mean_anomalies + the skinny (S x Et) x (Et x Et) GEMM, whose anomaly round trip through HBM
+// was most of their time.  One slot per thread.
+template <int MAXE>
+__global__ __launch_bounds__(256) void anomaly_increments(const double* __restrict__ X,
+                                                          const double* __restrict__ Z,
+                                                          double* __restrict__ G, int64_t S,
+                                                          int Et) {
+    __shared__ double Zs[MAXE * MAXE];
+    for (int i = threadIdx.x; i < Et * Et; i += 256) Zs[i] = Z[i];
+    __syncthreads();
+    const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (d >= S) return;
+    double a[MAXE];
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e)
+        if (e < Et) {
+            a[e] = X[e * S + d];
+            s += a[e];
+        }
+    const double xbar = s / (double)Et;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e)
+        if (e < Et) a[e] = a[e] - xbar;
+    for (int e = 0; e < Et; ++e) {
+        const double* z = Zs + e * Et;
+        double acc = 0.0;
+#pragma unroll
+        for (int f = 0; f < MAXE; ++f)
+            if (f < Et) acc = __builtin_fma(a[f], z[f], acc);
+        G[e * S + d] = acc;
+    }
+}
+
 // HA[g + e m] = A[e][gslot[g]],  D[g + e m] = Y[g][e] - X[e][gslot[g]]
 __global__ void gauge_gather(const double* __restrict__ A, const double* __restrict__ X,
                              const int64_t* __restrict__ gslot, const double* __restrict__ Y,
@@ -403,6 +441,20 @@ hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s) {
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s) {
     hipLaunchKernelGGL(mean_anomalies, grid_for(ns, 256), 256, 0, s, X, A, ns, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_anomaly_increments(const double* X, const double* Z, double* G, int64_t S,
+                                     int64_t Et, hipStream_t s) {
+    if (S <= 0) return hipSuccess;
+    if (Et < 2 || Et > kFusedIncrementsMax) return hipErrorInvalidValue;
+    const unsigned g = (unsigned)((S + 255) / 256);
+    if (Et <= 16)
+        hipLaunchKernelGGL(anomaly_increments<16>, g, 256, 0, s, X, Z, G, S, (int)Et);
+    else if (Et <= 32)
+        hipLaunchKernelGGL(anomaly_increments<32>, g, 256, 0, s, X, Z, G, S, (int)Et);
+    else
+        hipLaunchKernelGGL(anomaly_increments<64>, g, 256, 0, s, X, Z, G, S, (int)Et);
     return hipGetLastError();
 }
 

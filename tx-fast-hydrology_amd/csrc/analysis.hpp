@@ -30,6 +30,11 @@ constexpr int64_t kSpdSolveMax = 64;
 hipError_t launch_zero_if_failed(double* X, int64_t cnt, const int32_t* info, hipStream_t s);
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s);
+// G = (X - mean) Z for a member-major slice X [Et][S] and Z (Et x Et, column-major): the
+// increments of the slice in one pass (Et <= kFusedIncrementsMax)
+constexpr int64_t kFusedIncrementsMax = 64;
+hipError_t launch_anomaly_increments(const double* X, const double* Z, double* G, int64_t S,
+                                     int64_t Et, hipStream_t s);
 // HA (m x E) = A at the gauge slots; D (m x E) = Y[g][e] - X at the gauge slots (D may be NULL)
 hipError_t launch_gauge_gather(const double* A, const double* X, const int64_t* gslot,
                                const double* Y, double* HA, double* D, int64_t m, int64_t ns,

@@ -712,11 +712,16 @@ struct Net {
                                    stream, Wk.p, Wk.cap));
             HIPC(mcr::launch_zero_if_failed(Zn.p, Et * Et, info.p, stream));
         }
-        // slice anomalies and increments G = A Z  (= K D per member)
-        An.reserve((size_t)(S * Et));
-        HIPC(mcr::launch_mean_anomalies(Xs, An.p, S, Et, stream));
-        HIPC(mcr::launch_dgemm(false, false, S, Et, Et, 1.0, An.p, S, Zn.p, Et, 0.0, Gs, S,
-                               stream));
+        // slice anomalies and increments G = A Z  (= K D per member): one fused pass for the
+        // per-GPU ensemble sizes, the MFMA GEMM on materialised anomalies beyond
+        if (Et <= mcr::kFusedIncrementsMax) {
+            HIPC(mcr::launch_anomaly_increments(Xs, Zn.p, Gs, S, Et, stream));
+        } else {
+            An.reserve((size_t)(S * Et));
+            HIPC(mcr::launch_mean_anomalies(Xs, An.p, S, Et, stream));
+            HIPC(mcr::launch_dgemm(false, false, S, Et, Et, 1.0, An.p, S, Zn.p, Et, 0.0, Gs, S,
+                                   stream));
+        }
     }
 
     // increments of the local members from every rank's slice (Grecv [N][E][S]) -> _apply_gain

@@ -103,10 +103,14 @@ struct WaveArgs {
     int32_t ext_cap;              // LDS rows reserved for external inputs
 };
 
-// LDS bytes for `slots` lanes (chain * slots node slots)
+// LDS bytes of the multi-launch kernel for `slots` lanes (chain * slots node slots): the
+// parity double buffer XB [RS + 1][2] f64, forcing rows FR [RS][3] f64, the step-table window
+// and the external inputs of the launch (kernels.hip).  Over-allocating it costs resident
+// workgroups: 64 B per slot here (the flow kernel's tick planes) made Texas ens64 18.8 ms
+// instead of 12.7.
 inline size_t wavefront_lds_bytes(int slots, int chain, int table_cap, int ext_cap, int tile) {
     const size_t rs = (size_t)chain * slots;
-    return 64 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
+    return 16 * (rs + 1) + 24 * rs + 16 * (size_t)table_cap + 8 * (size_t)ext_cap * tile;
 }
 
 // dataflow kernel tick plane (flow.hip): every node slot, the zero slot and two chunk ring

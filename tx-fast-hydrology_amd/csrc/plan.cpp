@@ -57,10 +57,12 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";
     const int K = params.chain;
     if (K < 1 || K > kMaxChain) return "chain must be in [1, 4]";
-    // hard cap of external inputs: what is left of the LDS after the outflow tick rings (64 B)
-    // and forcing rows (24 B) of the chain * slots node slots and the step-table window
+    // hard cap of external inputs of the multi-launch kernel: what is left of its LDS after the
+    // outflow double buffer (16 B) and forcing rows (24 B) of the chain * slots node slots and
+    // the step-table window (kernels.hpp wavefront_lds_bytes; the dataflow kernel stages at most
+    // kFlowMaxExt and checks max_ext_wg against it)
     {
-        const int64_t left = kLdsBudget - 88 * (K * C + 1) - kTableEntryBytes * table_entries(C, B);
+        const int64_t left = kLdsBudget - 40 * (K * C + 1) - kTableEntryBytes * table_entries(C, B);
         const int64_t hard = std::min<int64_t>(left / (8 * (int64_t)B), 0x7fff);
         if (hard < 1) return "slots/tile too large for the 160 KiB LDS of a workgroup";
         P.ext_hard = (int32_t)hard;
