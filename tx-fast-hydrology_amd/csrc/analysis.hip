@@ -238,8 +238,15 @@ __global__ __launch_bounds__(256) void anomaly_increments(const double* __restri
                                                           const double* __restrict__ Z,
                                                           double* __restrict__ G, int64_t S,
                                                           int Et) {
-    __shared__ double Zs[MAXE * MAXE];
-    for (int i = threadIdx.x; i < Et * Et; i += 256) Zs[i] = Z[i];
+    // Zt[f][e] = Z[f + e Et]: the 8 coefficients of one anomaly for 8 consecutive outputs are
+    // contiguous (two 32-byte LDS reads), and 8 independent FMA chains run side by side
+    constexpr int EG = 8;
+    __shared__ __attribute__((aligned(16))) double Zt[MAXE * MAXE];
+    const int Ep = (Et + EG - 1) / EG * EG;               // padded row (zero columns)
+    for (int i = threadIdx.x; i < MAXE * Ep && i < MAXE * MAXE; i += 256) {
+        const int f = i / Ep, e = i - f * Ep;
+        Zt[i] = (f < Et && e < Et) ? Z[f + (int64_t)e * Et] : 0.0;
+    }
     __syncthreads();
     const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (d >= S) return;
@@ -255,13 +262,20 @@ __global__ __launch_bounds__(256) void anomaly_increments(const double* __restri
 #pragma unroll
     for (int e = 0; e < MAXE; ++e)
         if (e < Et) a[e] = a[e] - xbar;
-    for (int e = 0; e < Et; ++e) {
-        const double* z = Zs + e * Et;
-        double acc = 0.0;
+    for (int e0 = 0; e0 < Et; e0 += EG) {
+        double acc[EG];
+#pragma unroll
+        for (int j = 0; j < EG; ++j) acc[j] = 0.0;
 #pragma unroll
         for (int f = 0; f < MAXE; ++f)
-            if (f < Et) acc = __builtin_fma(a[f], z[f], acc);
-        G[e * S + d] = acc;
+            if (f < Et) {
+                const double* z = Zt + f * Ep + e0;
+#pragma unroll
+                for (int j = 0; j < EG; ++j) acc[j] = __builtin_fma(a[f], z[j], acc[j]);
+            }
+#pragma unroll
+        for (int j = 0; j < EG; ++j)
+            if (e0 + j < Et) G[(e0 + j) * S + d] = acc[j];
     }
 }
 

@@ -191,6 +191,8 @@ struct Net {
     bool fm_valid = false;
     int64_t vjbase_E = 0, vjbase_T = 0;
     bool out_vec = false;
+    // outputs of the last run are the {o, i} pairs of a member-dataflow step (Qm + nslots * E)
+    bool out_io = false;
 
     // launch trace (mc_set_trace)
     bool trace = false;
@@ -920,6 +922,7 @@ struct Net {
         trace_launch.clear();
         trace_wg.clear();
         out_vec = false;
+        out_io = false;
         size_t flds = 0;
         {
             // ---- the member-vector sweep (vector.hip), on request: bit-identical to the other
@@ -976,9 +979,9 @@ struct Net {
                 HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, plan.p.chain, flds,
                                               stream));
                 if (timing) HIPC(hipEventRecord(events[1], stream));
-                HIPC(mcr::launch_member_unpack(IOp, flags.p, G.p, wg_gmin.p, cur->wbase.p,
-                                               row_width(), O.p, cur->Otot, st_o.p, st_i.p,
-                                               plan.nslots, E, stream));
+                HIPC(mcr::launch_member_unpack(IOp, flags.p, st_o.p, st_i.p, plan.nslots, E,
+                                               stream));
+                out_io = true;             // the step's outputs stay in IO (fetch)
                 ++flow_runs;
                 last_flow.valid = false;       // member runs update the state in place
                 launched = 1;
@@ -1137,7 +1140,10 @@ struct Net {
         for (int c = 0; c < 2; ++c) {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
-            if (out_vec)
+            if (out_io)                    // T = 1: t0 = 0, t1 = 1
+                HIPC(mcr::launch_gather_io(Qm.p + plan.nslots * E, pos.p, c == 1, outT.p, n,
+                                           plan.nslots, E, stream));
+            else if (out_vec)
                 HIPC(mcr::launch_gather_steps(O.p, 1, vjbase.p, in_off.p, in_list.p, c == 1,
                                               (int)E, outT.p, n, t0, t1, E, stream));
             else
@@ -1160,7 +1166,10 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            if (out_vec)
+            if (out_io)                    // T = 1: [j][0][e] is the step layout
+                HIPC(mcr::launch_gather_io(Qm.p + plan.nslots * E, pos.p, k == 1, outT.p, n,
+                                           plan.nslots, E, stream));
+            else if (out_vec)
                 HIPC(mcr::launch_gather_series(O.p, 1, vjbase.p, in_off.p, in_list.p, k == 1,
                                                (int)E, outT.p, n, T_out, E, stream));
             else

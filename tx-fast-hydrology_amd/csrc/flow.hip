@@ -612,34 +612,47 @@ hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);
 }
 
-// After a member-dataflow step: session state and T = 1 output windows from the IO pairs
+// After a member-dataflow step: the session state from the IO pairs.  The IO pairs themselves
+// stay the step's outputs (o, and the inflow fold i) until the next run: the fetches read them
+// there (launch_gather_io) instead of scattering them into the T = 1 output windows.
 __global__ void member_unpack(const double2* __restrict__ IO, const uint8_t* __restrict__ flags,
-                              const int32_t* __restrict__ G, const int32_t* __restrict__ wg_gmin,
-                              const int64_t* __restrict__ wbase, int rs, double* __restrict__ O,
-                              int64_t mO, double* __restrict__ st_o, double* __restrict__ st_i,
-                              int64_t ns, int64_t cnt) {
+                              double* __restrict__ st_o, double* __restrict__ st_i, int64_t ns,
+                              int64_t cnt) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= cnt) return;
-    const int64_t e = idx / ns, d = idx - e * ns;
-    const uint8_t fl = flags[d];
-    if (fl == kSlotPad) return;
+    const int64_t d = idx % ns;
+    if (flags[d] == kSlotPad) return;
     const double2 v = IO[idx];
     st_o[idx] = v.x;
     st_i[idx] = v.y;
-    const int64_t w = d / rs;
-    O[e * mO + wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * rs + (d - w * rs)] =
-        fl == kSlotRouted ? v.x : 0.0;
 }
 
-hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, const int32_t* G,
-                                const int32_t* wg_gmin, const int64_t* wbase, int rs, double* O,
-                                int64_t mO, double* st_o, double* st_i, int64_t ns, int64_t E,
-                                hipStream_t s) {
+// out[j][e] = IO[e][pos[j]].x (outflow) or .y (inflow): the outputs of a member-dataflow step in
+// caller order, member innermost
+__global__ void gather_io(const double2* __restrict__ IO, const int64_t* __restrict__ pos,
+                          bool inflow, double* __restrict__ out, int64_t n, int64_t ns,
+                          int64_t E) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n * E) return;
+    const int64_t j = x / E, e = x - j * E;
+    const double2 v = IO[e * ns + pos[j]];
+    out[x] = inflow ? v.y : v.x;
+}
+
+hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, double* st_o,
+                                double* st_i, int64_t ns, int64_t E, hipStream_t s) {
     const int64_t cnt = ns * E;
     if (cnt == 0) return hipSuccess;
     hipLaunchKernelGGL(member_unpack, dim3((unsigned)((cnt + 255) / 256)), 256, 0, s,
-                       reinterpret_cast<const double2*>(IO), flags, G, wg_gmin, wbase, rs, O, mO,
-                       st_o, st_i, ns, cnt);
+                       reinterpret_cast<const double2*>(IO), flags, st_o, st_i, ns, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_io(const double* IO, const int64_t* pos, bool inflow, double* out,
+                            int64_t n, int64_t ns, int64_t E, hipStream_t s) {
+    if (n * E == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_io, dim3((unsigned)((n * E + 255) / 256)), 256, 0, s,
+                       reinterpret_cast<const double2*>(IO), pos, inflow, out, n, ns, E);
     return hipGetLastError();
 }
 

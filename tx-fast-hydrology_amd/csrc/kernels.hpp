@@ -144,11 +144,12 @@ hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t nslots, int
                                 int4 ent, const double* st_o, const double* st_i, double* IO,
                                 double* Qm, int64_t E, hipStream_t s);
 // After a member-dataflow step (which leaves each member's new {o, i} in IO): the session state
-// st_o / st_i and the T = 1 output windows O (member stride mO, row width rs).
-hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, const int32_t* G,
-                                const int32_t* wg_gmin, const int64_t* wbase, int rs, double* O,
-                                int64_t mO, double* st_o, double* st_i, int64_t nslots, int64_t E,
-                                hipStream_t s);
+// st_o / st_i.  IO keeps the step's outputs until the next run; launch_gather_io reads them in
+// caller order (out[j][e], the outflow or the inflow).
+hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, double* st_o,
+                                double* st_i, int64_t nslots, int64_t E, hipStream_t s);
+hipError_t launch_gather_io(const double* IO, const int64_t* pos, bool inflow, double* out,
+                            int64_t n, int64_t nslots, int64_t E, hipStream_t s);
 // Session state after a one-step run from its step-0 outputs:
 // st_o[e][pos[j]] = O, st_i[e][pos[j]] = the inflow fold of j (as the output gathers compute it)
 hipError_t launch_state_from_step(const double* O, int64_t mO, const int64_t* jbase,
