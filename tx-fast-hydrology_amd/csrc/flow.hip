@@ -4,10 +4,11 @@
 // G[j] + t, in-cluster upstreams one tick ahead through the LDS double buffer.  Instead of
 // cutting the horizon into launches of `tile` ticks, every workgroup of the network is resident
 // at once and walks its own tick window [gmin, gmax + T) chunk by chunk; registers and the LDS
-// double buffer persist across the horizon.  Inputs from other clusters (slack >= 2 chunks,
+// tick planes persist across the horizon; the workgroup's helper wave copies the plane of the
+// tick that just ended to the output window.  Inputs from other clusters (slack >= 2 chunks,
 // plan.hpp) travel as data-tagged granules: the producing lane writes {outflow, epoch} with a
-// write-through (sc1) 16-byte store, and a helper wave of the consuming workgroup prefetches the
-// next chunk's granules with sc1 loads, checks every tag and stages the values in an LDS ring
+// write-through (sc1) 16-byte store, and the helper wave of the consuming workgroup prefetches
+// the next chunk's granules with sc1 loads, checks every tag and stages the values in an LDS ring
 // (MI355X_MICROARCH.md, inter-workgroup visibility, granule form R2: no flag, no fence).  A tag
 // that is not yet current means the producer is behind: the helper polls that granule until it
 // is (bounded; on give-up it sets the status word and the run reports an error).
@@ -58,6 +59,7 @@ using dev::fold_values;
 using dev::read_inputs;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kHelperLanes = 64;                      // one helper wave per workgroup
 constexpr int kBatch = 8;                             // granules per helper lane per batch
@@ -220,6 +222,20 @@ void wavefront_flow(WaveArgs a) {
         Helper h{lds, xg, XE, XSLOT, EG, PL, tid & 63, e0, next * kChunk, T, a.epoch, a.status,
                  a.patience, false};
         const int nb = (h.nitems + kBatchItems - 1) / kBatchItems;   // <= 2 (host-checked)
+        // the outputs of tick k (plane k & 7, written by the compute waves before the barrier
+        // that ends tick k, overwritten at tick k + 8) -> row k of the workgroup's output window,
+        // 16 bytes per lane: the compute waves' tick loop issues no output stores
+        const int hl = tid & 63;
+        const int64_t wbh = a.wbase[w];
+        auto copy_row = [&](int k) {
+            if (MEMB || MCR_EXP_NO_STORES || k < gminw || k >= wend) return;   // wave-uniform
+            const char* src = lds + XB + (unsigned)(k & 7) * PL;
+            double* dst = a.O + wbh + (int64_t)(k - gminw) * RS;
+#pragma unroll
+            for (int c = 2 * hl; c < RS; c += 128)
+                __builtin_nontemporal_store(*reinterpret_cast<const f64x2*>(src + (unsigned)c * 8u),
+                                            reinterpret_cast<f64x2*>(dst + c));
+        };
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();                     // EG staged (LDS) before the helper reads it
         for (int b = 0; b < nb; ++b) h.fetch_now(b, kb, (unsigned)((kb >> 3) & 1));
@@ -234,21 +250,29 @@ void wavefront_flow(WaveArgs a) {
             if (pre) h.issue(0, kn, g);
             if (pre && nb > 1) h.issue(1, kn, g1);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 0
+            copy_row(kc);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 1
+            copy_row(kc + 1);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 2
+            copy_row(kc + 2);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 3
+            copy_row(kc + 3);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 4
             if (pre) {
                 const int bad = h.consume(0, kn, slot, g);
                 if (__any(bad >= 0)) h.settle(0, kn, slot, bad);
             }
+            copy_row(kc + 4);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 5
             if (pre && nb > 1) {
                 const int bad = h.consume(1, kn, slot, g1);
                 if (__any(bad >= 0)) h.settle(1, kn, slot, bad);
             }
+            copy_row(kc + 5);
             if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 6
+            copy_row(kc + 6);
             __syncthreads();                 // tick 7
+            copy_row(kc + 7);
         }
         return;
     }
@@ -257,7 +281,6 @@ void wavefront_flow(WaveArgs a) {
     const int lid = tid;                                // lane id over the compute waves
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
-    const int64_t wb = a.wbase[w];
     Slot S[K];                                          // every real slot runs steps 0 .. T-1
     uint64_t up[K];
 #pragma unroll
@@ -346,7 +369,7 @@ void wavefront_flow(WaveArgs a) {
                     rQ[p][r] = Qm[pa];
                 }
                 // the member's new state, in place of its inputs (read kRing ticks ago by this
-                // lane); launch_member_unpack forms the session state and output windows
+                // lane); launch_member_unpack forms the session state
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     const int e = k - S[p].G;
@@ -467,15 +490,12 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int p = 0; p < K; ++p)
                     *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
-                const bool inwin = k >= gminw && k < wend;
-                double* orow = inwin ? a.O + wb + (int64_t)(k - gminw) * RS : a.dummy;
+                // the tick's outputs reach the output window through the helper wave (plane
+                // k & 7 -> window row, copy_row; Texas det 0.515 -> 0.502 ms); the cross-cluster
+                // values leave from here (moving them to the helper too: 0.524, the helper's
+                // tick got longer than the compute waves')
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    if (!MCR_EXP_NO_STORES) {
-                        // non-temporal: rows are written once and read only by later fetches
-                        // (measured: Texas det horizon 0.734 -> 0.656 ms)
-                        __builtin_nontemporal_store(ov[p], orow + p * SLOTS + lid);
-                    }
                     if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T) {
                         const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
                         const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};

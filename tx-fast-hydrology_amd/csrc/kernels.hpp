@@ -114,8 +114,11 @@ inline size_t wavefront_lds_bytes(int slots, int chain, int table_cap, int ext_c
 }
 
 // dataflow kernel tick plane (flow.hip): every node slot, the zero slot and two chunk ring
-// slots of external inputs, 8 bytes each
-constexpr unsigned flow_plane_bytes(int rs) { return (unsigned)(rs + 1 + 2 * kFlowMaxExt) * 8u; }
+// slots of external inputs, 8 bytes each, padded to 16 bytes (the helper wave copies the node
+// slots of a plane to the output window with 16-byte LDS reads)
+constexpr unsigned flow_plane_bytes(int rs) {
+    return ((unsigned)(rs + 1 + 2 * kFlowMaxExt) * 8u + 15u) & ~15u;
+}
 
 inline size_t flow_lds_bytes(int slots, int chain, int T, int ext_cap) {
     (void)ext_cap;                               // external columns are sized for kFlowMaxExt
