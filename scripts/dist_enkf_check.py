@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
-    ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--reaches", type=int, default=20000)
     ap.add_argument("--members", type=int, default=8, help="members per rank")
     ap.add_argument("--gauges", type=int, default=50)
     args = ap.parse_args()
@@ -35,7 +35,7 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group(args.backend)
 
-    end = synthetic.river_network(args.n, 8, 300, np.random.default_rng(1))
+    end = synthetic.river_network(args.reaches, 8, 300, np.random.default_rng(1))
     n = end.size
     start = np.arange(n)
     indeg = orc.compute_indegree(start, end)
