@@ -171,7 +171,9 @@ def test_staged_driver_single_rank_equals_enkf_analysis():
     assert np.array_equal(oa, ob) and np.array_equal(ia, ib)
 
 
-@pytest.mark.parametrize("E,m", [(16, 40), (48, 12)])
+# (16, 40), (48, 12): the one-workgroup SPD solve; (96, 150), (200, 260): E > 64, the
+# factorisation and the two triangular solves of the large-ensemble path
+@pytest.mark.parametrize("E,m", [(16, 40), (48, 12), (96, 150), (200, 260)])
 def test_ensemble_space_solve_equals_observation_space(E, m):
     """Diagonal R with E <= m takes the E x E ensemble-space solve (push-through identity); a
     numerically identical R with a 1e-300 off-diagonal entry forces the m x m observation-space
