@@ -55,25 +55,40 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
     const int64_t kbeg = (int64_t)blockIdx.z * kc;
     const int64_t kend = kbeg + kc < K ? kbeg + kc : K;
     C += (int64_t)blockIdx.z * ldc * N;
-    for (int64_t k0 = kbeg; k0 < kend; k0 += kBK) {
+    // one K slice of both operands per thread (kTile * kBK / 256 elements each), read into
+    // registers one slice ahead: the next slice's loads are in flight during this slice's MFMAs
+    // (EnKF256 A Z 1.0 -> 0.72 ms per analysis)
+    constexpr int kPer = (kTile * kBK) / 256;
+    double ra[kPer], rb[kPer];
+    auto load_slice = [&](int64_t k0) {
 #pragma unroll
-        for (int r = 0; r < (kTile * kBK) / 256; ++r) {
+        for (int r = 0; r < kPer; ++r) {
             const int idx = tid + 256 * r;
             // coalesced along the contiguous dimension of each operand
             int i, k;
             if (TA) { k = idx % kBK; i = idx / kBK; } else { i = idx % kTile; k = idx / kTile; }
             const int64_t gi = row0 + i, gk = k0 + k;
-            double v = 0.0;
-            if (gi < M && gk < kend) v = TA ? A[gk + gi * lda] : A[gi + gk * lda];
-            As[k][i] = v;
+            ra[r] = (gi < M && gk < kend) ? (TA ? A[gk + gi * lda] : A[gi + gk * lda]) : 0.0;
             int j;
             if (TB) { j = idx % kTile; k = idx / kTile; } else { k = idx % kBK; j = idx / kBK; }
             const int64_t gj = col0 + j, gk2 = k0 + k;
-            double w = 0.0;
-            if (gj < N && gk2 < kend) w = TB ? B[gj + gk2 * ldb] : B[gk2 + gj * ldb];
-            Bs[k][j] = w;
+            rb[r] = (gj < N && gk2 < kend) ? (TB ? B[gj + gk2 * ldb] : B[gk2 + gj * ldb]) : 0.0;
+        }
+    };
+    if (kbeg < kend) load_slice(kbeg);
+    for (int64_t k0 = kbeg; k0 < kend; k0 += kBK) {
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int idx = tid + 256 * r;
+            int i, k;
+            if (TA) { k = idx % kBK; i = idx / kBK; } else { i = idx % kTile; k = idx / kTile; }
+            As[k][i] = ra[r];
+            int j;
+            if (TB) { j = idx % kTile; k = idx / kTile; } else { k = idx % kBK; j = idx / kBK; }
+            Bs[k][j] = rb[r];
         }
         __syncthreads();
+        if (k0 + kBK < kend) load_slice(k0 + kBK);
 #pragma unroll
         for (int kk = 0; kk < kBK; kk += 4) {
             // f64 16x16x4: A lane l holds A[l & 15][k = l >> 4], B lane l holds B[k = l >> 4][l & 15]
