@@ -236,8 +236,10 @@ __global__ void mean_anomalies(const double* __restrict__ X, double* __restrict_
     for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < ns;
          d += (int64_t)gridDim.x * blockDim.x) {
         double s = 0.0;
+#pragma unroll 8
         for (int64_t e = 0; e < E; ++e) s += X[e * ns + d];
         const double xbar = s / (double)E;
+#pragma unroll 8
         for (int64_t e = 0; e < E; ++e) A[e * ns + d] = X[e * ns + d] - xbar;
     }
 }
@@ -359,23 +361,44 @@ __global__ void unpack_slices(const double* __restrict__ in, double* __restrict_
 //   o_gain[j] = 0 + G[j] for reaches the reference walk processes, 0 otherwise;
 //   i_gain[j] = ((0 + o_gain[u1]) + o_gain[u2]) + ...  over j's routed upstreams in rank order;
 //   o += o_gain,  i += i_gain   (da.py:124-126)
-__global__ void apply_gain(const double* __restrict__ G, double* __restrict__ st_o,
-                           double* __restrict__ st_i, const uint8_t* __restrict__ flags,
-                           const int32_t* __restrict__ up_off, const int32_t* __restrict__ up,
-                           int64_t ns, int64_t E) {
-    const int64_t total = ns * E;
-    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
-         x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = x / ns;
-        const int64_t d = x - e * ns;
-        const uint8_t f = flags[d];
-        if (f != kSlotRouted && f != kSlotUnrouted) continue;   // padding / partial sums
-        const double* Ge = G + e * ns;
-        const double og = f == kSlotRouted ? 0.0 + Ge[d] : 0.0;
-        double ig = 0.0;
-        for (int32_t k = up_off[d]; k < up_off[d + 1]; ++k) ig = ig + (0.0 + Ge[up[k]]);
-        st_o[x] = st_o[x] + og;
-        st_i[x] = st_i[x] + ig;
+constexpr int kGainMembers = 4;   // members per thread in apply_gain
+__global__ __launch_bounds__(256) void apply_gain(const double* __restrict__ G,
+                                                  double* __restrict__ st_o,
+                                                  double* __restrict__ st_i,
+                                                  const uint8_t* __restrict__ flags,
+                                                  const int32_t* __restrict__ up_off,
+                                                  const int32_t* __restrict__ up, int64_t ns,
+                                                  int64_t E) {
+    // one slot (x) and kGainMembers members (y) per thread: the slot's upstream list is read
+    // once and the members' loads are independent (a grid-stride loop over [E][ns] with one
+    // element per iteration ran a 4-deep dependent load chain per element)
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= ns) return;
+    const uint8_t f = flags[d];
+    if (f != kSlotRouted && f != kSlotUnrouted) return;   // padding / partial sums
+    const int32_t u0 = up_off[d], u1 = up_off[d + 1];
+    const int64_t eb = (int64_t)blockIdx.y * kGainMembers;
+    double og[kGainMembers], ig[kGainMembers];
+#pragma unroll
+    for (int j = 0; j < kGainMembers; ++j) {
+        const int64_t e = eb + j < E ? eb + j : E - 1;
+        og[j] = f == kSlotRouted ? 0.0 + G[e * ns + d] : 0.0;
+        ig[j] = 0.0;
+    }
+    for (int32_t k = u0; k < u1; ++k) {
+        const int64_t u = up[k];
+#pragma unroll
+        for (int j = 0; j < kGainMembers; ++j) {
+            const int64_t e = eb + j < E ? eb + j : E - 1;
+            ig[j] = ig[j] + (0.0 + G[e * ns + u]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kGainMembers; ++j) {
+        if (eb + j >= E) break;
+        const int64_t x = (eb + j) * ns + d;
+        st_o[x] = st_o[x] + og[j];
+        st_i[x] = st_i[x] + ig[j];
     }
 }
 
@@ -520,8 +543,11 @@ hipError_t launch_unpack_slices(const double* in, double* G, int64_t ns, int64_t
 hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i, const uint8_t* flags,
                              const int32_t* up_off, const int32_t* up, int64_t ns, int64_t E,
                              hipStream_t s) {
-    hipLaunchKernelGGL(apply_gain, grid_for(ns * E, 256), 256, 0, s, G, st_o, st_i, flags,
-                       up_off, up, ns, E);
+    if (ns * E == 0) return hipSuccess;
+    const int64_t gy = (E + kGainMembers - 1) / kGainMembers;
+    if (gy > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(apply_gain, dim3((unsigned)((ns + 255) / 256), (unsigned)gy), 256, 0, s, G,
+                       st_o, st_i, flags, up_off, up, ns, E);
     return hipGetLastError();
 }
 
