@@ -68,7 +68,7 @@ def main():
         name = os.path.basename(f)[len(f"bench_{tag}_"):-4]
         lines[name] = last_json(f)
         json.dump(lines[name], open(os.path.join(P, f"{tag}_bench_{name}.json"), "w"), indent=1)
-    for name in ("det", "ens64", "enkf32", "kf"):
+    for name in ("det", "ens64", "enkf32", "enkf256", "kf"):
         src = os.path.join(O, f"prof_{name}", "run_kernel_stats.csv")
         if os.path.exists(src):
             shutil.copy(src, os.path.join(P, f"{tag}_{name}_kernel_stats.csv"))

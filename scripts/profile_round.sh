@@ -21,6 +21,7 @@ stats() {   # name, bench args
 stats det --steps 5 --warmup 1
 stats ens64 --steps 2 --warmup 1 --members 64
 stats enkf32 --steps 1 --warmup 1 --members 32 --enkf
+stats enkf256 --steps 1 --warmup 1 --members 256 --enkf
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$O/prof_kf" -o run \
     -- python3 "$PWD/scripts/bench_kf.py" --no-cpu --steps 1 > $O/prof_kf.log 2>&1 || exit $?
 BENCH_ARGS="" bash scripts/gpu_pmc.sh ${TAG}_hbm FETCH_SIZE WRITE_SIZE || exit $?
