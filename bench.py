@@ -1,25 +1,44 @@
 #!/usr/bin/env python3
 """Benchmark: reach·timesteps/s of the Muskingum routing hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): the full-Texas-scale synthetic network (190k reaches,
-~300 outlets, deepest flow path ~1500 reaches), deterministic run, 24 h at dt = 300 s
-(T = 288 steps), hourly lateral-inflow forcing (25 rows).  One bench "step" = one whole 24-h
-horizon routed by `mc_run` (forcing interpolation + network routing for all 288 timesteps),
-inputs and outputs resident in HBM.
+Workloads (BASELINE.json configs, SURVEY §8d synthetic generators):
+  * N = 1 default -- configs[1]: the full-Texas-scale synthetic network (190k reaches, ~300
+    outlets, deepest flow path ~1500 reaches), deterministic, 24 h at dt = 300 s (T = 288),
+    hourly lateral-inflow forcing (25 rows).  One bench "step" = one whole 24-h horizon routed
+    by `mc_run` (forcing interpolation + routing of all 288 timesteps), inputs and outputs
+    resident in HBM.
+  * N > 1 default -- configs[3]: the 256-member Texas EnKF (ensemble Kalman analysis at every
+    step of the first 2 h, 500 gauges, R = 1e-2 I) with the members SHARDED over the ranks
+    (256 / N each; RCCL all-gather + all-to-all in the analysis, ensemble.py): strong scaling,
+    value = reach·member·timesteps of the whole ensemble / max-over-ranks time.  The replicated
+    deterministic run (every rank its own Texas replica, no collective, "weak") is measured
+    after it and reported in the same line under "det_replicas".
+  * --members 64 (configs[2]), --conus (configs[4], one GPU's 16-member share), --enkf,
+    --det (N > 1: the replicated deterministic line as the headline).
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): the deterministic run does not shard
- -- every rank routes its own independent replica (different forcing seed), no
-data-path collective; value = reach·timesteps of all ranks / max-over-ranks time ("weak").
+`--gpus N` without a launcher starts `torch.distributed.run --nproc-per-node N` on this script
+as a CHILD process (never exec) and exits with its status; under a launcher, --gpus must equal
+WORLD_SIZE.
 
-Prints ONE JSON line on rank 0 with `roofline` (HIP-event timed wavefront launches against the
-HBM roofline, algorithmic 72 B per reach·timestep) and `cpu_baseline` (the serial
-C transliteration of the reference loop, oracle/, timed on this host; rank 0 at N=1 only).
+Prints ONE JSON line on rank 0 with
+  * `roofline`: the contract's algorithmic figure (SURVEY §8d bytes per unit / HIP-event launch
+    time vs the HBM peak) and what bounds the kernel: `latency` (schedule ticks x the measured
+    floor of the bare tick chain, mc_probe_tick_floor), `compulsory` (bytes the horizon must
+    move: outflows written, forcing / coefficients / state read, state written) and `dram`
+    (rocprofv3 PMC bytes of THIS build, profiles/*_hbm_traffic*.json, source-hash checked);
+  * `cpu_baseline`: the oracle's C transliteration of the reference loop (oracle/, test
+    infrastructure used only here) timed on this host, rank 0 at N = 1 only;
+  * `api_ms_per_horizon` (det, N = 1): the drop-in `Muskingum.simulate` over the same horizon,
+    host fetch of every step's outflows and inflows included.
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,7 +53,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_UNIT = 72.0        # 7 f64 reads + 2 f64 writes per reach·timestep
 
 
-def parse():
+def parse(argv=None, world=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -48,12 +67,15 @@ def parse():
     # Texas network one resident dataflow launch (two workgroups per CU); ensemble forecasts run
     # the multi-launch path at 256
     ap.add_argument("--slots", type=int, default=0)
-    ap.add_argument("--members", type=int, default=1,
-                    help="ensemble members (BASELINE configs[2]: 64); 1 = deterministic")
+    ap.add_argument("--members", type=int, default=None,
+                    help="ensemble members (BASELINE configs[2]: 64); default 1 at N = 1, the "
+                         "256-member EnKF at N > 1")
     ap.add_argument("--enkf", action="store_true",
                     help="BASELINE configs[3]: --members is the TOTAL ensemble, sharded over the "
                          "ranks, with the ensemble Kalman analysis at every step of the first "
                          "2 h (hourly gauge observations)")
+    ap.add_argument("--det", action="store_true",
+                    help="N > 1: the replicated deterministic run as the headline line")
     ap.add_argument("--gauges", type=int, default=500)
     ap.add_argument("--obs-hours", type=float, default=2.0)
     ap.add_argument("--one-plan", action="store_true",
@@ -61,44 +83,89 @@ def parse():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--chain", type=int, default=0,
                     help="node slots per lane (plan.hpp lane chains); 0 = per workload")
-    ap.add_argument("--vec-shape", default="",
-                    help="route with the member-vector sweep at shape H:W (node slots per wave "
-                         "instruction, waves per workgroup; 0 = automatic)")
     ap.add_argument("--conus", action="store_true",
                     help="BASELINE configs[4]: CONUS NWM-scale synthetic network (2.7M reaches, "
                          "4000 outlets, deepest path ~7000 reaches); --members per GPU (default "
                          "16: the 128-member ensemble over 8 GPUs, one 16-member shard per rank)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-api", action="store_true", help="skip the Muskingum.simulate timing")
     ap.add_argument("--timing-runs", type=int, default=3)
-    return apply_presets(ap.parse_args())
+    args = ap.parse_args(argv)
+    if world is None:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+    return apply_presets(args, world)
+
+
+def apply_presets(args, world=1):
+    if args.conus:
+        args.n, args.basins, args.depth = 2_700_000, 4000, 7000
+        if args.members is None:
+            args.members = 16
+    if args.members is None:
+        if world > 1 and not args.det:
+            args.members, args.enkf = 256, True      # BASELINE configs[3], members sharded
+        else:
+            args.members = 1
+    return args
+
+
+def launch_plan(gpus, env):
+    """("spawn", N): start N ranks of this script under torch.distributed.run as a child;
+    ("run", world): this process is one of `world` ranks (or the only one).  A launcher whose
+    world size differs from --gpus is an error (it would silently measure another GPU count)."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    launched = "RANK" in env or "LOCAL_RANK" in env
+    if gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if not launched and world == 1:
+        return ("spawn", gpus) if gpus > 1 else ("run", 1)
+    if gpus != world:
+        raise SystemExit(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return ("run", world)
+
+
+def spawn_ranks(n):
+    """One rank per GPU: torch.distributed.run on this script as a child process (never exec:
+    on this pool a process that touched the GPU must not be replaced); its stdout is ours."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def measured_traffic(info, n, T, E=1):
     """HBM bytes per launch of the routing kernel measured with rocprofv3 PMC counters for this
-    exact workload (scripts/hbm_traffic.py -> profiles/*_hbm_traffic.json), newest first."""
+    exact workload AND this build (scripts/hbm_traffic.py -> profiles/*_hbm_traffic*.json,
+    stamped with _build.source_hash()), newest first.  A profile of another build is refused."""
     import glob
+
+    from tx_fast_hydrology_amd._build import source_hash
     want = {"slots": info["slots"], "tile": info["tile"], "n": n, "T": T}
     if E > 1:
         want["E"] = E
+    h = source_hash()
+    stale = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic*.json")),
                     reverse=True):
         try:
             rec = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if rec.get("workload") == want:
-            rec["file"] = os.path.relpath(f, ROOT)
-            return rec
-    return None
-
-
-def apply_presets(args):
-    if args.conus:
-        args.n, args.basins, args.depth = 2_700_000, 4000, 7000
-        if args.members == 1:
-            args.members = 16
-    return args
+        if rec.get("workload") != want:
+            continue
+        if rec.get("source_hash") != h:
+            stale = stale or os.path.relpath(f, ROOT)
+            continue
+        rec["file"] = os.path.relpath(f, ROOT)
+        return rec, None
+    return None, (f"no PMC profile of this build (source hash {h})" +
+                  (f"; {stale} is of another build" if stale else ""))
 
 
 def build_workload(args, rank=0, world=1):
@@ -126,6 +193,7 @@ def build_workload(args, rank=0, world=1):
     x = xp[0] + dt * 1e9 * np.arange(1, args.T + 1)
     E = args.members
     enkf = None
+    K_arr, X_arr = K, X
     if args.enkf:
         if E % world or E < 2:
             raise SystemExit("--enkf needs >= 2 members, divisible by the number of ranks")
@@ -158,16 +226,11 @@ def build_workload(args, rank=0, world=1):
     # the resident dataflow kernels (det horizon, EnKF member steps); ensemble forecasts 256
     slots = args.slots or (192 if E == 1 or enkf is not None else 256)
     # ensemble forecasts (multi-launch path): 64-tick launches amortise the per-launch slot
-    # loads (Texas ens64 14.1 -> 13.1 ms per horizon); the EnKF keeps 32, whose shorter
-    # schedule its one-step member-dataflow launches pay for at every analysis
-    # the dataflow workloads at a 16-tick cross-cluster slack (two chunks, the minimum): Texas
-    # det 0.605 -> 0.594 ms
+    # loads (Texas ens64 14.1 -> 13.1 ms per horizon); the dataflow workloads at a 16-tick
+    # cross-cluster slack (two chunks, the minimum): Texas det 0.605 -> 0.594 ms
     tile = args.tile or (64 if E > 1 and enkf is None else 16)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E,
                             chain=args.chain)
-    if args.vec_shape:         # the member-vector sweep (mcroute.h mode 3) at this shape
-        net.set_mode("vector")
-        net.set_vector_shape(*(int(v) for v in args.vec_shape.split(":")))
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
@@ -180,7 +243,7 @@ def build_workload(args, rank=0, world=1):
         enkf.fnet = fnet
     w = SimpleNamespace(n=n, start=start, end=end, indeg=indeg, alpha=alpha, beta=beta, chi=chi,
                         gamma=gamma, o0=o0, i0=i0, x=x, xp=xp, fp=fp, rows=rows, dt=dt, E=E,
-                        enkf=enkf)
+                        enkf=enkf, K=K_arr, X=X_arr, xp_ns=xp_ns)
     return net, w
 
 
@@ -198,6 +261,14 @@ def workload_name(wl, E):
                 "24 h @ 300 s")
     return (f"texas-ens{E} (BASELINE configs[2]): full-Texas synthetic network, {E}-member "
             f"ensemble forecast, 24 h @ 300 s")
+
+
+def compulsory_bytes(n, E, T, rows):
+    """Bytes one horizon must move at least (SURVEY §8d data, counted once): every step's
+    outflow written (the inflows are recomputed from them, kernels.hpp), the forcing rows and
+    the four coefficient arrays read, the state {o, i} read at the start and written at the
+    end.  (The reference additionally writes every step's inflows: +T n E 8.)"""
+    return 8.0 * n * (E * T + E * rows + 4 + 4 * E)
 
 
 def cpu_enkf_baseline(args, wl, orc):
@@ -239,28 +310,118 @@ def cpu_enkf_baseline(args, wl, orc):
                       f"(OpenMP) + NumPy ensemble analysis + C _apply_gain, {t:.1f} s"}
 
 
+def cpu_baseline(args, wl, orc, E, x):
+    n = wl.n
+    if wl.enkf is not None:
+        return cpu_enkf_baseline(args, wl, orc)
+    if E > 1:
+        # E independent member runs over the host cores the box gives this job (OpenMP)
+        cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+        ms = min(E, cores)
+        o_s = np.ascontiguousarray(wl.o0[:, :ms])
+        i_s = np.ascontiguousarray(wl.i0[:, :ms])
+        fps = np.ascontiguousarray(wl.fp[:, :, :ms])
+        # bounded sample: consecutive 12-step chunks of the horizon (wrapping) until the budget
+        steps_done, t_cpu, k = 0, 0.0, 0
+        while t_cpu < args.cpu_seconds or steps_done == 0:
+            xs = x[k:k + 12]
+            c0 = time.perf_counter()
+            o_s, i_s = orc.simulate_members(wl.start, wl.end, wl.indeg, wl.alpha, wl.beta,
+                                            wl.chi, wl.gamma, o_s, i_s, xs, wl.xp, fps,
+                                            threads=cores)
+            t_cpu += time.perf_counter() - c0
+            steps_done += xs.size
+            k = (k + xs.size) % x.size
+        return {"value": float(n) * ms * steps_done / t_cpu,
+                "unit": "reach·member·timesteps/s", "cores": cores, "kind": "port",
+                "sample": f"{steps_done} timesteps (12-step chunks of the 24 h horizon, "
+                          f"T={args.T}) of {ms} members on the same {n}-reach network, C member "
+                          f"loop (-O3 -ffp-contract=off, OpenMP over members), {t_cpu:.1f} s"}
+    o_s, i_s = wl.o0.copy(), wl.i0.copy()
+    reps, t_cpu = 0, 0.0
+    while t_cpu < args.cpu_seconds or reps == 0:
+        c0 = time.perf_counter()
+        orc.simulate(wl.start, wl.end, wl.indeg, wl.alpha, wl.beta, wl.chi, wl.gamma, o_s,
+                     i_s, x, wl.xp, wl.fp, keep_outputs=False)
+        t_cpu += time.perf_counter() - c0
+        reps += 1
+    return {"value": float(n) * args.T * reps / t_cpu, "unit": "reach·timesteps/s",
+            "cores": 1, "kind": "port",
+            "sample": f"{reps} x full 24 h horizon (T={args.T}) on the same {n}-reach "
+                      f"network, serial C (-O3 -ffp-contract=off), {t_cpu:.1f} s"}
+
+
+def api_timing(wl, runs=2):
+    """ms per horizon of the drop-in API: Muskingum.simulate (tx_fast_hydrology interface,
+    muskingum.py:499-536) over the same network, forcing frame and 24-h horizon, iterating
+    every step (each yields fresh writable host arrays of that step's outflows and inflows)."""
+    import pandas as pd
+
+    from tx_fast_hydrology_amd.muskingum import Muskingum
+    n = wl.n
+    reach_ids = [f"r{j}" for j in range(n)]
+    start = pd.Timestamp(int(wl.xp_ns[0]), tz="UTC")
+    model = Muskingum({"name": "texas", "datetime": start,
+                       "timedelta": pd.to_timedelta(wl.dt, unit="s"), "reach_ids": reach_ids,
+                       "startnodes": wl.start.astype(np.int64),
+                       "endnodes": wl.end.astype(np.int64), "K": wl.K.astype(np.float64),
+                       "X": wl.X.astype(np.float64), "o_t": wl.o0.astype(np.float64)})
+    idx = pd.DatetimeIndex(pd.to_datetime(wl.xp_ns, utc=True))
+    df = pd.DataFrame(wl.fp, index=idx, columns=reach_ids)
+    end_time = start + pd.to_timedelta(wl.dt * wl.x.size, unit="s")
+    times = []
+    for r in range(runs + 1):                  # the first run builds the device session
+        model.datetime = start
+        t0 = time.perf_counter()
+        steps = 0
+        for _ in model.simulate(df, end_time=end_time, o_t_init=wl.o0):
+            steps += 1
+        if r:
+            times.append(time.perf_counter() - t0)
+    assert steps == wl.x.size, steps
+    model.close()
+    return 1e3 * min(times)
+
+
 def main():
     args = parse()
+    what, world = launch_plan(args.gpus, os.environ)
+    if what == "spawn":
+        sys.exit(spawn_ranks(world))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     dist = None
     if world > 1:
+        import datetime as _dt
+
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", timeout=_dt.timedelta(seconds=600))
     else:
         torch.cuda.set_device(0)
 
     from oracle import oracle as orc  # noqa: F401  (cpu_baseline leg only)
+    from tx_fast_hydrology_amd import engine, ensemble
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(v):
+        if dist is None:
+            return v
+        tt = torch.tensor([v], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
 
     # ---- workload -------------------------------------------------------------------------
     t_setup = time.time()
     net, wl = build_workload(args, rank, world)
     n, x = wl.n, wl.x
-    from tx_fast_hydrology_amd import ensemble
 
     def horizon():
         """One bench step: a 24-h horizon (with the analysis steps of the EnKF workload)."""
@@ -280,12 +441,6 @@ def main():
     info = net.info
     setup_s = time.time() - t_setup
 
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     # ---- warmup + timed region -------------------------------------------------------------
     for _ in range(args.warmup):
         horizon()
@@ -294,11 +449,7 @@ def main():
     for _ in range(args.steps):
         horizon()
     barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     E = wl.E
     if wl.enkf is not None:            # one ensemble sharded over the ranks (strong scaling)
         units = float(n) * wl.enkf.E_total * args.T * args.steps
@@ -320,71 +471,88 @@ def main():
         tm["kernel_ms"] += t_["kernel_ms"]
         tm["launches"] += t_["launches"]
         nt.set_timing(False)
-    launch_ms = tm["kernel_ms"] / max(tm["launches"], 1)
+    launches = max(tm["launches"], 1)
+    launch_ms = tm["kernel_ms"] / launches
+    path = net.mode()[1]
+    kernel = "wavefront_flow" if path == "dataflow" else "wavefront_det"
     # 72 B per reach·timestep deterministic, 40 + 32/E per reach·member·timestep
     per_unit = BYTES_PER_UNIT if E == 1 else 40.0 + 32.0 / E
-    bytes_per_launch = per_unit * n * E * args.T * args.timing_runs / max(tm["launches"], 1)
+    bytes_per_launch = per_unit * n * E * args.T * args.timing_runs / launches
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-    traffic = measured_traffic(info, n, args.T, E) if wl.enkf is None else None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
-                "traffic_source": traffic["file"] if traffic else None,
-                # measured HBM bytes per launch / launch time: the DRAM rate the kernel drives
-                "traffic_gbs": (round(traffic["traffic_bytes_per_launch"] / (launch_ms * 1e-3)
-                                      / 1e9, 3) if traffic else None),
-                # the same DRAM rate as a fraction of the HBM peak: the routing recurrence keeps
-                # coefficients and state in registers / LDS and is bound by its dependency chain
-                # (schedule ticks x per-tick latency), not by DRAM bandwidth
-                "dram_frac": (round(traffic["traffic_bytes_per_launch"] / (launch_ms * 1e-3)
-                                    / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
-                "algorithmic_bytes_per_unit": per_unit,
-                "kernel": {"dataflow": "wavefront_flow", "vector": "wavefront_vec"}.get(
-                    net.mode()[1], "wavefront_det"),
-                "launches_per_step": tm["launches"] / args.timing_runs,
-                "avg_launch_us": round(launch_ms * 1e3, 3),
+    launches_per_step = tm["launches"] / args.timing_runs
+    comp = compulsory_bytes(n, E, args.T, wl.rows) / launches_per_step
+    roofline = {"bound": "latency", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "algorithmic_bytes_per_unit": per_unit, "kernel": kernel,
+                "launches_per_step": launches_per_step, "avg_launch_us": round(launch_ms * 1e3, 3),
                 "kernel_ms_per_step": round(tm["kernel_ms"] / args.timing_runs, 4)}
+    # the routing recurrence keeps coefficients and state in registers / LDS: it is bound by its
+    # dependency chain (schedule ticks x per-tick latency), not by DRAM bandwidth
+    if wl.enkf is None and E == 1 and path == "dataflow" and info["chain"] == 2 and \
+            info["slots"] in (192, 384):
+        ticks = info["gmax"] + args.T
+        ns_tick = engine.probe_tick_floor(info["slots"], info["chain"], 8192)
+        floor_ms = ticks * ns_tick * 1e-6
+        roofline["latency"] = {
+            "schedule_ticks": ticks, "ns_per_tick": round(launch_ms * 1e6 / ticks, 2),
+            "floor_ns_per_tick": round(ns_tick, 2), "floor_ms": round(floor_ms, 4),
+            "frac": round(floor_ms / launch_ms, 4),
+            "floor": "mc_probe_tick_floor: the bare tick chain of this kernel shape (LDS inputs, "
+                     "chained updates, LDS outputs, barrier; 2 workgroups per CU, no memory "
+                     "traffic), measured now on this device"}
+    else:
+        roofline["latency"] = None
+    roofline["compulsory"] = {
+        "bytes_per_launch": comp, "gbs": round(comp / (launch_ms * 1e-3) / 1e9, 3),
+        "frac": round(comp / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "counts": "outflows written + forcing, coefficients, state read + state written"}
+    if wl.enkf is None:
+        traffic, note = measured_traffic(info, n, args.T, E)
+    else:
+        traffic, note = None, "EnKF horizon: several kernels, no single-kernel PMC profile"
+    if traffic:
+        tb = traffic["traffic_bytes_per_launch"]
+        roofline["traffic"] = tb
+        roofline["dram"] = {"source": traffic["file"], "source_hash": traffic["source_hash"],
+                            "bytes_per_launch": tb, "read_bytes": traffic["read_bytes"],
+                            "write_bytes": traffic["write_bytes"],
+                            "gbs": round(tb / (launch_ms * 1e-3) / 1e9, 3),
+                            "frac": round(tb / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "over_compulsory": round(tb / comp, 3)}
+    else:
+        roofline["dram"] = {"source": None, "note": note}
 
     # ---- CPU baseline (serial transliteration of the reference loop, rank 0 at N=1) --------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and wl.enkf is not None:
-        cpu = cpu_enkf_baseline(args, wl, orc)
-    elif rank == 0 and world == 1 and not args.no_cpu and E > 1:
-        # E independent member runs over the host cores the box gives this job (OpenMP)
-        cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
-        ms = min(E, cores)
-        o_s = np.ascontiguousarray(wl.o0[:, :ms])
-        i_s = np.ascontiguousarray(wl.i0[:, :ms])
-        fps = np.ascontiguousarray(wl.fp[:, :, :ms])
-        # bounded sample: consecutive 12-step chunks of the horizon (wrapping) until the budget
-        steps_done, t_cpu, k = 0, 0.0, 0
-        while t_cpu < args.cpu_seconds or steps_done == 0:
-            xs = x[k:k + 12]
-            c0 = time.perf_counter()
-            o_s, i_s = orc.simulate_members(wl.start, wl.end, wl.indeg, wl.alpha, wl.beta,
-                                            wl.chi, wl.gamma, o_s, i_s, xs, wl.xp, fps,
-                                            threads=cores)
-            t_cpu += time.perf_counter() - c0
-            steps_done += xs.size
-            k = (k + xs.size) % x.size
-        cpu = {"value": float(n) * ms * steps_done / t_cpu,
-               "unit": "reach·member·timesteps/s", "cores": cores, "kind": "port",
-               "sample": f"{steps_done} timesteps (12-step chunks of the 24 h horizon, T={args.T}) "
-                         f"of {ms} members on the same {n}-reach network, C member loop (-O3 "
-                         f"-ffp-contract=off, OpenMP over members), {t_cpu:.1f} s"}
-    elif rank == 0 and world == 1 and not args.no_cpu:
-        o_s, i_s = wl.o0.copy(), wl.i0.copy()
-        reps, t_cpu = 0, 0.0
-        while t_cpu < args.cpu_seconds or reps == 0:
-            c0 = time.perf_counter()
-            orc.simulate(wl.start, wl.end, wl.indeg, wl.alpha, wl.beta, wl.chi, wl.gamma, o_s,
-                         i_s, x, wl.xp, wl.fp, keep_outputs=False)
-            t_cpu += time.perf_counter() - c0
-            reps += 1
-        cpu = {"value": float(n) * args.T * reps / t_cpu, "unit": "reach·timesteps/s",
-               "cores": 1, "kind": "port",
-               "sample": f"{reps} x full 24 h horizon (T={args.T}) on the same {n}-reach "
-                         f"network, serial C (-O3 -ffp-contract=off), {t_cpu:.1f} s"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, wl, orc, E, x)
+
+    # ---- the drop-in API over the same horizon (det, N = 1) ---------------------------------
+    api_ms = None
+    if world == 1 and E == 1 and wl.enkf is None and not args.no_api and wl.n < 1_000_000:
+        api_ms = api_timing(wl)
+
+    # ---- N > 1 EnKF headline: the replicated deterministic run as well ----------------------
+    det_rep = None
+    if world > 1 and wl.enkf is not None:
+        for nt in nets:
+            nt.close()
+        dargs = copy.copy(args)
+        dargs.members, dargs.enkf, dargs.slots, dargs.tile = 1, False, 0, 0
+        dnet, dwl = build_workload(dargs, rank, world)
+        for _ in range(max(args.warmup, 1)):
+            dnet.run(dwl.x)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            dnet.run(dwl.x)
+        barrier()
+        de = max_over_ranks(time.perf_counter() - t0)
+        det_rep = {"value": float(dwl.n) * args.T * args.steps * world / de,
+                   "unit": "reach·timesteps/s", "ms_per_horizon": de / args.steps * 1e3,
+                   "scaling": "weak", "parallelism": f"replicas x{world}",
+                   "workload": workload_name(dwl, 1)}
+        dnet.close()
 
     if rank == 0:
         line = {
@@ -419,6 +587,12 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu"] = value / cpu["value"]
+        if api_ms is not None:
+            line["api_ms_per_horizon"] = round(api_ms, 3)
+            line["api_path"] = ("Muskingum.simulate over the same 24 h horizon, every step "
+                                "iterated (host outflows and inflows of each step)")
+        if det_rep is not None:
+            line["det_replicas"] = det_rep
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -20,7 +20,12 @@
  *   - the library never retains a caller pointer past the call;
  *   - a session handle is not thread-safe: use one thread per handle (or lock externally);
  *   - results are bit-identical to the reference's float64 arithmetic (same association, no
- *     FMA contraction, inflows summed in the reference's finalisation order).
+ *     FMA contraction, inflows summed in the reference's finalisation order) for FINITE inputs.
+ *     The kernels evaluate a clamped forcing step as (1 - 0) f + 0 f and give unrouted reaches
+ *     and padding slots zero coefficients instead of branching, so an Inf / NaN forcing value
+ *     or state on an unrouted reach, or an Inf forcing row beyond the last interpolation
+ *     point, yields NaN where the reference copies the row or keeps o = 0 (nutils.py:24-27,
+ *     72-88).  Non-finite inputs are outside the contract (no reference test pins them).
  */
 #ifndef MCROUTE_H
 #define MCROUTE_H
@@ -205,17 +210,10 @@ int mc_reset_timing(void* net);
 
 /* Execution path of mc_run / mc_step.  mode 0 (default): one resident dataflow launch for the
  * whole horizon when the network fits the device at once, else launches of `tile` ticks;
- * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit);
- * 3: the member-vector sweep (ensembles of E = a multiple of 16 members on a 64-lane plan:
- * lanes are members, launches of `tile` ticks; MC_E_STATE for a session it cannot route).
- * last_path: 1, 2 or 3 = the path the last run took (0 before any run). */
+ * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit).
+ * last_path: 1 or 2 = the path the last run took (0 before any run). */
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);
-/* Shape of the member-vector sweep: node slots per wave instruction (1, 2 or 4: 64, 32 or 16
- * members each) and waves per workgroup (4, 8 or 16); 0 = automatic.  A shape without a kernel
- * instantiation (or whose member width does not divide E) makes the session fall back to the
- * other paths (mode 3: MC_E_STATE). */
-int mc_set_vector_shape(void* net, int nodes_per_instr, int waves);
 
 /* How long a dataflow wait polls a stale upstream value before it gives up, in ticks of the
  * device's 100 MHz wall clock (0 = the default 2 s; < 0 = give up at once, for tests).  A run
@@ -223,6 +221,13 @@ int mc_set_vector_shape(void* net, int nodes_per_instr, int waves);
  * dataflow run since the previous one, the library routes the same horizon again from its
  * input state with launches (last_path then reads 1); otherwise that call fails (MC_E_HIP). */
 int mc_set_flow_patience(void* net, int64_t wall_ticks);
+
+/* Diagnostic (bench.py roofline): device time per tick of the bare dataflow tick chain -- LDS
+ * inputs of the previous tick, `chain` chained Muskingum updates per lane, LDS outputs, the
+ * workgroup barrier -- for the (slots, chain) = (192, 2) / (384, 2) kernel shape, two resident
+ * workgroups per CU on the current device, no global memory traffic.  Schedule ticks x
+ * *ns_per_tick is the latency floor of a horizon.  ticks: a multiple of 8. */
+int mc_probe_tick_floor(int32_t slots, int32_t chain, int64_t ticks, double* ns_per_tick);
 
 /* Launch trace of the last mc_run (off by default; diagnostic).  One record of 8 int64 per
  * workgroup per launch: {launch, workgroup, t_start, t_loop, t_end, hw_id, c_loop, c_end}.

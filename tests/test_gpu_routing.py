@@ -424,3 +424,75 @@ def test_dataflow_give_up_reroutes_with_launches():
     net.run(x)
     got_o, _ = net.fetch_outputs()
     assert net.mode()[1] == "dataflow" and np.array_equal(got_o, want_o)
+
+
+def test_dataflow_give_up_then_state_changes(exec_mode):
+    """a call that changes the state, coefficients or forcing right after a dataflow
+    horizon whose waits gave up must not lose its change to the re-run of that horizon (nor
+    replay the horizon with the new coefficients / a freed forcing buffer).  Each case: run with
+    patience < 0, then the change, then fetch -- the horizon's outputs are the old inputs'
+    (re-routed), and the change is in effect afterwards."""
+    from tx_fast_hydrology_amd import _native as nat  # noqa: F401
+    end = synthetic.texas(seed=0)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=0)
+    indeg, heads, coef, _, i0 = _model(end, K, X, 300.0, o0=o0)
+    xp, fp = synthetic.forcing(n, rows=6, seed=1)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 49)
+    start = np.arange(n)
+    want_o, want_i, fo, fi = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=192, tile=16)
+    net.load_forcing(xp, fp)
+    flow = exec_mode != "launches"
+
+    def give_up_run():
+        net.set_flow_patience(-1)
+        net.set_state(o0, i0)
+        net.run(x)
+
+    def check_outputs():
+        got_o, got_i = net.fetch_outputs()
+        assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+        if flow:
+            assert net.mode()[1] == "launches"          # given up and re-routed
+        net.set_flow_patience(0)
+
+    # set_state after the run: the caller's state survives the re-run
+    o1 = o0 * 1.5
+    i1 = orc.init_inflows(start, end, o1)
+    give_up_run()
+    net.set_state(o1, i1)
+    check_outputs()
+    so, si = net.get_state()
+    assert np.array_equal(so, o1) and np.array_equal(si, i1)
+
+    # apply_gain after the run: the gain lands on the horizon's final state
+    gain = np.random.default_rng(3).normal(0.0, 0.1, n)
+    give_up_run()
+    net.apply_gain(gain)
+    check_outputs()
+    ig, og = orc.apply_gain(heads, end, gain, indeg)
+    so, si = net.get_state()
+    assert np.array_equal(so, fo + og) and np.array_equal(si, fi + ig)
+
+    # set_coeffs after the run: the horizon keeps its coefficients, the next run the new ones
+    coef2 = orc.muskingum_coeffs(K, X, 600.0)
+    give_up_run()
+    net.set_coeffs(*coef2)
+    check_outputs()
+    net.set_state(o0, i0)
+    net.run(x)
+    w2_o, _, _, _ = orc.simulate(start, end, indeg, *coef2, o0, i0, x, xp, fp)
+    assert np.array_equal(net.fetch_outputs()[0], w2_o)
+    net.set_coeffs(*coef)
+
+    # load_forcing after the run (the old forcing buffer is replaced): re-run reads the old one
+    fp2 = fp * 2.0
+    give_up_run()
+    net.load_forcing(xp, fp2)
+    check_outputs()
+    net.set_state(o0, i0)
+    net.run(x)
+    w3_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp2)
+    assert np.array_equal(net.fetch_outputs()[0], w3_o)

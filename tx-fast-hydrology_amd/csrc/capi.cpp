@@ -35,9 +35,6 @@ mcr::PlanParams to_params(const mc_plan_params* pp) {
         if (pp->tile) p.tile = pp->tile;
         if (pp->ext_cap) p.ext_cap = pp->ext_cap;
         if (pp->chain) p.chain = pp->chain;
-        // 64-lane plans serve the member-vector ensemble kernel, which stages at most
-        // kVecMaxExt external inputs per workgroup
-        if (!pp->ext_cap && p.slots == 64) p.ext_cap = mcr::kVecMaxExt / 2;
     }
     return p;
 }
@@ -180,17 +177,6 @@ struct Net {
     int force_mode = -1;             // >= 0: mode override during a re-run
     int64_t patience = mcr::kFlowPatience;   // dataflow waits (mc_set_flow_patience)
 
-    // member-vector ensemble sweep (vector.hip): node records, external-input sources,
-    // member-minor forcing / state, and whether the last run's outputs are in its layout
-    // OM[slot][t][e] (fetches then read them through vjbase[j] = pos[j] * T * E)
-    bool vec_plan = false;           // 64-lane plan within the kernel's external-input cap
-    int vec_waves = 8;               // waves per workgroup
-    DBuf<mcr::VecMeta> vmeta;
-    DBuf<int64_t> vext_slot, vjbase;
-    DBuf<double> FMv, SMo, SMi;
-    bool fm_valid = false;
-    int64_t vjbase_E = 0, vjbase_T = 0;
-    bool out_vec = false;
     // outputs of the last run are the {o, i} pairs of a member-dataflow step (Qm + nslots * E)
     bool out_io = false;
 
@@ -269,7 +255,6 @@ struct Net {
             for (size_t w = 0; w < ids.size(); ++w) ids[w] = (int32_t)w;
             all_wg.upload(ids.data(), ids.size(), stream);
         }
-        init_vec();
         status.reserve(1);
         HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
         HIPC(hipHostMalloc(reinterpret_cast<void**>(&status_host), sizeof(int32_t),
@@ -277,134 +262,6 @@ struct Net {
         *status_host = 0;
         sync();
     }
-
-    // Node records of the member-vector kernel (codes -> plane columns; coefficients are filled
-    // in by set_coeffs).  Only 64-lane plans whose workgroups stay within kVecMaxExt external
-    // inputs qualify.
-    void init_vec() {
-        const int64_t RS = (int64_t)plan.p.chain * plan.p.slots;
-        vec_plan = plan.p.slots == 64 && plan.max_ext_wg <= mcr::kVecMaxExt && plan.nslots > 0 &&
-                   plan.nslots < (1ll << 31);
-        if (!vec_plan) return;
-        std::vector<mcr::VecMeta> m((size_t)plan.nslots);
-        for (int64_t d = 0; d < plan.nslots; ++d) {
-            mcr::VecMeta& r = m[d];
-            r.al = r.be = r.ch = r.ga = 0.0;
-            r.cnt = r.chained = r.pad = 0;
-            for (int u = 0; u < 4; ++u) r.in[u] = (int32_t)RS;
-            if (plan.flags[d] == mcr::kSlotPad) {
-                r.G = 1 << 29;
-                continue;
-            }
-            r.G = plan.G[d];
-            int k = 0;
-            for (int u = 0; u < plan.up_cnt[d]; ++u) {
-                const unsigned code = (unsigned)((plan.up4[d] >> (16 * u)) & 0xffffu);
-                if (code == mcr::kSelfCode) {
-                    r.chained = 1;
-                } else if (code & mcr::kExtBit) {
-                    r.in[k++] = (int32_t)(RS + 1 + (code & 0x7fffu));
-                } else {
-                    r.in[k++] = (int32_t)code;
-                }
-            }
-            r.cnt = k;
-        }
-        vmeta.upload(m.data(), m.size(), stream);
-        std::vector<int64_t> xs(plan.ext_src.size());
-        for (size_t x = 0; x < xs.size(); ++x) {
-            const int64_t src = plan.ext_src[x];
-            xs[x] = src < plan.n ? plan.pos[src] : src - plan.n;
-        }
-        vext_slot.upload(xs.data(), xs.size(), stream);
-        vext_slot.reserve(1);
-        sync();
-    }
-
-    // nodes per wave instruction (64 / H members each) of the member-vector kernel for this
-    // ensemble, and its waves per workgroup (H = 0: not eligible).  mc_set_vector_shape pins
-    // either; by default the first instantiated shape in the order below (measured: Texas
-    // ens64, 4 nodes x 16 members per instruction in 16-wave workgroups is the fastest)
-    int vec_pin_h = 0, vec_pin_w = 0;
-    int vec_H() {
-        if (!vec_plan || E < 2) return 0;
-        for (int H : {4, 2, 1}) {
-            if (vec_pin_h && H != vec_pin_h) continue;
-            if (E % (64 / H) != 0) continue;
-            for (int W : {16, 8, 4}) {
-                if (vec_pin_w && W != vec_pin_w) continue;
-                if (mcr::vec_shape_ok(plan.p.slots, plan.p.chain, W, H)) {
-                    vec_waves = W;
-                    return H;
-                }
-            }
-        }
-        return 0;
-    }
-
-    // T steps of all members with the member-vector kernel (vector.hip): node-major
-    // member-minor layouts FM [ns][rows][E], SM [ns][E], outputs [ns][T][E]
-    void run_vec(int64_t T, int H) {
-        const int64_t ns = plan.nslots, rows = n_rows;
-        const int Ew = 64 / H;
-        REQUIRE((int64_t)H * std::max(T, rows) * E * 8 < (1ll << 31),
-                "horizon x members too large for the member-vector path");
-        if (!fm_valid) {            // forcing [E][rows][ns] -> [ns][rows][E], row by row
-            FMv.reserve((size_t)(rows * ns * E));
-            for (int64_t r = 0; r < rows; ++r)
-                HIPC(mcr::launch_transpose_ld(F.p + r * ns, rows * ns, FMv.p + r * E, rows * E,
-                                              E, ns, stream));
-            fm_valid = true;
-        }
-        SMo.reserve((size_t)(ns * E));
-        SMi.reserve((size_t)(ns * E));
-        HIPC(mcr::launch_transpose(st_o.p, SMo.p, E, ns, 1, stream));
-        HIPC(mcr::launch_transpose(st_i.p, SMi.p, E, ns, 1, stream));
-        O.reserve((size_t)(T * ns * E));
-        if (vjbase_E != E || vjbase_T != T) {
-            std::vector<int64_t> jb((size_t)std::max<int64_t>(plan.n, 1));
-            for (int64_t j = 0; j < plan.n; ++j) jb[j] = plan.pos[j] * T * E;
-            vjbase.upload(jb.data(), jb.size(), stream);
-            vjbase_E = E;
-            vjbase_T = T;
-        }
-        mcr::VecArgs a{};
-        a.meta = vmeta.p;
-        a.wg_gmin = wg_gmin.p;
-        a.wg_gmax = wg_gmax.p;
-        a.ext_off = ext_off.p;
-        a.ext_slot = vext_slot.p;
-        a.ext_g = ext_g.p;
-        a.stab = stab.p;
-        a.FM = FMv.p;
-        a.SM_o = SMo.p;
-        a.SM_i = SMi.p;
-        a.OM = O.p;
-        a.nslots = ns;
-        a.E = E;
-        a.n_rows = (int32_t)rows;
-        a.T = (int32_t)T;
-        a.tile = plan.p.tile;
-        const int64_t nl = (int64_t)cur->off.size() - 1;
-        int64_t launched = 0;
-        for (int64_t k = 0; k < nl; ++k) {
-            const int64_t grid = cur->off[k + 1] - cur->off[k];
-            if (grid == 0) continue;
-            a.active = cur->active.p + cur->off[k];
-            a.kappa0 = (int32_t)(k * plan.p.tile);
-            if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-            HIPC(mcr::launch_vec(a, (int)grid, (int)(E / Ew), plan.p.chain, vec_waves, H,
-                                 stream));
-            if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
-            ++launched;
-        }
-        HIPC(mcr::launch_transpose(SMo.p, st_o.p, ns, E, 1, stream));
-        HIPC(mcr::launch_transpose(SMi.p, st_i.p, ns, E, 1, stream));
-        out_vec = true;
-        last_path = 3;
-        vec_launched = launched;
-    }
-    int64_t vec_launched = 0;
 
     // Copy k elements host -> device without waiting for the stream: the source is staged in a
     // pinned slot whose previous copy (8 uploads ago) must have completed.
@@ -525,6 +382,13 @@ struct Net {
     void settle() {
         if (flow_runs > 0) sync();
     }
+    // Before a call changes the state, coefficients or forcing: a pending dataflow horizon that
+    // could still be re-routed on give-up (sync) is resolved first, so the re-run can never
+    // replay it over the caller's change or from a freed forcing buffer.  Member
+    // steps are never re-routed (last_flow.valid is false), so the EnKF cycle does not sync here.
+    void settle_state() {
+        if (flow_runs > 0 && last_flow.valid) sync();
+    }
 
     void from_slots(const DBuf<double>& src, double* host, int64_t m = 1) {
         const int64_t n = plan.n;
@@ -541,6 +405,7 @@ struct Net {
     void apply_gain(const double* gain) {
         REQUIRE(plan.n == 0 || gain, "gain must not be NULL");
         if (plan.n == 0) return;
+        settle_state();
         const size_t ns = (size_t)plan.nslots;
         Gn.reserve(ns * E);
         to_slots(gain, Gn, E);
@@ -590,6 +455,7 @@ struct Net {
     void analysis_setup(int64_t m, const int64_t* gauges, const double* y, const double* R) {
         REQUIRE(E >= 2, "the ensemble analysis needs at least 2 members");
         REQUIRE(m >= 1 && m < (1ll << 31) && gauges && R, "bad gauge arguments");
+        settle_state();
         const int64_t n = plan.n, ns = plan.nslots;
         std::vector<int64_t> gs(m);
         for (int64_t g = 0; g < m; ++g) {
@@ -638,6 +504,7 @@ struct Net {
     // local members: HX [E][m] (gauge outflows), D [E][m] = y[g][e] - HX
     void ens_gauges(int64_t m, const int64_t* gauges, const double* y, double* HX, double* D) {
         REQUIRE(y && HX && D, "null argument");
+        settle_state();
         upload_gauges(m, gauges);
         upload_async(Yb, y, (size_t)(m * E));
         HIPC(mcr::launch_gauge_values(st_o.p, gslot.p, Yb.p, HX, D, m, plan.nslots, E, stream));
@@ -646,6 +513,7 @@ struct Net {
     // local member states -> reach slices for every rank: send [N][E][S]
     void ens_pack(int64_t N, double* send) {
         REQUIRE(N >= 1 && send, "bad pack arguments");
+        settle_state();
         HIPC(mcr::launch_pack_slices(st_o.p, send, plan.nslots, E, slice_size(N), N, stream));
     }
 
@@ -745,6 +613,7 @@ struct Net {
     // increments of the local members from every rank's slice (Grecv [N][E][S]) -> _apply_gain
     void ens_unpack_apply(int64_t N, const double* Grecv) {
         REQUIRE(N >= 1 && Grecv, "bad unpack arguments");
+        settle_state();
         const int64_t ns = plan.nslots;
         Gn.reserve((size_t)(ns * E));
         HIPC(mcr::launch_unpack_slices(Grecv, Gn.p, ns, E, slice_size(N), N, stream));
@@ -789,6 +658,7 @@ struct Net {
 
     void set_members(int64_t m) {
         REQUIRE(m >= 1 && m <= 65535, "members must be in [1, 65535]");
+        settle_state();
         sync();
         E = m;
         const size_t ns = (size_t)std::max<int64_t>(plan.nslots, 1);
@@ -799,12 +669,12 @@ struct Net {
         dummy.reserve(mcr::kDummyPerMember * m);
         n_rows = 0;                    // forcing and outputs are per member: load again
         T_out = 0;
-        fm_valid = false;
         sync();
     }
 
     void set_coeffs(const double* a, const double* b, const double* c, const double* g) {
         REQUIRE(plan.n == 0 || (a && b && c && g), "coefficient arrays must not be NULL");
+        settle_state();
         to_slots(a, alpha);
         to_slots(b, beta);
         to_slots(c, chi);
@@ -812,15 +682,13 @@ struct Net {
         // partial sums pass their fold through, unrouted reaches and padding output 0
         HIPC(mcr::launch_set_slot_coeffs(flags.p, alpha.p, beta.p, chi.p, gamma.p, plan.nslots,
                                          stream));
-        if (vec_plan)
-            HIPC(mcr::launch_vec_meta_coeffs(alpha.p, beta.p, chi.p, gamma.p, vmeta.p,
-                                             plan.nslots, stream));
         sync();  // `stage` is reused by the next call
         coeffs_set = true;
     }
 
     void set_state(const double* o, const double* i) {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
+        settle_state();
         to_slots(o, st_o, E);
         sync();
         to_slots(i, st_i, E);
@@ -877,6 +745,10 @@ struct Net {
     void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int4>& tabh) {
         REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
         REQUIRE(T >= 1 && T < (1ll << 30), "T out of range");
+        // a second run before the first was synchronised: the first can no longer be re-routed
+        // on give-up (its input state is about to be overwritten), so a give-up of either is
+        // reported as an error, never replayed over this run
+        if (flow_runs > 0) last_flow.valid = false;
         const int64_t n = plan.n;
         T_out = 0;
         if (n == 0) {
@@ -934,27 +806,9 @@ struct Net {
         int64_t launched = 0;
         trace_launch.clear();
         trace_wg.clear();
-        out_vec = false;
         out_io = false;
         size_t flds = 0;
         {
-            // ---- the member-vector sweep (vector.hip), on request: bit-identical to the other
-            // paths, but measured slower than the multi-launch sweep on Texas ens64 (DESIGN.md
-            // §6), so mode 0 does not choose it
-            const int H = mode == 3 ? vec_H() : 0;
-            const bool want = mode == 3;
-            if (mode == 3 && (H == 0 || Fsrc != F.p))
-                throw Fail(MC_E_STATE, "member-vector mode needs an ensemble (E a multiple of 16) "
-                                       "on a 64-lane plan within the kernel's external-input "
-                                       "cap, routed with mc_run");
-            if (want && H > 0 && Fsrc == F.p && !trace) {
-                run_vec(T, H);
-                launched = vec_launched;
-            }
-        }
-        if (last_path == 3) {
-            // outputs and state are complete; timing below
-        } else {
             if (E > 1 && mode == 2 && T != 1)
                 throw Fail(MC_E_STATE, "dataflow mode routes one member, or one step of an ensemble");
             if (E > 1 && T == 1 && members_fit(flds)) {
@@ -1093,10 +947,10 @@ struct Net {
         REQUIRE(xps && (plan.n == 0 || fp), "xp/fp must not be NULL");
         for (int64_t r = 1; r < rows; ++r)
             REQUIRE(!(xps[r] < xps[r - 1]), "xp must be sorted ascending");
+        settle_state();
         const int64_t n = plan.n;
         xp.assign(xps, xps + rows);
         n_rows = rows;
-        fm_valid = false;
         F.reserve((size_t)(rows * plan.nslots * E));
         if (n == 0) return;
         DBuf<double> tmp;
@@ -1156,9 +1010,6 @@ struct Net {
             if (out_io)                    // T = 1: t0 = 0, t1 = 1
                 HIPC(mcr::launch_gather_io(Qm.p + plan.nslots * E, pos.p, c == 1, outT.p, n,
                                            plan.nslots, E, stream));
-            else if (out_vec)
-                HIPC(mcr::launch_gather_steps(O.p, 1, vjbase.p, in_off.p, in_list.p, c == 1,
-                                              (int)E, outT.p, n, t0, t1, E, stream));
             else
                 HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p,
                                               in_list.p, c == 1, row_width(), outT.p, n, t0, t1,
@@ -1182,9 +1033,6 @@ struct Net {
             if (out_io)                    // T = 1: [j][0][e] is the step layout
                 HIPC(mcr::launch_gather_io(Qm.p + plan.nslots * E, pos.p, k == 1, outT.p, n,
                                            plan.nslots, E, stream));
-            else if (out_vec)
-                HIPC(mcr::launch_gather_series(O.p, 1, vjbase.p, in_off.p, in_list.p, k == 1,
-                                               (int)E, outT.p, n, T_out, E, stream));
             else
                 HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p,
                                                in_list.p, k == 1, row_width(), outT.p, n, T_out,
@@ -1398,6 +1246,7 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         const int64_t n = D->plan.n, E = D->E;
         if (n == 0) return;
         S->settle();
+        D->settle_state();
         // order: after the source's pending work, on the destination's stream; the source waits
         // for the copy before it may overwrite its state again
         hipEvent_t ev;
@@ -1485,22 +1334,8 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 3,
-                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow) or 3 (member-vector)");
+        REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
         as_net(net)->mode = mode;
-    });
-}
-
-int mc_set_vector_shape(void* net, int nodes_per_instr, int waves) {
-    return guarded([&] {
-        REQUIRE(nodes_per_instr == 0 || nodes_per_instr == 1 || nodes_per_instr == 2 ||
-                    nodes_per_instr == 4,
-                "nodes per instruction must be 0 (auto), 1, 2 or 4");
-        REQUIRE(waves == 0 || waves == 4 || waves == 8 || waves == 16,
-                "waves must be 0 (auto), 4, 8 or 16");
-        Net* N = as_net(net);
-        N->vec_pin_h = nodes_per_instr;
-        N->vec_pin_w = waves;
     });
 }
 
@@ -1508,6 +1343,42 @@ int mc_set_flow_patience(void* net, int64_t wall_ticks) {
     return guarded([&] {
         Net* N = as_net(net);
         N->patience = wall_ticks == 0 ? mcr::kFlowPatience : std::max<int64_t>(wall_ticks, 0);
+    });
+}
+
+int mc_probe_tick_floor(int32_t slots, int32_t chain, int64_t ticks, double* ns_per_tick) {
+    return guarded([&] {
+        REQUIRE(ns_per_tick && ticks > 0 && ticks % mcr::kChunk == 0 && ticks < (1ll << 30),
+                "ticks must be a positive multiple of 8");
+        REQUIRE((slots == 192 || slots == 384) && chain == 2, "instantiated: (192, 2), (384, 2)");
+        int dev = 0, cus = 0;
+        HIPC(hipGetDevice(&dev));
+        HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        const int grid = (slots == 192 ? 2 : 1) * cus;
+        hipStream_t s = nullptr;
+        HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        struct Guard {
+            hipStream_t s;
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            ~Guard() {
+                if (e0) (void)hipEventDestroy(e0);
+                if (e1) (void)hipEventDestroy(e1);
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamDestroy(s);
+            }
+        } g{s};
+        DBuf<double> out;
+        out.reserve((size_t)grid * slots);
+        HIPC(hipEventCreate(&g.e0));
+        HIPC(hipEventCreate(&g.e1));
+        HIPC(mcr::probe_tick_floor(slots, chain, grid, 64, s, out.p));     // warm-up
+        HIPC(hipEventRecord(g.e0, s));
+        HIPC(mcr::probe_tick_floor(slots, chain, grid, (int)ticks, s, out.p));
+        HIPC(hipEventRecord(g.e1, s));
+        HIPC(hipEventSynchronize(g.e1));
+        float ms = 0.f;
+        HIPC(hipEventElapsedTime(&ms, g.e0, g.e1));
+        *ns_per_tick = (double)ms * 1e6 / (double)ticks;
     });
 }
 

@@ -686,4 +686,82 @@ hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_r
     return hipGetLastError();
 }
 
+// ---- latency floor of the dataflow tick (diagnostic, mc_probe_tick_floor) -------------------
+// The irreducible per-tick chain of wavefront_flow<SLOTS, K> with no memory traffic: every lane
+// reads two inputs of each position from the previous tick plane (LDS), folds them, runs its K
+// chained Muskingum updates, writes the outputs to the current plane and joins the workgroup's
+// tick barrier (with the helper wave, which here only joins the barriers).  Same block shape,
+// waves-per-EU bound and LDS request as the real kernel, two workgroups per CU: ticks x this
+// kernel's time per tick is the schedule's latency floor (bench.py roofline.latency).
+template <int SLOTS, int K>
+__global__ __launch_bounds__(SLOTS + kHelperLanes)
+__attribute__((amdgpu_waves_per_eu(2, 2)))
+void tick_floor(int ticks, double* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RS = K * SLOTS;
+    constexpr unsigned PL = flow_plane_bytes(RS);
+    const int tid = threadIdx.x;
+    if ((tid >> 6) == SLOTS / 64) {
+        __syncthreads();
+        for (int k = 0; k < ticks; ++k) __syncthreads();
+        return;
+    }
+    unsigned m[K][2], own[K];
+    double op[K], ip[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        m[p][0] = (unsigned)((p * SLOTS + tid + 1) % RS) * 8u;
+        m[p][1] = (unsigned)((p * SLOTS + tid + 65) % RS) * 8u;
+        own[p] = (unsigned)(p * SLOTS + tid) * 8u;
+        op[p] = 1.0 + tid;
+        ip[p] = 2.0;
+        for (int k = 0; k < kChunk; ++k)
+            *reinterpret_cast<double*>(lds + own[p] + (unsigned)k * PL) = 1.0;
+    }
+    const double al = 0.1, be = 0.1, ch = 0.2, ga = 0.5, q = 1.0 + 1e-3 * tid;
+    __syncthreads();
+    for (int kc = 0; kc < ticks; kc += kChunk) {
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) {
+            const unsigned rd = (unsigned)((i + 7) & 7) * PL;
+            double v[K][2];
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                v[p][0] = lds_f64(lds, m[p][0] + rd);
+                v[p][1] = lds_f64(lds, m[p][1] + rd);
+            }
+            double prev = 0.0;
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                double I = v[p][0] + v[p][1];
+                if (p > 0) I = I + prev;
+                const double o = 0.0 + (((al * I + be * ip[p]) + ch * op[p]) + ga * q);
+                op[p] = o;
+                ip[p] = I;
+                prev = o;
+            }
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+                *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = op[p];
+            __syncthreads();
+        }
+    }
+    out[(int64_t)blockIdx.x * SLOTS + tid] = op[K - 1];
+}
+
+hipError_t probe_tick_floor(int slots, int chain, int grid, int ticks, hipStream_t s,
+                            double* out) {
+    if (ticks <= 0 || ticks % kChunk != 0 || grid <= 0) return hipErrorInvalidValue;
+    const size_t lds = flow_lds_bytes(slots, chain, 288, kFlowMaxExt);
+    if (slots == 192 && chain == 2)
+        hipLaunchKernelGGL((tick_floor<192, 2>), dim3(grid), dim3(192 + kHelperLanes), lds, s,
+                           ticks, out);
+    else if (slots == 384 && chain == 2)
+        hipLaunchKernelGGL((tick_floor<384, 2>), dim3(grid), dim3(384 + kHelperLanes), lds, s,
+                           ticks, out);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 }  // namespace mcr

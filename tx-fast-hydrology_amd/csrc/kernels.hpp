@@ -160,64 +160,11 @@ hipError_t launch_state_from_step(const double* O, int64_t mO, const int64_t* jb
                                   const int64_t* pos, int slots, double* st_o, double* st_i,
                                   int64_t n, int64_t nslots, int64_t E, hipStream_t s);
 
-// ---- member-vector ensemble sweep (vector.hip): lanes are members, Ew = 64 / H per node.
-// Plans of 64 lanes (slots = 64) at chain K; W waves per workgroup.  (K, W, H) instantiated:
-#define MCR_VEC_SHAPES(X)                                                                   \
-    X(1, 8, 1) X(1, 16, 1) X(1, 8, 2) X(1, 16, 2) X(1, 4, 4) X(1, 8, 4) X(1, 16, 4) X(2, 16, 2) \
-    X(2, 8, 4) X(2, 16, 4)
-// external inputs per workgroup the member-vector kernel stages in its tick planes; 64-lane
-// plans default to a soft cap of half that (a single cluster may exceed a soft cap: Texas at
-// cap 32 has at most 38 per workgroup at chain 1, 48 at chain 2)
-constexpr int kVecMaxExt = 64;
-// ticks between the issue of a forcing / external-input load and the tick that uses it
-constexpr int kVecPrefetch = 2;
-
-// Per node slot, built once per plan (codes) and per coefficient upload (al .. ga)
-struct alignas(16) VecMeta {
-    double al, be, ch, ga;
-    int32_t G;            // tick of step 0 (1 << 29 for padding: never active)
-    int32_t cnt;          // inputs read from the plane (the chained input not counted)
-    int32_t chained;      // 1: the previous position's output of the tick is the last input
-    int32_t pad;
-    int32_t in[4];        // plane columns of the inputs in fold order: workgroup-local slot,
-                          // RS (zero column) when unused, RS + 1 + x for external input x
-};
-
-struct VecArgs {
-    const int32_t* active;     // workgroups of this launch
-    const VecMeta* meta;       // [nslots]
-    const int32_t* wg_gmin;
-    const int32_t* wg_gmax;
-    const int32_t* ext_off;    // [nwg + 1]
-    const int64_t* ext_slot;   // node slot producing each external input
-    const int32_t* ext_g;      // G of the consuming node
-    const int4* stab;          // per step {row_lo, row_hi, frac}
-    const double* FM;          // forcing [nslots][n_rows][E]
-    double* SM_o;              // state [nslots][E], read at a launch's first tick, written back
-    double* SM_i;
-    double* OM;                // outputs [nslots][T][E]
-    int64_t nslots;
-    int64_t E;
-    int32_t n_rows;
-    int32_t T;
-    int32_t kappa0;
-    int32_t tile;
-};
-
-bool vec_shape_ok(int slots, int chain, int waves, int H);
-size_t vec_lds_bytes(int chain, int H, int tile);
-// grid = active workgroups x member blocks (E / Ew)
-hipError_t launch_vec(const VecArgs& a, int grid, int member_blocks, int chain, int waves, int H,
-                      hipStream_t s);
-hipError_t vec_occupancy(int chain, int waves, int H, int tile, int* blocks_per_cu);
-// dst[c * dst_ld + r] = src[r * src_ld + c]  (r < rows, c < cols)
-hipError_t launch_transpose_ld(const double* src, int64_t src_ld, double* dst, int64_t dst_ld,
-                               int64_t rows, int64_t cols, hipStream_t s);
-// dst[b][c][r] = src[b][r][c]
-hipError_t launch_transpose(const double* src, double* dst, int64_t rows, int64_t cols,
-                            int64_t batch, hipStream_t s);
-hipError_t launch_vec_meta_coeffs(const double* alpha, const double* beta, const double* chi,
-                                  const double* gamma, VecMeta* meta, int64_t ns, hipStream_t s);
+// Latency floor of the dataflow tick (flow.hip tick_floor): `ticks` ticks of the bare per-tick
+// chain (LDS inputs, chained updates, LDS outputs, barrier) on `grid` workgroups of the
+// (slots, chain) shape; out: grid * slots doubles.  (192, 2) and (384, 2) are instantiated.
+hipError_t probe_tick_floor(int slots, int chain, int grid, int ticks, hipStream_t s,
+                            double* out);
 
 // dense: the step table has a kChunk-step window spanning more than 3 forcing rows.
 // members: ensemble members (grid y); member strides are in `a`.

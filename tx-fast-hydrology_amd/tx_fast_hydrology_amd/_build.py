@@ -4,6 +4,9 @@ The library is compiled with ``hipcc --offload-arch=gfx950`` directly from ``csr
 lands next to this file (``lib/libmcroute.so``) so it travels with the repository snapshot.
 ``-ffp-contract=off`` is load-bearing: the routing arithmetic must keep separate multiply and add
 roundings to match the reference bit for bit.
+
+Every source compiles to its own object (``lib/obj/``) in parallel; an object is rebuilt when
+its source or any header is newer, then the objects are linked.
 """
 from __future__ import annotations
 
@@ -12,15 +15,20 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 SRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 REPO = os.path.dirname(os.path.dirname(PKG_DIR))
 INCLUDE = os.path.join(REPO, "include")
 LIB_DIR = os.path.join(PKG_DIR, "lib")
+OBJ_DIR = os.path.join(LIB_DIR, "obj")
 LIB_PATH = os.path.join(LIB_DIR, "libmcroute.so")
 
 ARCH = os.environ.get("MCROUTE_ARCH", "gfx950")
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+         "-fno-fast-math", "-Wall", "-Wno-unused-function"]
+LIBS = ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _hipcc() -> str:
@@ -35,24 +43,59 @@ def sources():
                   glob.glob(os.path.join(SRC_DIR, "*.hip")))
 
 
+def _headers():
+    return glob.glob(os.path.join(SRC_DIR, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of every library source, header and the compile flags: the
+    identity of a build.  Profiles measured on a build carry it (scripts/hbm_traffic.py) and
+    bench.py reports a profile only for the build it was measured on."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for p in sorted(sources() + _headers()):
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _obj(src: str) -> str:
+    return os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+
+
 def _stale() -> bool:
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    deps = sources() + glob.glob(os.path.join(SRC_DIR, "*.hpp")) + \
-        glob.glob(os.path.join(INCLUDE, "*.h"))
-    return any(os.path.getmtime(p) > t for p in deps)
+    return any(os.path.getmtime(p) > t for p in sources() + _headers())
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    hipcc = _hipcc()
+    t_hdr = max((os.path.getmtime(p) for p in _headers()), default=0.0)
+
+    def compile_one(src):
+        obj = _obj(src)
+        if (not force and os.path.exists(obj) and
+                os.path.getmtime(obj) >= max(os.path.getmtime(src), t_hdr)):
+            return
+        tmp = obj + f".{os.getpid()}.tmp"
+        cmd = [hipcc] + FLAGS + ["-I", INCLUDE, "-I", SRC_DIR, "-c", "-o", tmp, src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(tmp, obj)
+
+    srcs = sources()
+    with ThreadPoolExecutor(max_workers=min(len(srcs), 6)) as ex:
+        list(ex.map(compile_one, srcs))
     tmp = LIB_PATH + f".{os.getpid()}.tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
-           "-I", INCLUDE, "-I", SRC_DIR, "-o", tmp] + sources() + \
-        ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + \
+        [_obj(s) for s in srcs] + LIBS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -103,7 +103,7 @@ SIGNATURES = {
     "mc_ens_unpack_apply": (_i32, [_vp, _i64, _vp]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_set_flow_patience": (_i32, [_vp, _i64]),
-    "mc_set_vector_shape": (_i32, [_vp, ctypes.c_int, ctypes.c_int]),
+    "mc_probe_tick_floor": (_i32, [ctypes.c_int32, ctypes.c_int32, _i64, ctypes.POINTER(ctypes.c_double)]),
     "mc_get_mode": (_i32, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),
     "mc_get_trace": (_i32, [_vp, _vp, _i64, ctypes.POINTER(ctypes.c_int64),

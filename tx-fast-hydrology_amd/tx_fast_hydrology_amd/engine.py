@@ -109,8 +109,10 @@ class RoutingNet:
         h = ctypes.c_void_p()
         if slots == 0 and members == 1:
             # 3 compute waves + the dataflow helper: one wave per SIMD (Texas det horizon 0.61 ms
-            # vs 0.66 at 384 lanes and 0.82 through the multi-launch path at 256)
+            # vs 0.66 at 384 lanes and 0.82 through the multi-launch path at 256), cross-cluster
+            # slack of two chunks (0.605 -> 0.594 ms)
             slots = 192
+            tile = tile or 16
         p = _params(slots, tile, ext_cap, chain)
         nat.check(L.mc_net_create(self.n, ptr(end), ptr(deg), ptr(heads), heads.size,
                                   ctypes.byref(p), ctypes.byref(h)))
@@ -287,17 +289,11 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
-    MODES = {"auto": 0, "launches": 1, "dataflow": 2, "vector": 3}
+    MODES = {"auto": 0, "launches": 1, "dataflow": 2}
 
     def set_mode(self, mode: str):
-        """Execution path: "auto" (default), "launches", "dataflow" or "vector" (the
-        member-vector ensemble sweep; see mcroute.h)."""
+        """Execution path: "auto" (default), "launches" or "dataflow" (see mcroute.h)."""
         nat.check(nat.lib().mc_set_mode(self._h, self.MODES[mode]))
-
-    def set_vector_shape(self, nodes_per_instr: int = 0, waves: int = 0):
-        """Member-vector sweep shape: node slots per wave instruction (1, 2, 4) and waves per
-        workgroup (4, 8, 16); 0 = automatic (mcroute.h mc_set_vector_shape)."""
-        nat.check(nat.lib().mc_set_vector_shape(self._h, int(nodes_per_instr), int(waves)))
 
     def set_flow_patience(self, wall_ticks: int):
         """Dataflow wait limit in 100 MHz wall-clock ticks (0 = default 2 s, < 0 = give up at
@@ -310,7 +306,7 @@ class RoutingNet:
         p = ctypes.c_int()
         nat.check(nat.lib().mc_get_mode(self._h, ctypes.byref(m), ctypes.byref(p)))
         names = {v: k for k, v in self.MODES.items()}
-        return names[m.value], {1: "launches", 2: "dataflow", 3: "vector"}.get(p.value)
+        return names[m.value], {1: "launches", 2: "dataflow"}.get(p.value)
 
     def set_trace(self, enable: bool):
         nat.check(nat.lib().mc_set_trace(self._h, 1 if enable else 0))
@@ -335,6 +331,15 @@ class RoutingNet:
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
+
+
+def probe_tick_floor(slots=192, chain=2, ticks=8192) -> float:
+    """Device ns per tick of the bare dataflow tick chain (mcroute.h mc_probe_tick_floor):
+    the latency floor bench.py multiplies by the schedule length."""
+    v = ctypes.c_double()
+    nat.check(nat.lib().mc_probe_tick_floor(int(slots), int(chain), int(ticks),
+                                            ctypes.byref(v)))
+    return v.value
 
 
 def ax_bu(startnodes, endnodes, alpha, beta, chi, gamma, i_t_prev, o_t_prev, q_t_next,
