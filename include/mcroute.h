@@ -222,6 +222,20 @@ int mc_get_mode(void* net, int* mode, int* last_path);
  * input state with launches (last_path then reads 1); otherwise that call fails (MC_E_HIP). */
 int mc_set_flow_patience(void* net, int64_t wall_ticks);
 
+/* Sub-basin coupling on the device (reference AsyncSimulation._accumulate, simulation.py:
+ * 137-166): adds the inflow correction of the upstream session's outlet reach `src_reach`
+ * (its outflow series of the last horizon, o_start = the outflow before that horizon) to the
+ * lateral-inflow forcing of reach `dst_reach` of the downstream session, row r:
+ *   F[r] += alpha * I(r + 1) / gamma + beta * I(r) / gamma   (I(0) = o_start),
+ * alpha / beta / gamma being the downstream reach's coefficients.  The destination's forcing
+ * must have one row per source step.  Ordered on the streams (after the source's run, before
+ * the destination's next call), no host synchronisation.  Single-member sessions. */
+int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_net,
+                              int64_t src_reach, double o_start, double alpha, double beta,
+                              double gamma);
+/* Horizons this session re-routed with launches after a dataflow wait gave up. */
+int mc_net_reroutes(const void* net, int64_t* count);
+
 /* Diagnostic (bench.py roofline): device time per tick of the bare dataflow tick chain -- LDS
  * inputs of the previous tick, `chain` chained Muskingum updates per lane, LDS outputs, the
  * workgroup barrier -- for the (slots, chain) = (192, 2) / (384, 2) kernel shape, two resident

@@ -125,3 +125,65 @@ def test_checkpoint_and_reload(golden):
     m.load_state()
     o2, i2, t2 = run(m, df)
     assert np.array_equal(o2, o[k + 1:]) and np.array_equal(i2, i[k + 1:])
+
+
+class _Idle(BaseCallback):
+    """A callback that never needs the steps: the per-sub-basin fused path still runs, but the
+    device DAG does not (it requires no callbacks), so the host driver routes the collection."""
+
+    def __idle_steps__(self):
+        return True
+
+
+def _split_case(n, n_cuts, seed, sibling_cuts=True):
+    from api_helpers import model_dict
+    from tx_fast_hydrology_amd import synthetic
+    from tx_fast_hydrology_amd.muskingum import Muskingum
+    rng = np.random.default_rng(seed)
+    end = synthetic.river_network(n, 3, max(40, n // 60), rng)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=seed)
+    start = pd.Timestamp("2024-05-01T00:00:00Z")
+    T = 24
+    whole = Muskingum(model_dict(end, K, X, o0, start, 3600.0, name="whole"))
+    idx = pd.date_range(start + pd.Timedelta(3600, unit="s"), periods=T, freq="1h", tz="UTC")
+    df = pd.DataFrame(rng.gamma(2.0, 0.5, (T, n)), index=idx, columns=whole.reach_ids)
+    indeg = whole.indegree
+    cand = np.flatnonzero((indeg > 0) & (end != np.arange(n)))
+    cuts = set(rng.choice(cand, size=n_cuts, replace=False).tolist())
+    if sibling_cuts:
+        # two cut reaches draining into the same entry reach: two corrections of one column
+        for d in np.flatnonzero(indeg >= 2):
+            ups = [u for u in np.flatnonzero(end == d) if indeg[u] > 0 and u != d]
+            if len(ups) >= 2:
+                cuts.update(ups[:2])
+                break
+    return whole, df, np.sort(np.array(sorted(cuts)))
+
+
+@pytest.mark.parametrize("n,n_cuts", [(3000, 12), (20000, 60)])
+def test_async_simulation_device_dag_equals_host_driver(n, n_cuts):
+    """The device DAG (every sub-basin launched on its stream, corrections added on the device)
+    is bit-identical to the host driver (outflow frames, corrected inputs, final states)."""
+    res = []
+    for device in (True, False):
+        whole, df, cuts = _split_case(n, n_cuts, 7 + n)
+        coll = whole.split(cuts, create_state_space=False)
+        assert len(coll.models) > n_cuts
+        if not device:
+            for m in coll.models.values():
+                m.bind_callback(_Idle(), key="idle")
+        sim = AsyncSimulation(coll, df)
+        outputs = asyncio.run(sim.simulate())
+        res.append((outputs, sim.inputs,
+                    {k: (m.o_t_next, m.i_t_next, m.o_t_prev, m.datetime)
+                     for k, m in coll.models.items()}))
+    (o_d, in_d, st_d), (o_h, in_h, st_h) = res
+    assert o_d.keys() == o_h.keys()
+    for k in o_h:
+        assert np.array_equal(o_d[k].values, o_h[k].values), k
+        assert o_d[k].index.equals(o_h[k].index), k
+        assert np.array_equal(in_d[k].values, in_h[k].values), k
+        for a, b in zip(st_d[k][:3], st_h[k][:3]):
+            assert np.array_equal(a, b), k
+        assert st_d[k][3] == st_h[k][3], k

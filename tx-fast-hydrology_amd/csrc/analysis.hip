@@ -8,7 +8,8 @@
 //       W = (HA HA^T / (E-1) + R)^-1 D,   D = Y - HX  (per-member innovations)
 //       G = A (HA^T W) / (E-1)             (per-member increments, = K D)
 //       o += 0 + G,  i += one-hop(G)       (rank-ordered sums, as _apply_gain)
-// The dense products run on f64 MFMA (v_mfma_f64_16x16x4f64); the m x m SPD solve is rocSOLVER.
+// The dense products run on f64 MFMA (v_mfma_f64_16x16x4f64); the SPD solves and the large
+// slice product are dense.hip.
 // Device arrays are member-major slot order ([E][nslots]) like the routing session.
 #include "analysis.hpp"
 #include "plan.hpp"
@@ -32,12 +33,16 @@ constexpr int kPad = 1;     // LDS row padding (f64)
 // Split-K (gridDim.z > 1): slice z covers k in [z * kc, (z + 1) * kc) and writes its raw
 // partial product to C + z * ldc * N (alpha = 1, beta = 0 passed by the launcher); splitk_reduce
 // sums the slices in order (deterministic).
+// Columns j >= n1 of op(B) come from B2 (column j - n1) and go to C2 (column j - n1): two
+// products sharing op(A) in one launch.
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
                                                   const double* __restrict__ A, int64_t lda,
                                                   const double* __restrict__ B, int64_t ldb,
                                                   double beta, double* __restrict__ C,
-                                                  int64_t ldc, int64_t kc) {
+                                                  int64_t ldc, int64_t kc,
+                                                  const double* __restrict__ B2, int64_t n1,
+                                                  double* __restrict__ C2) {
     __shared__ double As[kBK][kTile + kPad];   // As[k][i] = op(A)(row0 + i, k0 + k)
     __shared__ double Bs[kBK][kTile + kPad];   // Bs[k][j] = op(B)(k0 + k, col0 + j)
     const int tid = threadIdx.x;
@@ -55,6 +60,7 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
     const int64_t kbeg = (int64_t)blockIdx.z * kc;
     const int64_t kend = kbeg + kc < K ? kbeg + kc : K;
     C += (int64_t)blockIdx.z * ldc * N;
+    if (C2) C2 += (int64_t)blockIdx.z * ldc * N;
     // one K slice of both operands per thread (kTile * kBK / 256 elements each), read into
     // registers one slice ahead: the next slice's loads are in flight during this slice's MFMAs
     // (EnKF256 A Z 1.0 -> 0.72 ms per analysis)
@@ -72,7 +78,9 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
             int j;
             if (TB) { j = idx % kTile; k = idx / kTile; } else { k = idx % kBK; j = idx / kBK; }
             const int64_t gj = col0 + j, gk2 = k0 + k;
-            rb[r] = (gj < N && gk2 < kend) ? (TB ? B[gj + gk2 * ldb] : B[gk2 + gj * ldb]) : 0.0;
+            const double* Bp = gj < n1 ? B : B2;
+            const int64_t bj = gj < n1 ? gj : gj - n1;
+            rb[r] = (gj < N && gk2 < kend) ? (TB ? Bp[bj + gk2 * ldb] : Bp[gk2 + bj * ldb]) : 0.0;
         }
     };
     if (kbeg < kend) load_slice(kbeg);
@@ -114,21 +122,23 @@ __global__ __launch_bounds__(256) void dgemm_mfma(int64_t M, int64_t N, int64_t 
                 const int64_t gi = row0 + wr + 16 * i + (lane >> 4) + 4 * r;
                 const int64_t gj = col0 + wc + 16 * j + (lane & 15);
                 if (gi < M && gj < N) {
-                    double* c = C + gi + gj * ldc;
+                    double* c = gj < n1 ? C + gi + gj * ldc : C2 + gi + (gj - n1) * ldc;
                     *c = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *c;
                 }
             }
 }
 
-// C = alpha * (W[0] + W[1] + ... + W[splits-1]) + beta * C  (W[z]: M x N, leading dim M)
+// C = alpha * (W[0] + W[1] + ... + W[splits-1]) + beta * C  (W[z]: M x N, leading dim M;
+// columns j >= n1 go to C2)
 __global__ void splitk_reduce(const double* __restrict__ W, int splits, int64_t M, int64_t N,
-                              double alpha, double beta, double* __restrict__ C, int64_t ldc) {
+                              double alpha, double beta, double* __restrict__ C, int64_t ldc,
+                              int64_t n1, double* __restrict__ C2) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= M * N) return;
     const int64_t i = idx % M, j = idx / M;
     double acc = W[idx];
     for (int z = 1; z < splits; ++z) acc += W[(int64_t)z * M * N + idx];
-    double* c = C + i + j * ldc;
+    double* c = j < n1 ? C + i + j * ldc : C2 + i + (j - n1) * ldc;
     *c = beta == 0.0 ? alpha * acc : alpha * acc + beta * *c;
 }
 
@@ -139,95 +149,6 @@ __global__ void scale_rows(const double* __restrict__ HA, const double* __restri
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x)
         U[x] = HA[x] / r[x % m];
-}
-
-// Small SPD system M Z = V in one workgroup (k <= kSpdMax): right-looking Cholesky M = L L^T
-// and both triangular solves column-oriented over all right-hand sides at once (every step is
-// a parallel update between two barriers).  M, V column-major k x k; the solution overwrites V.  A pivot
-// <= 0 (not positive definite) stores j + 1 in info (rocSOLVER's convention) and zeroes V.
-// The ensemble-space analysis matrix M = I + S^T R^-1 S is k = E <= 64 in the EnKF cycle:
-// one launch replaces rocSOLVER's potrf + potrs small-size kernels (~65 us per analysis).
-constexpr int kSpdMax = 64;
-__global__ __launch_bounds__(256) void spd_solve_small(const double* __restrict__ M,
-                                                       double* __restrict__ V, int k,
-                                                       int32_t* __restrict__ info) {
-    __shared__ double L[kSpdMax][kSpdMax + 1];   // L[i][j], lower triangle
-    __shared__ double B[kSpdMax][kSpdMax + 1];   // B[i][c] = V(i, c)
-    __shared__ int bad;
-    const int tid = threadIdx.x;
-    for (int x = tid; x < k * k; x += 256) {
-        const int i = x % k, j = x / k;
-        L[i][j] = M[x];
-        B[i][j] = V[x];
-    }
-    if (tid == 0) bad = 0;
-    __syncthreads();
-    // right-looking Cholesky: pivot, scale the column below it, update the trailing triangle
-    for (int j = 0; j < k; ++j) {
-        if (tid == 0) {
-            const double d = L[j][j];
-            if (!(d > 0.0)) bad = j + 1;
-            L[j][j] = sqrt(d);
-        }
-        __syncthreads();
-        if (bad) break;
-        const double ljj = L[j][j];
-        for (int i = j + 1 + tid; i < k; i += 256) L[i][j] = L[i][j] / ljj;
-        __syncthreads();
-        const int r = k - j - 1;                      // trailing rows / columns
-        for (int x = tid; x < r * r; x += 256) {
-            const int i = j + 1 + x / r, c = j + 1 + x % r;
-            if (c <= i) L[i][c] = L[i][c] - L[i][j] * L[c][j];
-        }
-        __syncthreads();
-    }
-    if (bad) {                         // no usable solution: a zero update, reported at sync
-        for (int x = tid; x < k * k; x += 256) V[x] = 0.0;
-        if (tid == 0) *info = bad;
-        return;
-    }
-    // L Y = B, column-oriented: finish row i of every right-hand side, then eliminate it below
-    for (int i = 0; i < k; ++i) {
-        if (tid < k) B[i][tid] = B[i][tid] / L[i][i];
-        __syncthreads();
-        const int r = k - i - 1;
-        for (int x = tid; x < r * k; x += 256) {
-            const int t = i + 1 + x / k, c = x % k;
-            B[t][c] = B[t][c] - L[t][i] * B[i][c];
-        }
-        __syncthreads();
-    }
-    // L^T X = Y, backwards
-    for (int i = k - 1; i >= 0; --i) {
-        if (tid < k) B[i][tid] = B[i][tid] / L[i][i];
-        __syncthreads();
-        for (int x = tid; x < i * k; x += 256) {
-            const int t = x / k, c = x % k;
-            B[t][c] = B[t][c] - L[i][t] * B[i][c];
-        }
-        __syncthreads();
-    }
-    __syncthreads();
-    for (int x = tid; x < k * k; x += 256) V[x] = B[x % k][x / k];
-    if (tid == 0) *info = 0;
-}
-
-// X := 0 when the factorisation before it failed (*info != 0): a rocSOLVER potrs on a partly
-// factored matrix returns garbage, so the analysis increment becomes zero, as in spd_solve_small
-__global__ void zero_if_failed(double* __restrict__ X, int64_t cnt,
-                               const int32_t* __restrict__ info) {
-    if (*info == 0) return;
-    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < cnt;
-         x += (int64_t)gridDim.x * blockDim.x)
-        X[x] = 0.0;
-}
-
-// M = I (k x k, column-major)
-__global__ void set_identity(double* __restrict__ M, int64_t k) {
-    const int64_t total = k * k;
-    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
-         x += (int64_t)gridDim.x * blockDim.x)
-        M[x] = (x % k) == (x / k) ? 1.0 : 0.0;
 }
 
 // xbar[d] = (sum_e X[e][d]) / E ;  A[e][d] = X[e][d] - xbar[d]
@@ -253,6 +174,7 @@ __global__ void mean_anomalies(const double* __restrict__ X, double* __restrict_
 template <int MAXE>
 __global__ __launch_bounds__(256) void anomaly_increments(const double* __restrict__ X,
                                                           const double* __restrict__ Z,
+                                                          int64_t ldz,
                                                           double* __restrict__ G, int64_t S,
                                                           int Et) {
     // Zt[f][e] = Z[f + e Et]: the 8 coefficients of one anomaly for 8 consecutive outputs are
@@ -262,7 +184,7 @@ __global__ __launch_bounds__(256) void anomaly_increments(const double* __restri
     const int Ep = (Et + EG - 1) / EG * EG;               // padded row (zero columns)
     for (int i = threadIdx.x; i < MAXE * Ep && i < MAXE * MAXE; i += 256) {
         const int f = i / Ep, e = i - f * Ep;
-        Zt[i] = (f < Et && e < Et) ? Z[f + (int64_t)e * Et] : 0.0;
+        Zt[i] = (f < Et && e < Et) ? Z[f + (int64_t)e * ldz] : 0.0;
     }
     __syncthreads();
     const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -402,15 +324,15 @@ __global__ __launch_bounds__(256) void apply_gain(const double* __restrict__ G,
     }
 }
 
-// Kt[g + j m] (m x n, solved in place) -> K_out[j][g] in caller order: K_out[j * m + g]
-__global__ void gain_to_caller(const double* __restrict__ Kt, double* __restrict__ out,
+// Kt[g + j ldk] (m x n, solved in place) -> K_out[j][g] in caller order: K_out[j * m + g]
+__global__ void gain_to_caller(const double* __restrict__ Kt, int64_t ldk, double* __restrict__ out,
                                const int64_t* __restrict__ pos, int64_t m, int64_t n) {
     const int64_t total = n * m;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = x / m;
         const int64_t g = x - j * m;
-        out[x] = Kt[g + pos[j] * m];
+        out[x] = Kt[g + pos[j] * ldk];
     }
 }
 
@@ -425,20 +347,29 @@ inline int grid_for(int64_t work, int block) {
 
 namespace {
 
+struct Second {
+    const double* B2;
+    int64_t n1;
+    double* C2;
+};
+
 template <bool TA, bool TB>
 void dgemm_go(dim3 grid, hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha,
               const double* A, int64_t lda, const double* B, int64_t ldb, double beta, double* C,
-              int64_t ldc, int64_t kc) {
+              int64_t ldc, int64_t kc, Second t) {
     hipLaunchKernelGGL((dgemm_mfma<TA, TB>), grid, 256, 0, s, M, N, K, alpha, A, lda, B, ldb,
-                       beta, C, ldc, kc);
+                       beta, C, ldc, kc, t.B2, t.n1, t.C2);
 }
 
 }  // namespace
 
 hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha,
                         const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
-                        double* C, int64_t ldc, hipStream_t s, double* work, size_t work_elems) {
+                        double* C, int64_t ldc, hipStream_t s, double* work, size_t work_elems,
+                        const double* B2, int64_t n1, double* C2) {
     if (M <= 0 || N <= 0) return hipSuccess;
+    if (n1 < 0 || n1 > N) n1 = N;
+    if (n1 < N && (!B2 || !C2)) return hipErrorInvalidValue;
     const int64_t gm = (M + kTile - 1) / kTile, gn = (N + kTile - 1) / kTile;
     if (gm > 0x7fffffff || gn > 65535) return hipErrorInvalidValue;
     // few output tiles and a deep reduction (the E x E products of the analysis, K = gauges):
@@ -454,14 +385,16 @@ hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, doubl
     double* out = splits > 1 ? work : C;
     const double a = splits > 1 ? 1.0 : alpha, b = splits > 1 ? 0.0 : beta;
     const int64_t ld = splits > 1 ? M : ldc;
-    if (!ta && !tb) dgemm_go<false, false>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
-    else if (!ta && tb) dgemm_go<false, true>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
-    else if (ta && !tb) dgemm_go<true, false>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
-    else dgemm_go<true, true>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc);
+    // split-K slices are contiguous M x N panels: the second part stays in them until the reduce
+    const Second t = splits > 1 ? Second{B2, n1, work + n1 * M} : Second{B2, n1, C2};
+    if (!ta && !tb) dgemm_go<false, false>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc, t);
+    else if (!ta && tb) dgemm_go<false, true>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc, t);
+    else if (ta && !tb) dgemm_go<true, false>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc, t);
+    else dgemm_go<true, true>(grid, s, M, N, K, a, A, lda, B, ldb, b, out, ld, kc, t);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || splits == 1) return e;
     hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), 256, 0, s, work,
-                       splits, M, N, alpha, beta, C, ldc);
+                       splits, M, N, alpha, beta, C, ldc, n1, C2);
     return hipGetLastError();
 }
 
@@ -472,41 +405,23 @@ hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64
     return hipGetLastError();
 }
 
-hipError_t launch_spd_solve_small(const double* M, double* V, int64_t k, int32_t* info,
-                                  hipStream_t s) {
-    if (k < 1 || k > kSpdMax) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(spd_solve_small, 1, 256, 0, s, M, V, (int)k, info);
-    return hipGetLastError();
-}
-
-hipError_t launch_zero_if_failed(double* X, int64_t cnt, const int32_t* info, hipStream_t s) {
-    if (cnt > 0)
-        hipLaunchKernelGGL(zero_if_failed, grid_for(cnt, 256), 256, 0, s, X, cnt, info);
-    return hipGetLastError();
-}
-
-hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s) {
-    if (k > 0) hipLaunchKernelGGL(set_identity, grid_for(k * k, 256), 256, 0, s, M, k);
-    return hipGetLastError();
-}
-
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s) {
     hipLaunchKernelGGL(mean_anomalies, grid_for(ns, 256), 256, 0, s, X, A, ns, E);
     return hipGetLastError();
 }
 
-hipError_t launch_anomaly_increments(const double* X, const double* Z, double* G, int64_t S,
-                                     int64_t Et, hipStream_t s) {
+hipError_t launch_anomaly_increments(const double* X, const double* Z, int64_t ldz, double* G,
+                                     int64_t S, int64_t Et, hipStream_t s) {
     if (S <= 0) return hipSuccess;
     if (Et < 2 || Et > kFusedIncrementsMax) return hipErrorInvalidValue;
     const unsigned g = (unsigned)((S + 255) / 256);
     if (Et <= 16)
-        hipLaunchKernelGGL(anomaly_increments<16>, g, 256, 0, s, X, Z, G, S, (int)Et);
+        hipLaunchKernelGGL(anomaly_increments<16>, g, 256, 0, s, X, Z, ldz, G, S, (int)Et);
     else if (Et <= 32)
-        hipLaunchKernelGGL(anomaly_increments<32>, g, 256, 0, s, X, Z, G, S, (int)Et);
+        hipLaunchKernelGGL(anomaly_increments<32>, g, 256, 0, s, X, Z, ldz, G, S, (int)Et);
     else
-        hipLaunchKernelGGL(anomaly_increments<64>, g, 256, 0, s, X, Z, G, S, (int)Et);
+        hipLaunchKernelGGL(anomaly_increments<64>, g, 256, 0, s, X, Z, ldz, G, S, (int)Et);
     return hipGetLastError();
 }
 
@@ -551,10 +466,10 @@ hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i, const 
     return hipGetLastError();
 }
 
-hipError_t launch_gain_to_caller(const double* Kt, double* out, const int64_t* pos, int64_t m,
-                                 int64_t n, hipStream_t s) {
+hipError_t launch_gain_to_caller(const double* Kt, int64_t ldk, double* out, const int64_t* pos,
+                                 int64_t m, int64_t n, hipStream_t s) {
     if (n <= 0 || m <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gain_to_caller, grid_for(n * m, 256), 256, 0, s, Kt, out, pos, m, n);
+    hipLaunchKernelGGL(gain_to_caller, grid_for(n * m, 256), 256, 0, s, Kt, ldk, out, pos, m, n);
     return hipGetLastError();
 }
 

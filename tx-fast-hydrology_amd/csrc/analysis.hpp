@@ -10,31 +10,49 @@ namespace mcr {
 
 // C = alpha op(A) op(B) + beta C  (op = transpose when ta / tb; op(A) M x K, op(B) K x N)
 // work (optional, work_elems doubles): lets a GEMM with few output tiles and a deep K split K
-// over workgroups (partial products in work, reduced in slice order: deterministic)
+// over workgroups (partial products in work, reduced in slice order: deterministic).
+// Two-part operands (optional): columns j >= n1 of op(B) come from B2 (column j - n1, same
+// leading dimension) and land in C2 (column j - n1, leading dimension ldc): one launch for
+// [C | C2] = op(A) [op(B) | op(B2)].
 hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha,
                         const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                         double* C, int64_t ldc, hipStream_t s, double* work = nullptr,
-                        size_t work_elems = 0);
+                        size_t work_elems = 0, const double* B2 = nullptr, int64_t n1 = -1,
+                        double* C2 = nullptr);
+
+// ---- dense.hip: hand-written f64 MFMA kernels of the large-ensemble analysis -------------
+// G = (X - mean_e X) Z: member-major slice X [Et][S], Z (Et x Et, leading dimension ldz),
+// G [Et][S]; 128 x 128 MFMA tiles, member mean as a rank-1 epilogue correction
+hipError_t launch_slice_increments(const double* X, const double* Z, int64_t ldz, double* G,
+                                   int64_t S, int64_t Et, hipStream_t s);
+// SPD systems through a block LDL^T with 32 x 32 blocks on a padded copy (kp = spd_padded(k)):
+//   launch_pad_matrix: dst (kp x ncols, ld kp) = src where i < rows and j < cols, `diag` on the
+//     other diagonal entries, 0 elsewhere (the padded SPD matrix: diag 1; right-hand sides: 0)
+//   launch_spd_factor: P (kp x kp, overwritten) = Lt D Lt^T; Lt / LtT (kp x kp) the unit block
+//     lower factor and its transpose (strictly lower blocks written), Sd (kp / 32 blocks of
+//     32 x 32) the inverses of the D blocks; info = 0, or the 1-based index of the first
+//     non-positive pivot.  One launch per block column.
+//   launch_spd_solve: B (kp x nrhs, ld kp, padding rows 0) := P^-1 B; U scratch of B's shape;
+//     B = 0 when the factorisation failed.
+int64_t spd_padded(int64_t k);
+hipError_t launch_pad_matrix(const double* src, int64_t rows, int64_t cols, int64_t lds,
+                             double* dst, int64_t kp, double diag, int64_t ncols, hipStream_t s);
+hipError_t launch_spd_factor(double* P, int64_t kp, double* Lt, double* LtT, double* Sd,
+                             int32_t* info, hipStream_t s);
+hipError_t launch_spd_solve(const double* Lt, const double* LtT, const double* Sd, int64_t kp,
+                            double* B, int64_t nrhs, double* U, const int32_t* info,
+                            hipStream_t s);
 // ensemble mean over members and anomalies A = X - mean (both [E][ns])
 // U = R^-1 HA for a diagonal R (r = its diagonal), column-major m x E
 hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64_t m, int64_t E,
                              hipStream_t s);
-// M = I (k x k)
-hipError_t launch_set_identity(double* M, int64_t k, hipStream_t s);
-// V := M^-1 V for SPD M (k x k, column-major, k <= 64) in one workgroup; info = 0, or j + 1 when
-// the j-th leading minor is not positive definite (V then zeroed)
-hipError_t launch_spd_solve_small(const double* M, double* V, int64_t k, int32_t* info,
-                                  hipStream_t s);
-constexpr int64_t kSpdSolveMax = 64;
-// X[0 .. cnt) := 0 when *info != 0 (device-side gate after a rocSOLVER potrf / potrs pair)
-hipError_t launch_zero_if_failed(double* X, int64_t cnt, const int32_t* info, hipStream_t s);
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s);
 // G = (X - mean) Z for a member-major slice X [Et][S] and Z (Et x Et, column-major): the
 // increments of the slice in one pass (Et <= kFusedIncrementsMax)
 constexpr int64_t kFusedIncrementsMax = 64;
-hipError_t launch_anomaly_increments(const double* X, const double* Z, double* G, int64_t S,
-                                     int64_t Et, hipStream_t s);
+hipError_t launch_anomaly_increments(const double* X, const double* Z, int64_t ldz, double* G,
+                                     int64_t S, int64_t Et, hipStream_t s);
 // HA (m x E) = A at the gauge slots; D (m x E) = Y[g][e] - X at the gauge slots (D may be NULL)
 hipError_t launch_gauge_gather(const double* A, const double* X, const int64_t* gslot,
                                const double* Y, double* HA, double* D, int64_t m, int64_t ns,
@@ -53,8 +71,8 @@ hipError_t launch_unpack_slices(const double* in, double* G, int64_t ns, int64_t
 hipError_t launch_apply_gain(const double* G, double* st_o, double* st_i, const uint8_t* flags,
                              const int32_t* up_off, const int32_t* up, int64_t ns, int64_t E,
                              hipStream_t s);
-// Kt (m x nslots, column-major) -> K_out[j][g] in caller reach order
-hipError_t launch_gain_to_caller(const double* Kt, double* out, const int64_t* pos, int64_t m,
-                                 int64_t n, hipStream_t s);
+// Kt (m x nslots, column-major, leading dimension ldk) -> K_out[j][g] in caller reach order
+hipError_t launch_gain_to_caller(const double* Kt, int64_t ldk, double* out, const int64_t* pos,
+                                 int64_t m, int64_t n, hipStream_t s);
 
 }  // namespace mcr

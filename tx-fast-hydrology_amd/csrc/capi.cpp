@@ -14,9 +14,6 @@
 #include <string>
 #include <vector>
 
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
-
 #include "analysis.hpp"
 #include "capi_common.hpp"
 #include "kernels.hpp"
@@ -138,11 +135,13 @@ struct Net {
     int64_t E = 1;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
-    DBuf<double> An, HA, Dn, C2, Zn, Gn, Yb, HXb, Db, Rd, Ub, Mb, Wk;   // Wk: split-K slices
+    DBuf<double> An, HA, Zn, Gn, Yb, HXb, Db, Rd, Rb, Ub, EE, Wk;   // Wk: split-K slices
+    // SPD solves (dense.hip block LDL^T): padded matrix, unit block factor and its transpose,
+    // inverted diagonal blocks, solve scratch, padded right-hand sides
+    DBuf<double> Pf, Lt, LtT, Sd, Ubuf, Rhs;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
-    rocblas_handle blas = nullptr;
-    int32_t* info_host = nullptr;      // pinned copy of the Cholesky status, checked at sync()
+    int32_t* info_host = nullptr;      // pinned copy of the factorisation status, read at sync()
     bool info_pending = false;
 
     // pinned staging ring for asynchronous host -> device uploads (no stream sync per call)
@@ -176,6 +175,7 @@ struct Net {
     std::vector<int4> stab_host;     // step table last uploaded to stab
     int force_mode = -1;             // >= 0: mode override during a re-run
     int64_t patience = mcr::kFlowPatience;   // dataflow waits (mc_set_flow_patience)
+    int64_t reroutes = 0;            // horizons re-routed after a give-up (mc_net_reroutes)
 
     // outputs of the last run are the {o, i} pairs of a member-dataflow step (Qm + nslots * E)
     bool out_io = false;
@@ -188,7 +188,6 @@ struct Net {
 
     ~Net() {
         if (status_host) (void)hipHostFree(status_host);
-        if (blas) (void)rocblas_destroy_handle(blas);
         if (info_host) (void)hipHostFree(info_host);
         for (PinSlot& ps : pins) {
             if (ps.ev) (void)hipEventSynchronize(ps.ev);
@@ -312,6 +311,7 @@ struct Net {
                     st_o.swap(st_o2);
                     st_i.swap(st_i2);
                     last_flow.valid = false;
+                    ++reroutes;
                     std::fprintf(stderr, "[mcroute] dataflow launch gave up waiting for upstream "
                                          "workgroups; the horizon was re-routed with launches\n");
                     force_mode = 1;
@@ -427,32 +427,32 @@ struct Net {
         return true;
     }
 
-    rocblas_handle solver() {
-        if (!blas && rocblas_create_handle(&blas) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocblas_create_handle failed");
-        if (rocblas_set_stream(blas, stream) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocblas_set_stream failed");
-        return blas;
+    // P (kp x kp, padded SPD) = Lt D Lt^T, the status in `info` (device); kp = spd_padded(k)
+    void spd_factor(double* P, int64_t kp) {
+        Lt.reserve((size_t)(kp * kp));
+        LtT.reserve((size_t)(kp * kp));
+        Sd.reserve((size_t)(kp * 32));
+        info.reserve(1);
+        HIPC(mcr::launch_spd_factor(P, kp, Lt.p, LtT.p, Sd.p, info.p, stream));
+    }
+    // B (kp x nrhs, leading dimension kp, padding rows 0) := P^-1 B; B = 0 if the factorisation
+    // failed
+    void spd_solve(int64_t kp, double* B, int64_t nrhs) {
+        Ubuf.reserve((size_t)(kp * std::max<int64_t>(nrhs, 1)));
+        HIPC(mcr::launch_spd_solve(Lt.p, LtT.p, Sd.p, kp, B, nrhs, Ubuf.p, info.p, stream));
+    }
+    // the factorisation status, read back asynchronously and reported at the next sync()
+    void info_async() {
+        if (!info_host)
+            HIPC(hipHostMalloc(reinterpret_cast<void**>(&info_host), sizeof(int32_t),
+                               hipHostMallocDefault));
+        HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        info_pending = true;
     }
 
-    // B := (L L^T)^-1 B for the lower Cholesky factor L (k x k) of a potrf, B k x nrhs (both
-    // column-major, leading dimension k): two rocBLAS triangular solves.  rocSOLVER's potrs ran
-    // its substitution kernels for 440 us at k = nrhs = 256 (EnKF256, every analysis).
-    void chol_solve(const double* L, int64_t k, double* B, int64_t nrhs) {
-        const double one = 1.0;
-        rocblas_handle hb = solver();
-        if (rocblas_dtrsm(hb, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none,
-                          rocblas_diagonal_non_unit, (rocblas_int)k, (rocblas_int)nrhs, &one, L,
-                          (rocblas_int)k, B, (rocblas_int)k) != rocblas_status_success ||
-            rocblas_dtrsm(hb, rocblas_side_left, rocblas_fill_lower, rocblas_operation_transpose,
-                          rocblas_diagonal_non_unit, (rocblas_int)k, (rocblas_int)nrhs, &one, L,
-                          (rocblas_int)k, B, (rocblas_int)k) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocblas_dtrsm failed");
-    }
-
-    // C2 = HA HA^T / (E-1) + R factored (Cholesky, lower) from the current member state;
-    // anomalies in An, gauge anomalies in HA, innovations Y - HX in Dn (when y != NULL)
-    void analysis_setup(int64_t m, const int64_t* gauges, const double* y, const double* R) {
+    // C = HA HA^T / (E-1) + R (m x m) factored from the current member state (padded to
+    // mp = spd_padded(m) in Pf); anomalies in An, gauge anomalies in HA
+    void analysis_setup(int64_t m, const int64_t* gauges, const double* R) {
         REQUIRE(E >= 2, "the ensemble analysis needs at least 2 members");
         REQUIRE(m >= 1 && m < (1ll << 31) && gauges && R, "bad gauge arguments");
         settle_state();
@@ -465,19 +465,17 @@ struct Net {
         gslot.upload(gs.data(), gs.size(), stream);
         An.reserve((size_t)(ns * E));
         HA.reserve((size_t)(m * E));
-        Dn.reserve((size_t)(m * E));
-        C2.upload(R, (size_t)(m * m), stream);   // symmetric: row-major == column-major
-        if (y) Yb.upload(y, (size_t)(m * E), stream);
+        Rb.upload(R, (size_t)(m * m), stream);     // symmetric: row-major == column-major
         HIPC(mcr::launch_mean_anomalies(st_o.p, An.p, ns, E, stream));
-        HIPC(mcr::launch_gauge_gather(An.p, st_o.p, gslot.p, y ? Yb.p : nullptr, HA.p,
-                                      y ? Dn.p : nullptr, m, ns, E, stream));
+        HIPC(mcr::launch_gauge_gather(An.p, st_o.p, gslot.p, nullptr, HA.p, nullptr, m, ns, E,
+                                      stream));
         const double inv = 1.0 / (double)(E - 1);
-        HIPC(mcr::launch_dgemm(false, true, m, m, E, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
+        const int64_t mp = mcr::spd_padded(m);
+        Pf.reserve((size_t)(mp * mp));
+        HIPC(mcr::launch_pad_matrix(Rb.p, m, m, m, Pf.p, mp, 1.0, mp, stream));
+        HIPC(mcr::launch_dgemm(false, true, m, m, E, inv, HA.p, m, HA.p, m, 1.0, Pf.p, mp,
                                stream));
-        info.reserve(1);
-        if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p, (rocblas_int)m,
-                             info.p) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
+        spd_factor(Pf.p, mp);
         int32_t ih = 0;
         HIPC(hipMemcpyAsync(&ih, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         sync();
@@ -528,86 +526,58 @@ struct Net {
         // gauge anomalies HA = HX - mean over members
         HA.reserve((size_t)(m * Et));
         HIPC(mcr::launch_mean_anomalies(HXall, HA.p, m, Et, stream));
-        if (!info_host)
-            HIPC(hipHostMalloc(reinterpret_cast<void**>(&info_host), sizeof(int32_t),
-                               hipHostMallocDefault));
-        info.reserve(1);
-        Zn.reserve((size_t)(Et * Et));
+        const double* Z = nullptr;
+        int64_t ldz = Et;
         std::vector<double> rd;
         if (Et <= m && diagonal_R(R, m, rd)) {
             // ensemble space (diagonal R): with S = HA / sqrt(Et-1),
             //   S^T (S S^T + R)^-1 D = (I + S^T R^-1 S)^-1 S^T R^-1 D   (push-through identity)
             // so Z = HA^T C^-1 D / (Et-1) = M^-1 V with M = I + HA^T R^-1 HA / (Et-1) (Et x Et,
             // SPD, eigenvalues >= 1) and V = (R^-1 HA)^T D / (Et-1): an Et x Et solve instead
-            // of m x m
+            // of m x m.  [M | V] = [I | 0] + U^T [HA | D] / (Et-1) (U = R^-1 HA) is ONE split-K
+            // MFMA launch into the padded system buffer EE = [M (kp x kp) | V (kp x Et)]
             upload_async(Rd, rd.data(), rd.size());
             Ub.reserve((size_t)(m * Et));
             HIPC(mcr::launch_scale_rows(HA.p, Rd.p, Ub.p, m, Et, stream));
-            Mb.reserve((size_t)(Et * Et));
-            HIPC(mcr::launch_set_identity(Mb.p, Et, stream));
-            Wk.reserve((size_t)(64 * Et * Et));
-            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Ub.p, m, 1.0, Mb.p, Et,
-                                   stream, Wk.p, Wk.cap));
-            if (Et <= mcr::kSpdSolveMax) {
-                // factor + both solves in one workgroup (analysis.hip spd_solve_small)
-                HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p,
-                                       Et, stream, Wk.p, Wk.cap));
-                HIPC(mcr::launch_spd_solve_small(Mb.p, Zn.p, Et, info.p, stream));
-                HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                    stream));
-                info_pending = true;
-            } else {
-                if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)Et, Mb.p,
-                                     (rocblas_int)Et, info.p) != rocblas_status_success)
-                    throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
-                HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                    stream));
-                info_pending = true;
-                HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, Ub.p, m, Dall, m, 0.0, Zn.p,
-                                       Et, stream, Wk.p, Wk.cap));
-                chol_solve(Mb.p, Et, Zn.p, Et);
-                // a failed factorisation leaves garbage in Zn: zero update instead
-                HIPC(mcr::launch_zero_if_failed(Zn.p, Et * Et, info.p, stream));
-            }
+            const int64_t kp = mcr::spd_padded(Et);
+            EE.reserve((size_t)(kp * (kp + Et)));
+            HIPC(mcr::launch_pad_matrix(nullptr, 0, 0, 0, EE.p, kp, 1.0, kp + Et, stream));
+            Wk.reserve((size_t)(64 * Et * 2 * Et));
+            double* V = EE.p + kp * kp;
+            HIPC(mcr::launch_dgemm(true, false, Et, 2 * Et, m, inv, Ub.p, m, HA.p, m, 1.0, EE.p,
+                                   kp, stream, Wk.p, Wk.cap, Dall, Et, V));
+            spd_factor(EE.p, kp);
+            spd_solve(kp, V, Et);
+            info_async();
+            Z = V;
+            ldz = kp;
         } else {
             // observation space: C = HA HA^T / (Et-1) + R (m x m), W = C^-1 D,
             // Z = HA^T W / (Et-1)
-            upload_async(C2, R, (size_t)(m * m));      // symmetric: row-major == column-major
-            HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, C2.p, m,
+            const int64_t mp = mcr::spd_padded(m);
+            upload_async(Rb, R, (size_t)(m * m));      // symmetric: row-major == column-major
+            Pf.reserve((size_t)(mp * mp));
+            HIPC(mcr::launch_pad_matrix(Rb.p, m, m, m, Pf.p, mp, 1.0, mp, stream));
+            HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, Pf.p, mp,
                                    stream));
-            if (rocsolver_dpotrf(solver(), rocblas_fill_lower, (rocblas_int)m, C2.p,
-                                 (rocblas_int)m, info.p) != rocblas_status_success)
-                throw Fail(MC_E_HIP, "rocsolver_dpotrf failed");
-            // status checked at the next sync (a failed factorisation leaves the update unusable)
-            HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                stream));
-            info_pending = true;
-            Dn.reserve((size_t)(m * Et));
-            HIPC(hipMemcpyAsync(Dn.p, Dall, (size_t)(m * Et) * sizeof(double),
-                                hipMemcpyDeviceToDevice, stream));
-            chol_solve(C2.p, m, Dn.p, Et);
+            spd_factor(Pf.p, mp);
+            info_async();
+            Rhs.reserve((size_t)(mp * Et));
+            HIPC(mcr::launch_pad_matrix(Dall, m, Et, m, Rhs.p, mp, 0.0, Et, stream));
+            spd_solve(mp, Rhs.p, Et);
+            Zn.reserve((size_t)(Et * Et));
             Wk.reserve((size_t)(64 * Et * Et));
-            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Dn.p, m, 0.0, Zn.p, Et,
+            HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Rhs.p, mp, 0.0, Zn.p, Et,
                                    stream, Wk.p, Wk.cap));
-            HIPC(mcr::launch_zero_if_failed(Zn.p, Et * Et, info.p, stream));
+            Z = Zn.p;
+            ldz = Et;
         }
-        // slice anomalies and increments G = A Z  (= K D per member): one fused pass for the
-        // per-GPU ensemble sizes; beyond, the anomalies and a plain (S x Et) x (Et x Et) rocBLAS
-        // GEMM (EnKF256: 0.49 ms per analysis against 0.72 for analysis.hip's MFMA tile, whose
-        // LDS padding / K-slice / XCD-order / fused-centring variants were no faster)
-        if (Et <= mcr::kFusedIncrementsMax) {
-            HIPC(mcr::launch_anomaly_increments(Xs, Zn.p, Gs, S, Et, stream));
-        } else {
-            An.reserve((size_t)(S * Et));
-            HIPC(mcr::launch_mean_anomalies(Xs, An.p, S, Et, stream));
-            const double one = 1.0, zero = 0.0;
-            if (S > (1ll << 31) ||
-                rocblas_dgemm(solver(), rocblas_operation_none, rocblas_operation_none,
-                              (rocblas_int)S, (rocblas_int)Et, (rocblas_int)Et, &one, An.p,
-                              (rocblas_int)S, Zn.p, (rocblas_int)Et, &zero, Gs,
-                              (rocblas_int)S) != rocblas_status_success)
-                throw Fail(MC_E_HIP, "rocblas_dgemm failed");
-        }
+        // slice increments G = A Z (= K D per member): one fused pass for the per-GPU ensemble
+        // sizes, the 128 x 128 MFMA tile with the member mean folded in beyond (dense.hip)
+        if (Et <= mcr::kFusedIncrementsMax)
+            HIPC(mcr::launch_anomaly_increments(Xs, Z, ldz, Gs, S, Et, stream));
+        else
+            HIPC(mcr::launch_slice_increments(Xs, Z, ldz, Gs, S, Et, stream));
     }
 
     // increments of the local members from every rank's slice (Grecv [N][E][S]) -> _apply_gain
@@ -642,15 +612,16 @@ struct Net {
         REQUIRE(K_out, "K_out must not be NULL");
         if (plan.n == 0) return;
         REQUIRE(plan.nslots < (1ll << 31), "network too large for the explicit gain");
-        analysis_setup(m, gauges, nullptr, R);
-        const int64_t ns = plan.nslots;
+        analysis_setup(m, gauges, R);
+        const int64_t ns = plan.nslots, mp = mcr::spd_padded(m);
         const double inv = 1.0 / (double)(E - 1);
-        Gn.reserve((size_t)(m * ns));               // K^T (m x ns), solved in place
-        HIPC(mcr::launch_dgemm(false, true, m, ns, E, inv, HA.p, m, An.p, ns, 0.0, Gn.p, m,
+        Gn.reserve((size_t)(mp * ns));              // K^T (mp x ns, padding rows 0), solved in place
+        HIPC(hipMemsetAsync(Gn.p, 0, (size_t)(mp * ns) * sizeof(double), stream));
+        HIPC(mcr::launch_dgemm(false, true, m, ns, E, inv, HA.p, m, An.p, ns, 0.0, Gn.p, mp,
                                stream));
-        chol_solve(C2.p, m, Gn.p, ns);
+        spd_solve(mp, Gn.p, ns);
         outT.reserve((size_t)(plan.n * m));
-        HIPC(mcr::launch_gain_to_caller(Gn.p, outT.p, pos.p, m, plan.n, stream));
+        HIPC(mcr::launch_gain_to_caller(Gn.p, mp, outT.p, pos.p, m, plan.n, stream));
         HIPC(hipMemcpyAsync(K_out, outT.p, (size_t)(plan.n * m) * sizeof(double),
                             hipMemcpyDeviceToHost, stream));
         sync();
@@ -1269,6 +1240,46 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         }
         HIPC(hipEventRecord(ev, D->stream));
         HIPC(hipStreamWaitEvent(S->stream, ev, 0));
+    });
+}
+
+int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_net,
+                              int64_t src_reach, double o_start, double alpha, double beta,
+                              double gamma) {
+    return guarded([&] {
+        Net* D = as_net(dst_net);
+        Net* S = as_net(const_cast<void*>(src_net));
+        REQUIRE(D != S, "source and destination must be different sessions");
+        REQUIRE(D->E == 1 && S->E == 1, "lateral corrections route single-member sessions");
+        REQUIRE(0 <= dst_reach && dst_reach < D->plan.n && 0 <= src_reach && src_reach < S->plan.n,
+                "reach index out of range");
+        REQUIRE(S->T_out > 0 && S->cur && !S->out_io, "the source session has no horizon outputs");
+        REQUIRE(D->n_rows == S->T_out,
+                "the destination's forcing rows must be the source horizon's steps (one input "
+                "row per step, as the reference's positional add requires)");
+        D->settle_state();
+        // order: after the source's run, on the destination's stream; the source waits for the
+        // read before it may overwrite its outputs (no host synchronisation)
+        hipEvent_t ev;
+        HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        struct EvGuard {
+            hipEvent_t e;
+            ~EvGuard() { (void)hipEventDestroy(e); }
+        } guard{ev};
+        HIPC(hipEventRecord(ev, S->stream));
+        HIPC(hipStreamWaitEvent(D->stream, ev, 0));
+        HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, S->row_width(),
+                                            o_start, alpha, beta, gamma, D->F.p, D->plan.nslots,
+                                            D->plan.pos[dst_reach], S->T_out, D->stream));
+        HIPC(hipEventRecord(ev, D->stream));
+        HIPC(hipStreamWaitEvent(S->stream, ev, 0));
+    });
+}
+
+int mc_net_reroutes(const void* net, int64_t* count) {
+    return guarded([&] {
+        REQUIRE(net && count, "null argument");
+        *count = static_cast<const Net*>(net)->reroutes;
     });
 }
 

@@ -1,0 +1,491 @@
+// Dense f64 linear algebra of the ensemble analysis on CDNA4 (gfx950), hand-written on
+// v_mfma_f64_16x16x4f64 (da.py:119-122 K = P H^T (H P H^T + R)^-1 in its
+// ensemble-space form):
+//
+//  * slice_increments: G = (X - mean_e X) Z for a member-major reach slice X [Et][S] and the
+//    Et x Et analysis weights Z -- the largest product of the analysis (S x Et x Et,
+//    2 S Et^2 flops).  128 x 128 output tiles, 4 waves of 64 x 64, K slices double-buffered in
+//    LDS, the member mean folded in as a rank-1 epilogue correction (G = X Z - xbar zs^T) so
+//    X is read once and no anomaly array is materialised.
+//  * block LDL^T of an SPD k x k matrix (32 x 32 blocks): A = Lt D Lt^T with Lt unit block lower
+//    triangular and D = blockdiag(D_J); every D_J is inverted (S_J = D_J^-1) by a Cholesky of
+//    the 32 x 32 block, which also detects a matrix that is not positive definite.  One launch
+//    per block column (the step kernel recomputes Lt_IJ = A_IJ S_J in every workgroup that
+//    needs it, and the workgroup of the next diagonal block inverts it right after its update).
+//  * the solve B := A^-1 B: W = Lt^-1 B (unit block lower), U_I = S_I W_I, Z = Lt^-T U, one
+//    workgroup per 16 right-hand sides, the block sums on MFMA.
+// Matrices are column-major; the factorisation works on a copy padded to kp = 32 * ceil(k / 32)
+// with an identity block (pad_square), so every block is full.
+#include "analysis.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+namespace mcr {
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// =============================================================================================
+// slice increments  G[e][d] = sum_f (X[f][d] - xbar[d]) Z[f][e]
+// MFMA rows = members e (A operand = Z^T), columns = slots d (B operand = X), k = member f.
+constexpr int kGM = 128;          // members per tile
+constexpr int kGN = 128;          // slots per tile
+constexpr int kGK = 16;           // K slice
+constexpr int kGStage = kGK * (kGM + kGN);   // doubles per LDS stage
+
+__global__ __launch_bounds__(256, 2) void slice_increments(const double* __restrict__ X,
+                                                           const double* __restrict__ Z,
+                                                           int64_t ldz,
+                                                           double* __restrict__ G, int64_t S,
+                                                           int Et, int n_slot_tiles,
+                                                           int n_member_tiles) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    // XCD-aware tile order: the member tiles of one slot tile share its X rows; consecutive
+    // workgroups go to consecutive XCDs, so blocks b, b + 8, ... (same XCD) take them
+    const int b = blockIdx.x;
+    const int xcd = b & 7;
+    const int rest = b >> 3;
+    const int mt = rest % n_member_tiles;
+    const int st = (rest / n_member_tiles) * 8 + xcd;
+    if (st >= n_slot_tiles) return;
+    const int64_t d0 = (int64_t)st * kGN;
+    const int e0 = mt * kGM;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+
+    // global -> register staging of one K slice: Z^T (128 members x 16 f) and X (16 f x 128 d)
+    // Z: thread -> member e = tid >> 1, f pairs (tid & 1) * 8 + 2 p (p < 4)
+    // X: thread -> f = (tid >> 6) + 4 p, slot pair 2 (tid & 63)
+    const int ze = tid >> 1, zf = (tid & 1) * 8;
+    const int xf = tid >> 6, xd = 2 * (tid & 63);
+    const bool zrow = e0 + ze < Et;
+    const int64_t gd = d0 + xd;
+    double rz[8], rx[8];
+    double zsum = 0.0, xs0 = 0.0, xs1 = 0.0;     // partial sums for zs[e] and the mean of X
+    auto load = [&](int f0) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int f = f0 + zf + p;
+            rz[p] = (zrow && f < Et) ? Z[f + (int64_t)(e0 + ze) * ldz] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int f = f0 + xf + 4 * p;
+            const double* src = X + (int64_t)f * S + gd;
+            const bool okf = f < Et;
+            rx[2 * p] = (okf && gd < S) ? src[0] : 0.0;
+            rx[2 * p + 1] = (okf && gd + 1 < S) ? src[1] : 0.0;
+        }
+    };
+    auto stage = [&](int buf) {
+        double* As = sm + buf * kGStage;          // As[f][e]
+        double* Bs = As + kGK * kGM;              // Bs[f][d]
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            As[(zf + p) * kGM + ze] = rz[p];
+            zsum += rz[p];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int f = xf + 4 * p;
+            *reinterpret_cast<double2*>(Bs + f * kGN + xd) = make_double2(rx[2 * p], rx[2 * p + 1]);
+            xs0 += rx[2 * p];
+            xs1 += rx[2 * p + 1];
+        }
+    };
+
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+    load(0);
+    stage(0);
+    __syncthreads();
+    int buf = 0;
+    for (int f0 = 0; f0 < Et; f0 += kGK) {
+        const bool more = f0 + kGK < Et;
+        if (more) load(f0 + kGK);                 // next slice in flight during the MFMAs
+        const double* As = sm + buf * kGStage;
+        const double* Bs = As + kGK * kGM;
+#pragma unroll
+        for (int kk = 0; kk < kGK; kk += 4) {
+            const int k = kk + (lane >> 4);
+            double a[4], bb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[k * kGM + wr + 16 * i + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bb[j] = Bs[k * kGN + wc + 16 * j + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(a[i], bb[j], acc[i][j]);
+        }
+        if (more) stage(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    // member sums of X (4 partials per slot pair) and column sums of Z (2 partials per member)
+    double* red = sm;                              // the K loop is over: reuse stage 0
+    red[xf * kGN + xd] = xs0;
+    red[xf * kGN + xd + 1] = xs1;
+    const double zs_all = zsum + __shfl_xor(zsum, 1);
+    if ((tid & 1) == 0) red[4 * kGN + ze] = zs_all;
+    __syncthreads();
+    const double inv = 1.0 / (double)Et;
+    // C/D of f64 16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int dl = wc + 16 * j + (lane & 15);
+        const double xbar = (((red[dl] + red[kGN + dl]) + red[2 * kGN + dl]) + red[3 * kGN + dl]) * inv;
+        const int64_t d = d0 + dl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int el = wr + 16 * i + (lane >> 4) + 4 * r;
+                const int e = e0 + el;
+                if (e < Et && d < S) G[(int64_t)e * S + d] = acc[i][j][r] - red[4 * kGN + el] * xbar;
+            }
+    }
+}
+
+// =============================================================================================
+// block LDL^T (32 x 32 blocks) and its solve
+constexpr int kB = 32;
+constexpr int kL = kB + 1;        // LDS row stride of a block (conflict-free column reads)
+
+// One 16 x 16 output block per wave of a 32 x 32 x 32 product: wave w owns rows
+// 16 (w >> 1) .. and columns 16 (w & 1) ..; a(i, k), b(k, j) read the operands
+template <class FA, class FB>
+__device__ __forceinline__ f64x4 mma32(FA a, FB b, f64x4 acc, int wave, int lane) {
+    const int i = (wave >> 1) * 16 + (lane & 15);
+    const int j = (wave & 1) * 16 + (lane & 15);
+#pragma unroll
+    for (int kk = 0; kk < kB; kk += 4) {
+        const int k = kk + (lane >> 4);
+        acc = mfma4(a(i, k), b(k, j), acc);
+    }
+    return acc;
+}
+__device__ __forceinline__ int blk_row(int wave, int lane, int r) {
+    return (wave >> 1) * 16 + (lane >> 4) + 4 * r;
+}
+__device__ __forceinline__ int blk_col(int wave, int lane) {
+    return (wave & 1) * 16 + (lane & 15);
+}
+
+// S = A^-1 of the SPD 32 x 32 block in `a` (LDS, rows of stride kL, lower part used; it is
+// overwritten), by Gaussian elimination of [A | I] with symmetric pivots: the right part becomes
+// Lu^-1 (A = Lu D Lu^T, Lu unit lower), T = D^-1/2 Lu^-1 = L^-1 for the Cholesky factor L, and
+// S = T^T T.  t: LDS scratch.  Returns the 1-based index of the first non-positive pivot (0 =
+// positive definite); all 256 threads call it.
+__device__ int block_inverse(double* a, double* t, double* s) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int x = tid; x < kB * kB; x += 256) {
+        const int i = x / kB, c = x % kB;
+        t[i * kL + c] = i == c ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    int bad = 0;
+    for (int j = 0; j < kB; ++j) {
+        const double d = a[j * kL + j];
+        if (!(d > 0.0)) {          // same value in every thread: a uniform exit
+            bad = j + 1;
+            break;
+        }
+        const double invd = 1.0 / d;
+        for (int x = tid; x < (kB - 1 - j) * kB; x += 256) {
+            const int i = j + 1 + x / kB, c = x % kB;
+            const double m = a[i * kL + j] * invd;
+            if (c <= j) t[i * kL + c] = t[i * kL + c] - m * t[j * kL + c];
+            else if (c <= i) a[i * kL + c] = a[i * kL + c] - m * a[c * kL + j];
+        }
+        __syncthreads();
+    }
+    if (bad) return bad;
+    for (int x = tid; x < kB * kB; x += 256) {    // rows of Lu^-1 scaled by D^-1/2
+        const int i = x / kB, c = x % kB;
+        t[i * kL + c] = c <= i ? t[i * kL + c] / sqrt(a[i * kL + i]) : 0.0;
+    }
+    __syncthreads();
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = mma32([&](int i, int k) { return t[k * kL + i]; },
+                [&](int k, int j) { return t[k * kL + j]; }, acc, wave, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = acc[r];
+    __syncthreads();
+    return 0;
+}
+
+__device__ __forceinline__ void store_block(const double* src, double* dst, int64_t ld) {
+    // LDS block (row stride kL) -> column-major global block (leading dimension ld)
+    for (int x = threadIdx.x; x < kB * kB; x += 256) {
+        const int i = x % kB, c = x / kB;
+        dst[i + (int64_t)c * ld] = src[i * kL + c];
+    }
+}
+__device__ __forceinline__ void load_block(const double* src, int64_t ld, double* dst) {
+    for (int x = threadIdx.x; x < kB * kB; x += 256) {
+        const int i = x % kB, c = x / kB;
+        dst[i * kL + c] = src[i + (int64_t)c * ld];
+    }
+}
+
+// dst (kp x ncols, leading dimension kp) = src (rows x cols valid, leading dimension lds),
+// `diag` on the diagonal outside it and 0 elsewhere
+__global__ void pad_matrix(const double* __restrict__ src, int64_t rows, int64_t cols,
+                           int64_t lds, double* __restrict__ dst, int64_t kp, double diag,
+                           int64_t ncols) {
+    const int64_t total = kp * ncols;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = x % kp, j = x / kp;
+        dst[x] = (i < rows && j < cols) ? src[i + j * lds] : (i == j ? diag : 0.0);
+    }
+}
+
+// first diagonal block: S_0 = A_00^-1
+__global__ __launch_bounds__(256) void ldl_first(const double* __restrict__ P, int64_t kp,
+                                                 double* __restrict__ Sd,
+                                                 int32_t* __restrict__ info) {
+    __shared__ double a[kB * kL], t[kB * kL], s[kB * kL];
+    if (threadIdx.x == 0) *info = 0;
+    load_block(P, kp, a);
+    __syncthreads();
+    const int bad = block_inverse(a, t, s);
+    if (bad) {
+        if (threadIdx.x == 0) *info = bad;
+        return;
+    }
+    store_block(s, Sd, kB);
+}
+
+// Block column J: every workgroup owns one trailing block (I, C), J < C <= I:
+//   Lt_IJ = A_IJ S_J,  A_IC -= Lt_IJ A_CJ^T;
+// the workgroup (I, J + 1) stores Lt_IJ (and its transpose), the workgroup (J + 1, J + 1)
+// inverts its updated block into S_{J+1}.
+__global__ __launch_bounds__(256) void ldl_step(double* __restrict__ P, int64_t kp, int J,
+                                                int nbk, double* __restrict__ Lt,
+                                                double* __restrict__ LtT,
+                                                double* __restrict__ Sd,
+                                                int32_t* __restrict__ info) {
+    __shared__ double sS[kB * kL], sA[kB * kL], sC[kB * kL], sL[kB * kL];
+    if (*info != 0) return;                          // an earlier block was not SPD
+    // blockIdx -> (I, C): pairs enumerated column by column, C = J+1 .. nbk-1, I = C .. nbk-1
+    int rem = blockIdx.x, C = J + 1;
+    while (rem >= nbk - C) {
+        rem -= nbk - C;
+        ++C;
+    }
+    const int I = C + rem;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t ro = (int64_t)I * kB, co = (int64_t)C * kB, jo = (int64_t)J * kB;
+    load_block(Sd + (int64_t)J * kB * kB, kB, sS);
+    load_block(P + ro + jo * kp, kp, sA);
+    if (I != C) load_block(P + co + jo * kp, kp, sC);
+    f64x4 acc;                                       // A_IC in the MFMA layout
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        acc[r] = P[ro + blk_row(wave, lane, r) + (co + blk_col(wave, lane)) * kp];
+    __syncthreads();
+    f64x4 l = {0.0, 0.0, 0.0, 0.0};
+    l = mma32([&](int i, int k) { return sA[i * kL + k]; },
+              [&](int k, int j) { return sS[k * kL + j]; }, l, wave, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sL[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = l[r];
+    __syncthreads();
+    const double* cj = I != C ? sC : sA;
+    acc = mma32([&](int i, int k) { return -sL[i * kL + k]; },
+                [&](int k, int j) { return cj[j * kL + k]; }, acc, wave, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        P[ro + blk_row(wave, lane, r) + (co + blk_col(wave, lane)) * kp] = acc[r];
+    if (C == J + 1) {
+        store_block(sL, Lt + ro + jo * kp, kp);
+        for (int x = tid; x < kB * kB; x += 256) {    // LtT block (J, I) = Lt_IJ^T
+            const int i = x % kB, c = x / kB;
+            LtT[jo + i + (ro + c) * kp] = sL[c * kL + i];
+        }
+        if (I == C) {
+            // the next diagonal block: fully updated now; invert it (after every wave's update
+            // read of sA)
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sA[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = acc[r];
+            __syncthreads();
+            const int bad = block_inverse(sA, sC, sS);
+            if (bad) {
+                if (tid == 0) *info = (int32_t)(co + bad);
+                return;
+            }
+            store_block(sS, Sd + (int64_t)C * kB * kB, kB);
+        }
+    }
+}
+
+// B := A^-1 B for the factored A (kp x kp; B kp x nrhs, column-major, rows >= k zero), 16
+// right-hand sides per workgroup.  Wave (rb, kh): output rows 16 rb of a block row, block
+// sums over the k blocks of parity kh (the two halves are added through LDS).  U: scratch of
+// B's shape.  A factorisation that failed (*info != 0) gives B = 0.
+__global__ __launch_bounds__(256) void ldl_solve(const double* __restrict__ Lt,
+                                                 const double* __restrict__ LtT,
+                                                 const double* __restrict__ Sd, int64_t kp,
+                                                 int nbk, double* __restrict__ B, int64_t nrhs,
+                                                 double* __restrict__ U,
+                                                 const int32_t* __restrict__ info) {
+    __shared__ double red[2][16 * 17];
+    __shared__ double wI[kB * 17];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rb = wave & 1, kh = wave >> 1;
+    const int64_t c0 = (int64_t)blockIdx.x * 16;
+    const int64_t col = c0 + (lane & 15);
+    const bool colok = col < nrhs;
+    if (*info != 0) {
+        for (int64_t x = tid; x < kp * 16; x += 256) {
+            const int64_t c = c0 + x / kp;
+            if (c < nrhs) B[x % kp + c * kp] = 0.0;
+        }
+        return;
+    }
+    // ---- forward: W_I = B_I - sum_{J<I} Lt_IJ W_J ;  U_I = S_I W_I
+    for (int I = 0; I < nbk; ++I) {
+        const int64_t ro = (int64_t)I * kB + rb * 16;
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int J = kh; J < I; J += 2) {
+#pragma unroll
+            for (int kk = 0; kk < kB; kk += 4) {
+                const int64_t k = (int64_t)J * kB + kk + (lane >> 4);
+                const double a = Lt[ro + (lane & 15) + k * kp];
+                const double bv = colok ? B[k + col * kp] : 0.0;
+                acc = mfma4(a, bv, acc);
+            }
+        }
+        if (kh == 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[rb][((lane >> 4) + 4 * r) * 17 + (lane & 15)] = acc[r];
+        }
+        __syncthreads();
+        if (kh == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = (lane >> 4) + 4 * r;
+                const double bv = colok ? B[ro + row + col * kp] : 0.0;
+                const double w = bv - (acc[r] + red[rb][row * 17 + (lane & 15)]);
+                wI[(rb * 16 + row) * 17 + (lane & 15)] = w;
+                if (colok) B[ro + row + col * kp] = w;
+            }
+        }
+        __syncthreads();
+        if (kh == 0) {       // U rows of this wave: S_I (rows 16 rb ..) x W_I
+            f64x4 u = {0.0, 0.0, 0.0, 0.0};
+            const double* Si = Sd + (int64_t)I * kB * kB;
+#pragma unroll
+            for (int kk = 0; kk < kB; kk += 4) {
+                const int k = kk + (lane >> 4);
+                u = mfma4(Si[rb * 16 + (lane & 15) + k * kB], wI[k * 17 + (lane & 15)], u);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (colok) U[ro + (lane >> 4) + 4 * r + col * kp] = u[r];
+        }
+        __syncthreads();
+    }
+    // ---- backward: Z_I = U_I - sum_{J>I} Lt_JI^T Z_J  (Z overwrites B)
+    for (int I = nbk - 1; I >= 0; --I) {
+        const int64_t ro = (int64_t)I * kB + rb * 16;
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int J = I + 1 + kh; J < nbk; J += 2) {
+#pragma unroll
+            for (int kk = 0; kk < kB; kk += 4) {
+                const int64_t k = (int64_t)J * kB + kk + (lane >> 4);
+                const double a = LtT[ro + (lane & 15) + k * kp];
+                const double bv = colok ? B[k + col * kp] : 0.0;
+                acc = mfma4(a, bv, acc);
+            }
+        }
+        if (kh == 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[rb][((lane >> 4) + 4 * r) * 17 + (lane & 15)] = acc[r];
+        }
+        __syncthreads();
+        if (kh == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = (lane >> 4) + 4 * r;
+                if (colok)
+                    B[ro + row + col * kp] =
+                        U[ro + row + col * kp] - (acc[r] + red[rb][row * 17 + (lane & 15)]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+inline int grid_of(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, 65536));
+}
+
+}  // namespace
+
+int64_t spd_padded(int64_t k) { return (k + kB - 1) / kB * kB; }
+
+hipError_t launch_pad_matrix(const double* src, int64_t rows, int64_t cols, int64_t lds,
+                             double* dst, int64_t kp, double diag, int64_t ncols, hipStream_t s) {
+    if (kp <= 0 || ncols <= 0) return hipSuccess;
+    if (rows > 0 && cols > 0 && !src) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pad_matrix, grid_of(kp * ncols, 256), 256, 0, s, src, rows, cols, lds, dst,
+                       kp, diag, ncols);
+    return hipGetLastError();
+}
+
+hipError_t launch_spd_factor(double* P, int64_t kp, double* Lt, double* LtT, double* Sd,
+                             int32_t* info, hipStream_t s) {
+    if (kp <= 0 || kp % kB) return hipErrorInvalidValue;
+    const int nbk = (int)(kp / kB);
+    hipLaunchKernelGGL(ldl_first, 1, 256, 0, s, P, kp, Sd, info);
+    hipError_t e = hipGetLastError();
+    for (int J = 0; J + 1 < nbk && e == hipSuccess; ++J) {
+        const int pairs = (nbk - 1 - J) * (nbk - J) / 2;
+        hipLaunchKernelGGL(ldl_step, pairs, 256, 0, s, P, kp, J, nbk, Lt, LtT, Sd, info);
+        e = hipGetLastError();
+    }
+    return e;
+}
+
+hipError_t launch_spd_solve(const double* Lt, const double* LtT, const double* Sd, int64_t kp,
+                            double* B, int64_t nrhs, double* U, const int32_t* info,
+                            hipStream_t s) {
+    if (kp <= 0 || kp % kB || nrhs <= 0) return nrhs == 0 ? hipSuccess : hipErrorInvalidValue;
+    const int64_t g = (nrhs + 15) / 16;
+    if (g > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ldl_solve, dim3((unsigned)g), 256, 0, s, Lt, LtT, Sd, kp, (int)(kp / kB),
+                       B, nrhs, U, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_slice_increments(const double* X, const double* Z, int64_t ldz, double* G,
+                                   int64_t S, int64_t Et, hipStream_t s) {
+    if (S <= 0) return hipSuccess;
+    if (Et < 2 || Et > (1 << 20)) return hipErrorInvalidValue;
+    const int64_t nst = (S + kGN - 1) / kGN;
+    const int nmt = (int)((Et + kGM - 1) / kGM);
+    const int64_t groups = (nst + 7) / 8;
+    const int64_t grid = groups * 8 * nmt;
+    if (grid > 0x7fffffff || nst > 0x7fffffff) return hipErrorInvalidValue;
+    const size_t lds = 2 * kGStage * sizeof(double);
+    hipLaunchKernelGGL(slice_increments, dim3((unsigned)grid), 256, lds, s, X, Z, ldz, G, S,
+                       (int)Et, (int)nst, nmt);
+    return hipGetLastError();
+}
+
+}  // namespace mcr

@@ -441,6 +441,24 @@ __global__ void gather_series(const double* __restrict__ O, int64_t mO,
     }
 }
 
+// Lateral-inflow correction of a sub-basin entry reach from the upstream sub-basin's outlet
+// series (simulation.py:152-159, AsyncSimulation._accumulate): forcing row r of slot `dslot`
+//   F[r][dslot] += alpha * I(r + 1) / gamma + beta * I(r) / gamma,  r < T,
+// I(t) = the outlet's outflow after step t - 1 of the upstream run (I(0) = o_start, the outflow
+// the run started from), in the reference's association.
+__global__ void lateral_correction(const double* __restrict__ O, const int64_t* __restrict__ jbase,
+                                   int64_t j, int slots, double o_start, double alpha,
+                                   double beta, double gamma, double* __restrict__ F,
+                                   int64_t ns, int64_t dslot, int64_t T) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < T;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const double inext = O[jbase[j] + r * slots];
+        const double iprev = r == 0 ? o_start : O[jbase[j] + (r - 1) * slots];
+        double* f = F + r * ns + dslot;
+        *f = *f + (alpha * inext / gamma + beta * iprev / gamma);
+    }
+}
+
 inline int grid_for(int64_t work, int block) {
     int64_t g = (work + block - 1) / block;
     if (g < 1) g = 1;
@@ -449,6 +467,16 @@ inline int grid_for(int64_t work, int block) {
 }
 
 }  // namespace
+
+hipError_t launch_lateral_correction(const double* O, const int64_t* jbase, int64_t j, int slots,
+                                     double o_start, double alpha, double beta, double gamma,
+                                     double* F, int64_t ns, int64_t dslot, int64_t T,
+                                     hipStream_t s) {
+    if (T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lateral_correction, grid_for(T, 256), 256, 0, s, O, jbase, j, slots,
+                       o_start, alpha, beta, gamma, F, ns, dslot, T);
+    return hipGetLastError();
+}
 
 template <bool DENSE>
 hipError_t launch_wavefront_t(const WaveArgs& a, int grid, int slots, int chain, size_t lds,

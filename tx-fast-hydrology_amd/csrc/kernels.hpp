@@ -207,4 +207,12 @@ hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbas
                                 int slots, double* out, int64_t n, int64_t T, int64_t E,
                                 hipStream_t s);
 
+// F[r][dslot] += alpha * I(r + 1) / gamma + beta * I(r) / gamma for r < T, I(t) = the outflow of
+// caller reach j after step t - 1 in the output windows O / jbase (I(0) = o_start): the
+// sub-basin lateral correction of simulation.py:152-159
+hipError_t launch_lateral_correction(const double* O, const int64_t* jbase, int64_t j, int slots,
+                                     double o_start, double alpha, double beta, double gamma,
+                                     double* F, int64_t ns, int64_t dslot, int64_t T,
+                                     hipStream_t s);
+
 }  // namespace mcr

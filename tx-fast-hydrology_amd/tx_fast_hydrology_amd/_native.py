@@ -103,6 +103,9 @@ SIGNATURES = {
     "mc_ens_unpack_apply": (_i32, [_vp, _i64, _vp]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_set_flow_patience": (_i32, [_vp, _i64]),
+    "mc_net_lateral_correction": (_i32, [_vp, _i64, _vp, _i64, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_double, ctypes.c_double]),
+    "mc_net_reroutes": (_i32, [_vp, ctypes.POINTER(ctypes.c_int64)]),
     "mc_probe_tick_floor": (_i32, [ctypes.c_int32, ctypes.c_int32, _i64, ctypes.POINTER(ctypes.c_double)]),
     "mc_get_mode": (_i32, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "mc_set_trace": (_i32, [_vp, ctypes.c_int]),

@@ -167,6 +167,22 @@ class RoutingNet:
         the forecast)."""
         nat.check(nat.lib().mc_net_copy_state(self._h, other._h))
 
+    def add_lateral_correction(self, reach: int, src: "RoutingNet", src_reach: int,
+                               o_start: float, alpha: float, beta: float, gamma: float):
+        """Forcing row r of `reach` += alpha I(r+1) / gamma + beta I(r) / gamma, I = the outflow
+        series of `src_reach` in src's last horizon (I(0) = o_start): the sub-basin coupling of
+        the reference's AsyncSimulation, on the device and ordered on the streams
+        (mcroute.h mc_net_lateral_correction)."""
+        nat.check(nat.lib().mc_net_lateral_correction(
+            self._h, int(reach), src._h, int(src_reach), float(o_start), float(alpha),
+            float(beta), float(gamma)))
+
+    def reroutes(self) -> int:
+        """Horizons re-routed with launches after a dataflow wait gave up."""
+        c = ctypes.c_int64()
+        nat.check(nat.lib().mc_net_reroutes(self._h, ctypes.byref(c)))
+        return c.value
+
     # -- routing -------------------------------------------------------------------------
     def step(self, q_t_next, o_t_prev=None, i_t_prev=None):
         """One timestep; returns fresh (i_t_next, o_t_next) like nutils._ax_bu."""

@@ -7,6 +7,14 @@ into the lateral-inflow correction of the downstream entry reach,
 ``alpha * I / gamma + beta * I_prev / gamma`` (reference ``simulation.py:137-166``), which
 makes the collection reproduce the routing of the whole network.
 
+When no sub-basin has callbacks, the collection runs as a device DAG instead: every
+sub-basin's horizon is launched on its own session stream in dependency order, each cut edge's
+correction is added on the device into the downstream session's forcing
+(``RoutingNet.add_lateral_correction``, ordered by stream events), and the outflows are fetched
+only after every launch -- no host round trip between sub-basins, independent sub-basins run
+concurrently.  The corrections are applied in the order the reference's task group applies them
+(its FIFO schedule is replayed on the host), so results are bit-identical to the host driver.
+
 ``CheckPoint`` saves the model state once at a checkpoint time (reference :169-211).
 """
 from __future__ import annotations
@@ -15,6 +23,7 @@ import asyncio
 import datetime
 import logging
 
+import numpy as np
 import pandas as pd
 
 from .callbacks import BaseCallback
@@ -100,6 +109,8 @@ class AsyncSimulation(Simulation):
         return self.outputs
 
     async def _main(self):
+        if _device_dag(self):
+            return
         self._indegree = {model.name: len(model.sources)
                           for model in self.model_collection.models.values()}
         async with TaskGroup() as taskgroup:
@@ -131,6 +142,112 @@ class AsyncSimulation(Simulation):
                 taskgroup.create_task(self._simulate(taskgroup, link.downstream_model, frame,
                                                      target))
         logger.debug(f"Finished job for sub-watershed {name}")
+
+
+def _task_order(sim):
+    """Replay of the reference task group's FIFO schedule (simulation.py:110-166): the order
+    the sub-basins run in and, per downstream sub-basin, the order its corrections arrive."""
+    from collections import deque
+    indeg = {m.name: len(m.sources) for m in sim.models.values()}
+    ready = deque(("sim", name) for name, k in indeg.items() if k == 0)
+    runs, corrections = [], {name: [] for name in sim.models}
+    while ready:
+        kind, name = ready.popleft()
+        if kind == "sim":
+            runs.append(name)
+            ready.append(("acc", name))
+            continue
+        for link in sim.models[name].sinks:
+            target = link.downstream_model.name
+            if target == name:
+                continue
+            corrections[target].append(link)
+            indeg[target] -= 1
+            if not indeg[target]:
+                ready.append(("sim", target))
+    return runs, corrections
+
+
+def _step_times(model, end_time):
+    xs, t = [], model.datetime
+    while t < end_time:
+        t = t + model.timedelta
+        xs.append(t)
+    return xs
+
+
+def _device_dag(sim):
+    """Route the collection as a device DAG (module docstring).  Returns False, having changed
+    nothing, when the host driver must run it: callbacks bound, a session that is not a device
+    session, an empty horizon, or forcing rows that do not match the upstream horizon."""
+    models = sim.models
+    if any(m.callbacks for m in models.values()):
+        return False
+    runs, corrections = _task_order(sim)
+    if len(runs) != len(models):
+        return False
+    steps = {}
+    for name in runs:
+        inputs = sim.inputs[name]
+        if not isinstance(inputs.index, pd.DatetimeIndex) or inputs.index.tz is None:
+            return False
+        steps[name] = _step_times(models[name], inputs.index.max())
+        if not steps[name]:
+            return False
+    for name in runs:
+        for link in corrections[name]:
+            if len(sim.inputs[name]) != len(steps[link.upstream_model.name]):
+                return False
+    nets = {}
+    for name in runs:
+        net = models[name]._device.session(models[name])
+        if not hasattr(net, "add_lateral_correction"):
+            return False
+        nets[name] = net
+    before = {name: nets[name].reroutes() for name in runs}
+    start = {name: (models[name].datetime, models[name].o_t_next, models[name].i_t_next)
+             for name in runs}
+    for name in runs:
+        m, inputs, net = models[name], sim.inputs[name], nets[name]
+        xp = inputs.index.astype(int).astype(float).values
+        net.load_forcing(xp, np.ascontiguousarray(inputs.values, dtype=np.float64))
+        net.set_state(m.o_t_next, m.i_t_next)
+    # enqueue: corrections then the horizon of every sub-basin, in the reference's order
+    for name in runs:
+        m, net = models[name], nets[name]
+        for link in corrections[name]:
+            up = link.upstream_model
+            j = link.downstream_index
+            net.add_lateral_correction(j, nets[up.name], link.upstream_index,
+                                       start[up.name][1][link.upstream_index], m.alpha[j],
+                                       m.beta[j], m.gamma[j])
+        net.run(np.array([float(t.value) for t in steps[name]]))
+    outs = {name: nets[name].fetch_outputs() for name in runs}
+    if any(nets[name].reroutes() != before[name] for name in runs):
+        raise RuntimeError("a sub-basin horizon was re-routed after a dataflow wait gave up; "
+                           "the device DAG's corrections used incomplete outflows")
+    for name in runs:
+        m, inputs = models[name], sim.inputs[name]
+        t0, o0, i0 = start[name]
+        out_o, out_i = outs[name]
+        T = len(steps[name])
+        # the state simulate_iter leaves (muskingum.py:458-464 per step)
+        m.o_t_prev, m.i_t_prev = (out_o[-2], out_i[-2]) if T > 1 else (o0, i0)
+        m.o_t_next, m.i_t_next = out_o[-1].copy(), out_i[-1].copy()
+        m.datetime = steps[name][-1]
+        index = pd.to_datetime([t0] + steps[name], utc=True)
+        sim.outputs[name] = pd.DataFrame(np.vstack([o0[None, :], out_o]), index=index,
+                                         columns=inputs.columns)
+    # the corrected input frames, as the reference's += leaves them (same arithmetic)
+    for name in runs:
+        frame = sim.inputs[name]
+        for link in corrections[name]:
+            up = link.upstream_model
+            series = sim.outputs[up.name][up.reach_ids[link.upstream_index]]
+            column = models[name].reach_ids[link.downstream_index]
+            frame.loc[:, column] += _lateral_correction(models[name], link.downstream_index,
+                                                        series)
+    return True
 
 
 def _outflow_frame(model, inputs):
