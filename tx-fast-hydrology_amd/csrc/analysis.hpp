@@ -25,24 +25,18 @@ hipError_t launch_dgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, doubl
 // G [Et][S]; 128 x 128 MFMA tiles, member mean as a rank-1 epilogue correction
 hipError_t launch_slice_increments(const double* X, const double* Z, int64_t ldz, double* G,
                                    int64_t S, int64_t Et, hipStream_t s);
-// SPD systems through a block LDL^T with 32 x 32 blocks on a padded copy (kp = spd_padded(k)):
+// SPD systems B := P^-1 B by block Gauss-Jordan elimination (32 x 32 pivot blocks) on a padded
+// copy (kp = spd_padded(k)):
 //   launch_pad_matrix: dst (kp x ncols, ld kp) = src where i < rows and j < cols, `diag` on the
 //     other diagonal entries, 0 elsewhere (the padded SPD matrix: diag 1; right-hand sides: 0)
-//   launch_spd_factor: P (kp x kp, overwritten) = Lt D Lt^T; Lt / LtT (kp x kp) the unit block
-//     lower factor and its transpose (strictly lower blocks written), Sd (kp / 32 blocks of
-//     32 x 32) the inverses of the D blocks; info = 0, or the 1-based index of the first
-//     non-positive pivot.  One launch per block column.
-//   launch_spd_solve: B (kp x nrhs, ld kp, padding rows 0) := P^-1 B; U scratch of B's shape;
-//     B = 0 when the factorisation failed.
+//   launch_spd_solve: P (kp x kp, full symmetric, overwritten) and B (kp x nrhs, ld kp,
+//     padding rows 0) := P^-1 B; Sd: kp x 32 doubles of pivot-block inverses; info = 0, or the
+//     1-based index of the first non-positive pivot (then B = 0).  kp / 32 + 2 launches.
 int64_t spd_padded(int64_t k);
 hipError_t launch_pad_matrix(const double* src, int64_t rows, int64_t cols, int64_t lds,
                              double* dst, int64_t kp, double diag, int64_t ncols, hipStream_t s);
-hipError_t launch_spd_factor(double* P, int64_t kp, double* Lt, double* LtT, double* Sd,
-                             int32_t* info, hipStream_t s);
-hipError_t launch_spd_solve(const double* Lt, const double* LtT, const double* Sd, int64_t kp,
-                            double* B, int64_t nrhs, double* U, const int32_t* info,
-                            hipStream_t s);
-// ensemble mean over members and anomalies A = X - mean (both [E][ns])
+hipError_t launch_spd_solve(double* P, int64_t kp, double* B, int64_t nrhs, double* Sd,
+                            int32_t* info, hipStream_t s);
 // U = R^-1 HA for a diagonal R (r = its diagonal), column-major m x E
 hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64_t m, int64_t E,
                              hipStream_t s);

@@ -138,7 +138,7 @@ struct Net {
     DBuf<double> An, HA, Zn, Gn, Yb, HXb, Db, Rd, Rb, Ub, EE, Wk;   // Wk: split-K slices
     // SPD solves (dense.hip block LDL^T): padded matrix, unit block factor and its transpose,
     // inverted diagonal blocks, solve scratch, padded right-hand sides
-    DBuf<double> Pf, Lt, LtT, Sd, Ubuf, Rhs;
+    DBuf<double> Pf, Sd, Rhs;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
     int32_t* info_host = nullptr;      // pinned copy of the factorisation status, read at sync()
@@ -427,19 +427,12 @@ struct Net {
         return true;
     }
 
-    // P (kp x kp, padded SPD) = Lt D Lt^T, the status in `info` (device); kp = spd_padded(k)
-    void spd_factor(double* P, int64_t kp) {
-        Lt.reserve((size_t)(kp * kp));
-        LtT.reserve((size_t)(kp * kp));
+    // B (kp x nrhs, leading dimension kp, padding rows 0) := P^-1 B for the padded SPD P
+    // (kp x kp, overwritten); the status in `info` (device): B = 0 if P is not positive definite
+    void spd_solve(double* P, int64_t kp, double* B, int64_t nrhs) {
         Sd.reserve((size_t)(kp * 32));
         info.reserve(1);
-        HIPC(mcr::launch_spd_factor(P, kp, Lt.p, LtT.p, Sd.p, info.p, stream));
-    }
-    // B (kp x nrhs, leading dimension kp, padding rows 0) := P^-1 B; B = 0 if the factorisation
-    // failed
-    void spd_solve(int64_t kp, double* B, int64_t nrhs) {
-        Ubuf.reserve((size_t)(kp * std::max<int64_t>(nrhs, 1)));
-        HIPC(mcr::launch_spd_solve(Lt.p, LtT.p, Sd.p, kp, B, nrhs, Ubuf.p, info.p, stream));
+        HIPC(mcr::launch_spd_solve(P, kp, B, nrhs, Sd.p, info.p, stream));
     }
     // the factorisation status, read back asynchronously and reported at the next sync()
     void info_async() {
@@ -450,7 +443,7 @@ struct Net {
         info_pending = true;
     }
 
-    // C = HA HA^T / (E-1) + R (m x m) factored from the current member state (padded to
+    // C = HA HA^T / (E-1) + R (m x m) from the current member state (padded to
     // mp = spd_padded(m) in Pf); anomalies in An, gauge anomalies in HA
     void analysis_setup(int64_t m, const int64_t* gauges, const double* R) {
         REQUIRE(E >= 2, "the ensemble analysis needs at least 2 members");
@@ -475,11 +468,6 @@ struct Net {
         HIPC(mcr::launch_pad_matrix(Rb.p, m, m, m, Pf.p, mp, 1.0, mp, stream));
         HIPC(mcr::launch_dgemm(false, true, m, m, E, inv, HA.p, m, HA.p, m, 1.0, Pf.p, mp,
                                stream));
-        spd_factor(Pf.p, mp);
-        int32_t ih = 0;
-        HIPC(hipMemcpyAsync(&ih, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
-        sync();
-        if (ih != 0) throw Fail(MC_E_INVALID, "HPH^T + R is not positive definite");
     }
 
     // ---- staged ensemble analysis: the member-sharded form (several ranks, one per GPU; the
@@ -546,8 +534,7 @@ struct Net {
             double* V = EE.p + kp * kp;
             HIPC(mcr::launch_dgemm(true, false, Et, 2 * Et, m, inv, Ub.p, m, HA.p, m, 1.0, EE.p,
                                    kp, stream, Wk.p, Wk.cap, Dall, Et, V));
-            spd_factor(EE.p, kp);
-            spd_solve(kp, V, Et);
+            spd_solve(EE.p, kp, V, Et);
             info_async();
             Z = V;
             ldz = kp;
@@ -560,11 +547,10 @@ struct Net {
             HIPC(mcr::launch_pad_matrix(Rb.p, m, m, m, Pf.p, mp, 1.0, mp, stream));
             HIPC(mcr::launch_dgemm(false, true, m, m, Et, inv, HA.p, m, HA.p, m, 1.0, Pf.p, mp,
                                    stream));
-            spd_factor(Pf.p, mp);
-            info_async();
             Rhs.reserve((size_t)(mp * Et));
             HIPC(mcr::launch_pad_matrix(Dall, m, Et, m, Rhs.p, mp, 0.0, Et, stream));
-            spd_solve(mp, Rhs.p, Et);
+            spd_solve(Pf.p, mp, Rhs.p, Et);
+            info_async();
             Zn.reserve((size_t)(Et * Et));
             Wk.reserve((size_t)(64 * Et * Et));
             HIPC(mcr::launch_dgemm(true, false, Et, Et, m, inv, HA.p, m, Rhs.p, mp, 0.0, Zn.p, Et,
@@ -619,7 +605,11 @@ struct Net {
         HIPC(hipMemsetAsync(Gn.p, 0, (size_t)(mp * ns) * sizeof(double), stream));
         HIPC(mcr::launch_dgemm(false, true, m, ns, E, inv, HA.p, m, An.p, ns, 0.0, Gn.p, mp,
                                stream));
-        spd_solve(mp, Gn.p, ns);
+        spd_solve(Pf.p, mp, Gn.p, ns);
+        int32_t ih = 0;
+        HIPC(hipMemcpyAsync(&ih, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        sync();
+        if (ih != 0) throw Fail(MC_E_INVALID, "HPH^T + R is not positive definite");
         outT.reserve((size_t)(plan.n * m));
         HIPC(mcr::launch_gain_to_caller(Gn.p, mp, outT.p, pos.p, m, plan.n, stream));
         HIPC(hipMemcpyAsync(K_out, outT.p, (size_t)(plan.n * m) * sizeof(double),

@@ -7,15 +7,17 @@
 //    2 S Et^2 flops).  128 x 128 output tiles, 4 waves of 64 x 64, K slices double-buffered in
 //    LDS, the member mean folded in as a rank-1 epilogue correction (G = X Z - xbar zs^T) so
 //    X is read once and no anomaly array is materialised.
-//  * block LDL^T of an SPD k x k matrix (32 x 32 blocks): A = Lt D Lt^T with Lt unit block lower
-//    triangular and D = blockdiag(D_J); every D_J is inverted (S_J = D_J^-1) by a Cholesky of
-//    the 32 x 32 block, which also detects a matrix that is not positive definite.  One launch
-//    per block column (the step kernel recomputes Lt_IJ = A_IJ S_J in every workgroup that
-//    needs it, and the workgroup of the next diagonal block inverts it right after its update).
-//  * the solve B := A^-1 B: W = Lt^-1 B (unit block lower), U_I = S_I W_I, Z = Lt^-T U, one
-//    workgroup per 16 right-hand sides, the block sums on MFMA.
-// Matrices are column-major; the factorisation works on a copy padded to kp = 32 * ceil(k / 32)
-// with an identity block (pad_square), so every block is full.
+//  * SPD solves B := A^-1 B by block Gauss-Jordan elimination with 32 x 32 pivot blocks on the
+//    augmented system [A | B]: step J eliminates block column J from every other block row
+//    (A_IC -= A_IJ S_J A_JC, B_I -= A_IJ S_J B_J, S_J = D_J^-1 the inverse of the pivot block),
+//    and a last launch scales B_I := S_I B_I.  Every step is one launch whose workgroups each
+//    update one block; the workgroup that updates the next pivot block inverts it (a Cholesky
+//    of the 32 x 32 block, which also detects a matrix that is not positive definite).  The
+//    sequential chain is k / 32 + 2 launches and no separate substitution passes (a blocked
+//    LDL^T + forward / backward substitution took ~250 us at k = 256: ~20 dependent cross-XCD
+//    round trips).
+// Matrices are column-major; the elimination works on a copy padded to kp = 32 * ceil(k / 32)
+// with an identity block (pad_matrix), so every block is full.
 #include "analysis.hpp"
 
 #include <hip/hip_runtime.h>
@@ -183,40 +185,67 @@ __device__ __forceinline__ int blk_col(int wave, int lane) {
     return (wave & 1) * 16 + (lane & 15);
 }
 
-// S = A^-1 of the SPD 32 x 32 block in `a` (LDS, rows of stride kL, lower part used; it is
-// overwritten), by Gaussian elimination of [A | I] with symmetric pivots: the right part becomes
-// Lu^-1 (A = Lu D Lu^T, Lu unit lower), T = D^-1/2 Lu^-1 = L^-1 for the Cholesky factor L, and
-// S = T^T T.  t: LDS scratch.  Returns the 1-based index of the first non-positive pivot (0 =
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// S = A^-1 of the SPD 32 x 32 block in `a` (LDS, rows of stride kL; its lower part is read)
+// by Gaussian elimination of [A | I] with symmetric pivots: the right part becomes Lu^-1
+// (A = Lu D Lu^T, Lu unit lower), T = D^-1/2 Lu^-1 = L^-1 for the Cholesky factor L, and
+// S = T^T T.  The elimination runs in ONE wave without barriers: lane l holds row l & 31 of A
+// (lanes 0-31) or of the identity / T (lanes 32-63) in registers.  At pivot j the A rows need
+// the pivot row's entries c > j and the T rows its entries c <= j (the others are zero or no
+// longer read), so every column takes ONE uniform scalar read of the pivot lane (readlane);
+// only the multipliers of the T rows cross the halves (one swap per pivot).  (A 256-thread
+// LDS form with a barrier per pivot took ~20 us per block, cross-lane permutes ~18 us.)
+// t: LDS scratch for T.  Returns the 1-based index of the first non-positive pivot (0 =
 // positive definite); all 256 threads call it.
-__device__ int block_inverse(double* a, double* t, double* s) {
+__device__ __forceinline__ int block_inverse(const double* a, double* t, double* s) {
+    __shared__ int bad_sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int x = tid; x < kB * kB; x += 256) {
-        const int i = x / kB, c = x % kB;
-        t[i * kL + c] = i == c ? 1.0 : 0.0;
+    if (wave == 0) {
+        const int row = lane & 31;
+        const bool up = lane >= 32;
+        double r[kB];
+#pragma unroll
+        for (int c = 0; c < kB; ++c) {
+            const double v = row >= c ? a[row * kL + c] : a[c * kL + row];   // symmetric
+            r[c] = up ? (row == c ? 1.0 : 0.0) : v;
+        }
+        int bad = 0;
+        double mydiag = 1.0;
+        // runtime pivot loop (a fully unrolled 32 x 32 body sends the compiler's scheduler into
+        // tens of minutes); the pivot column is picked from the registers by a select chain
+#pragma unroll 1
+        for (int j = 0; j < kB; ++j) {
+            double rj = r[0];
+#pragma unroll
+            for (int c = 1; c < kB; ++c) rj = j == c ? r[c] : rj;
+            const double d = readlane_f64(rj, j);               // pivot of the Schur complement
+            if (!(d > 0.0) && bad == 0) bad = j + 1;
+            if (row == j) mydiag = d;
+            const double aj = __shfl_xor(rj, 32);               // T lanes: A[row][j]
+            const double m = row > j ? (up ? aj : rj) / d : 0.0;
+            const double mlo = up ? 0.0 : m, mup = up ? m : 0.0;
+#pragma unroll
+            for (int c = 0; c < kB; ++c) {
+                const bool a_part = c > j;                      // A rows: pivot row entries c > j
+                const double mm = a_part ? mlo : mup;           // T rows: entries c <= j
+                r[c] = r[c] - mm * readlane_f64(r[c], a_part ? j : j + 32);
+            }
+        }
+        if (up) {
+            const double sc = 1.0 / sqrt(mydiag);
+#pragma unroll
+            for (int c = 0; c < kB; ++c) t[row * kL + c] = c <= row ? r[c] * sc : 0.0;
+        }
+        if (lane == 0) bad_sh = bad;
     }
     __syncthreads();
-    int bad = 0;
-    for (int j = 0; j < kB; ++j) {
-        const double d = a[j * kL + j];
-        if (!(d > 0.0)) {          // same value in every thread: a uniform exit
-            bad = j + 1;
-            break;
-        }
-        const double invd = 1.0 / d;
-        for (int x = tid; x < (kB - 1 - j) * kB; x += 256) {
-            const int i = j + 1 + x / kB, c = x % kB;
-            const double m = a[i * kL + j] * invd;
-            if (c <= j) t[i * kL + c] = t[i * kL + c] - m * t[j * kL + c];
-            else if (c <= i) a[i * kL + c] = a[i * kL + c] - m * a[c * kL + j];
-        }
-        __syncthreads();
-    }
+    const int bad = bad_sh;
     if (bad) return bad;
-    for (int x = tid; x < kB * kB; x += 256) {    // rows of Lu^-1 scaled by D^-1/2
-        const int i = x / kB, c = x % kB;
-        t[i * kL + c] = c <= i ? t[i * kL + c] / sqrt(a[i * kL + i]) : 0.0;
-    }
-    __syncthreads();
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     acc = mma32([&](int i, int k) { return t[k * kL + i]; },
                 [&](int k, int j) { return t[k * kL + j]; }, acc, wave, lane);
@@ -269,33 +298,39 @@ __global__ __launch_bounds__(256) void ldl_first(const double* __restrict__ P, i
     store_block(s, Sd, kB);
 }
 
-// Block column J: every workgroup owns one trailing block (I, C), J < C <= I:
-//   Lt_IJ = A_IJ S_J,  A_IC -= Lt_IJ A_CJ^T;
-// the workgroup (I, J + 1) stores Lt_IJ (and its transpose), the workgroup (J + 1, J + 1)
-// inverts its updated block into S_{J+1}.
-__global__ __launch_bounds__(256) void ldl_step(double* __restrict__ P, int64_t kp, int J,
-                                                int nbk, double* __restrict__ Lt,
-                                                double* __restrict__ LtT,
-                                                double* __restrict__ Sd,
-                                                int32_t* __restrict__ info) {
-    __shared__ double sS[kB * kL], sA[kB * kL], sC[kB * kL], sL[kB * kL];
-    if (*info != 0) return;                          // an earlier block was not SPD
-    // blockIdx -> (I, C): pairs enumerated column by column, C = J+1 .. nbk-1, I = C .. nbk-1
-    int rem = blockIdx.x, C = J + 1;
-    while (rem >= nbk - C) {
-        rem -= nbk - C;
-        ++C;
-    }
-    const int I = C + rem;
+// Block Gauss-Jordan step J on [P | B] (P kp x kp, B kp x nrhs, both column-major with
+// leading dimension kp): every workgroup updates one block X_IC' of a row I != J, where C' is a
+// matrix block column C > J or a right-hand-side block r (32 columns):
+//   X_IC' -= (A_IJ S_J) X_JC'
+// Row J and column J are read only, so the blocks of one step are independent.  The workgroup
+// of block (J + 1, J + 1) inverts it into S_{J+1} after its update.
+__global__ __launch_bounds__(256) void gj_step(double* __restrict__ P, int64_t kp, int J,
+                                               int nbk, double* __restrict__ B, int64_t nrhs,
+                                               int nrb, double* __restrict__ Sd,
+                                               int32_t* __restrict__ info) {
+    __shared__ double sS[kB * kL], sA[kB * kL], sX[kB * kL], sL[kB * kL];
+    if (*info != 0) return;                          // an earlier pivot block was not SPD
+    const int per_row = (nbk - 1 - J) + nrb;         // blocks C' of one row I
+    const int ii = blockIdx.x / per_row, cc = blockIdx.x - ii * per_row;
+    const int I = ii < J ? ii : ii + 1;              // every row but J
+    const bool mat = cc < nbk - 1 - J;
+    const int C = mat ? J + 1 + cc : cc - (nbk - 1 - J);   // matrix block column / RHS block
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t ro = (int64_t)I * kB, co = (int64_t)C * kB, jo = (int64_t)J * kB;
+    const int64_t ro = (int64_t)I * kB, jo = (int64_t)J * kB;
+    double* X = mat ? P : B;                         // the operand this block belongs to
+    const int64_t co = (int64_t)C * kB;
+    const int64_t ncol = mat ? kp : nrhs;            // columns of X
     load_block(Sd + (int64_t)J * kB * kB, kB, sS);
-    load_block(P + ro + jo * kp, kp, sA);
-    if (I != C) load_block(P + co + jo * kp, kp, sC);
-    f64x4 acc;                                       // A_IC in the MFMA layout
+    load_block(P + ro + jo * kp, kp, sA);            // A_IJ
+    for (int x = tid; x < kB * kB; x += 256) {       // X_JC' (row J)
+        const int i = x % kB, c = x / kB;
+        sX[i * kL + c] = co + c < ncol ? X[jo + i + (co + c) * kp] : 0.0;
+    }
+    f64x4 acc;                                       // X_IC' in the MFMA layout
+    const int64_t mycol = co + blk_col(wave, lane);
+    const bool colok = mycol < ncol;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-        acc[r] = P[ro + blk_row(wave, lane, r) + (co + blk_col(wave, lane)) * kp];
+    for (int r = 0; r < 4; ++r) acc[r] = colok ? X[ro + blk_row(wave, lane, r) + mycol * kp] : 0.0;
     __syncthreads();
     f64x4 l = {0.0, 0.0, 0.0, 0.0};
     l = mma32([&](int i, int k) { return sA[i * kL + k]; },
@@ -303,131 +338,52 @@ __global__ __launch_bounds__(256) void ldl_step(double* __restrict__ P, int64_t 
 #pragma unroll
     for (int r = 0; r < 4; ++r) sL[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = l[r];
     __syncthreads();
-    const double* cj = I != C ? sC : sA;
     acc = mma32([&](int i, int k) { return -sL[i * kL + k]; },
-                [&](int k, int j) { return cj[j * kL + k]; }, acc, wave, lane);
+                [&](int k, int j) { return sX[k * kL + j]; }, acc, wave, lane);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-        P[ro + blk_row(wave, lane, r) + (co + blk_col(wave, lane)) * kp] = acc[r];
-    if (C == J + 1) {
-        store_block(sL, Lt + ro + jo * kp, kp);
-        for (int x = tid; x < kB * kB; x += 256) {    // LtT block (J, I) = Lt_IJ^T
-            const int i = x % kB, c = x / kB;
-            LtT[jo + i + (ro + c) * kp] = sL[c * kL + i];
-        }
-        if (I == C) {
-            // the next diagonal block: fully updated now; invert it (after every wave's update
-            // read of sA)
-            __syncthreads();
+        if (colok) X[ro + blk_row(wave, lane, r) + mycol * kp] = acc[r];
+    if (mat && I == J + 1 && C == J + 1) {
+        // the next pivot block: fully updated now; invert it (after every wave's read of sA)
+        __syncthreads();
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sA[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = acc[r];
-            __syncthreads();
-            const int bad = block_inverse(sA, sC, sS);
-            if (bad) {
-                if (tid == 0) *info = (int32_t)(co + bad);
-                return;
-            }
-            store_block(sS, Sd + (int64_t)C * kB * kB, kB);
+        for (int r = 0; r < 4; ++r) sA[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = acc[r];
+        __syncthreads();
+        const int bad = block_inverse(sA, sX, sS);
+        if (bad) {
+            if (tid == 0) *info = (int32_t)(co + bad);
+            return;
         }
+        store_block(sS, Sd + (int64_t)C * kB * kB, kB);
     }
 }
 
-// B := A^-1 B for the factored A (kp x kp; B kp x nrhs, column-major, rows >= k zero), 16
-// right-hand sides per workgroup.  Wave (rb, kh): output rows 16 rb of a block row, block
-// sums over the k blocks of parity kh (the two halves are added through LDS).  U: scratch of
-// B's shape.  A factorisation that failed (*info != 0) gives B = 0.
-__global__ __launch_bounds__(256) void ldl_solve(const double* __restrict__ Lt,
-                                                 const double* __restrict__ LtT,
-                                                 const double* __restrict__ Sd, int64_t kp,
-                                                 int nbk, double* __restrict__ B, int64_t nrhs,
-                                                 double* __restrict__ U,
-                                                 const int32_t* __restrict__ info) {
-    __shared__ double red[2][16 * 17];
-    __shared__ double wI[kB * 17];
+// Last launch of the Gauss-Jordan solve: B_I := S_I B_I for every block row I and right-hand
+// side block (the rows are decoupled now); B := 0 when a pivot block was not SPD.
+__global__ __launch_bounds__(256) void gj_scale(const double* __restrict__ Sd, int64_t kp,
+                                                double* __restrict__ B, int64_t nrhs, int nrb,
+                                                const int32_t* __restrict__ info) {
+    __shared__ double sS[kB * kL], sX[kB * kL];
+    const int I = blockIdx.x / nrb, rbk = blockIdx.x - (blockIdx.x / nrb) * nrb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int rb = wave & 1, kh = wave >> 1;
-    const int64_t c0 = (int64_t)blockIdx.x * 16;
-    const int64_t col = c0 + (lane & 15);
-    const bool colok = col < nrhs;
-    if (*info != 0) {
-        for (int64_t x = tid; x < kp * 16; x += 256) {
-            const int64_t c = c0 + x / kp;
-            if (c < nrhs) B[x % kp + c * kp] = 0.0;
+    const int64_t ro = (int64_t)I * kB, co = (int64_t)rbk * kB;
+    const bool failed = *info != 0;
+    if (!failed) {
+        load_block(Sd + (int64_t)I * kB * kB, kB, sS);
+        for (int x = tid; x < kB * kB; x += 256) {
+            const int i = x % kB, c = x / kB;
+            sX[i * kL + c] = co + c < nrhs ? B[ro + i + (co + c) * kp] : 0.0;
         }
-        return;
     }
-    // ---- forward: W_I = B_I - sum_{J<I} Lt_IJ W_J ;  U_I = S_I W_I
-    for (int I = 0; I < nbk; ++I) {
-        const int64_t ro = (int64_t)I * kB + rb * 16;
-        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int J = kh; J < I; J += 2) {
+    __syncthreads();
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (!failed)
+        acc = mma32([&](int i, int k) { return sS[i * kL + k]; },
+                    [&](int k, int j) { return sX[k * kL + j]; }, acc, wave, lane);
+    const int64_t mycol = co + blk_col(wave, lane);
 #pragma unroll
-            for (int kk = 0; kk < kB; kk += 4) {
-                const int64_t k = (int64_t)J * kB + kk + (lane >> 4);
-                const double a = Lt[ro + (lane & 15) + k * kp];
-                const double bv = colok ? B[k + col * kp] : 0.0;
-                acc = mfma4(a, bv, acc);
-            }
-        }
-        if (kh == 1) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) red[rb][((lane >> 4) + 4 * r) * 17 + (lane & 15)] = acc[r];
-        }
-        __syncthreads();
-        if (kh == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = (lane >> 4) + 4 * r;
-                const double bv = colok ? B[ro + row + col * kp] : 0.0;
-                const double w = bv - (acc[r] + red[rb][row * 17 + (lane & 15)]);
-                wI[(rb * 16 + row) * 17 + (lane & 15)] = w;
-                if (colok) B[ro + row + col * kp] = w;
-            }
-        }
-        __syncthreads();
-        if (kh == 0) {       // U rows of this wave: S_I (rows 16 rb ..) x W_I
-            f64x4 u = {0.0, 0.0, 0.0, 0.0};
-            const double* Si = Sd + (int64_t)I * kB * kB;
-#pragma unroll
-            for (int kk = 0; kk < kB; kk += 4) {
-                const int k = kk + (lane >> 4);
-                u = mfma4(Si[rb * 16 + (lane & 15) + k * kB], wI[k * 17 + (lane & 15)], u);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (colok) U[ro + (lane >> 4) + 4 * r + col * kp] = u[r];
-        }
-        __syncthreads();
-    }
-    // ---- backward: Z_I = U_I - sum_{J>I} Lt_JI^T Z_J  (Z overwrites B)
-    for (int I = nbk - 1; I >= 0; --I) {
-        const int64_t ro = (int64_t)I * kB + rb * 16;
-        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int J = I + 1 + kh; J < nbk; J += 2) {
-#pragma unroll
-            for (int kk = 0; kk < kB; kk += 4) {
-                const int64_t k = (int64_t)J * kB + kk + (lane >> 4);
-                const double a = LtT[ro + (lane & 15) + k * kp];
-                const double bv = colok ? B[k + col * kp] : 0.0;
-                acc = mfma4(a, bv, acc);
-            }
-        }
-        if (kh == 1) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) red[rb][((lane >> 4) + 4 * r) * 17 + (lane & 15)] = acc[r];
-        }
-        __syncthreads();
-        if (kh == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = (lane >> 4) + 4 * r;
-                if (colok)
-                    B[ro + row + col * kp] =
-                        U[ro + row + col * kp] - (acc[r] + red[rb][row * 17 + (lane & 15)]);
-            }
-        }
-        __syncthreads();
-    }
+    for (int r = 0; r < 4; ++r)
+        if (mycol < nrhs) B[ro + blk_row(wave, lane, r) + mycol * kp] = acc[r];
 }
 
 inline int grid_of(int64_t work, int block) {
@@ -448,28 +404,24 @@ hipError_t launch_pad_matrix(const double* src, int64_t rows, int64_t cols, int6
     return hipGetLastError();
 }
 
-hipError_t launch_spd_factor(double* P, int64_t kp, double* Lt, double* LtT, double* Sd,
-                             int32_t* info, hipStream_t s) {
-    if (kp <= 0 || kp % kB) return hipErrorInvalidValue;
+hipError_t launch_spd_solve(double* P, int64_t kp, double* B, int64_t nrhs, double* Sd,
+                            int32_t* info, hipStream_t s) {
+    if (kp <= 0 || kp % kB || nrhs < 0) return hipErrorInvalidValue;
     const int nbk = (int)(kp / kB);
+    const int64_t nrb = (nrhs + kB - 1) / kB;
+    if (nrb * nbk > 0x7fffffff) return hipErrorInvalidValue;
     hipLaunchKernelGGL(ldl_first, 1, 256, 0, s, P, kp, Sd, info);
     hipError_t e = hipGetLastError();
-    for (int J = 0; J + 1 < nbk && e == hipSuccess; ++J) {
-        const int pairs = (nbk - 1 - J) * (nbk - J) / 2;
-        hipLaunchKernelGGL(ldl_step, pairs, 256, 0, s, P, kp, J, nbk, Lt, LtT, Sd, info);
+    for (int J = 0; J < nbk && e == hipSuccess; ++J) {
+        const int64_t blocks = (int64_t)(nbk - 1) * ((nbk - 1 - J) + nrb);
+        if (blocks == 0) continue;
+        hipLaunchKernelGGL(gj_step, dim3((unsigned)blocks), 256, 0, s, P, kp, J, nbk, B, nrhs,
+                           (int)nrb, Sd, info);
         e = hipGetLastError();
     }
-    return e;
-}
-
-hipError_t launch_spd_solve(const double* Lt, const double* LtT, const double* Sd, int64_t kp,
-                            double* B, int64_t nrhs, double* U, const int32_t* info,
-                            hipStream_t s) {
-    if (kp <= 0 || kp % kB || nrhs <= 0) return nrhs == 0 ? hipSuccess : hipErrorInvalidValue;
-    const int64_t g = (nrhs + 15) / 16;
-    if (g > 0x7fffffff) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(ldl_solve, dim3((unsigned)g), 256, 0, s, Lt, LtT, Sd, kp, (int)(kp / kB),
-                       B, nrhs, U, info);
+    if (e != hipSuccess || nrb == 0) return e;
+    hipLaunchKernelGGL(gj_scale, dim3((unsigned)(nbk * nrb)), 256, 0, s, Sd, kp, B, nrhs,
+                       (int)nrb, info);
     return hipGetLastError();
 }
 

@@ -139,7 +139,13 @@ class RoutingNet:
         return info.as_dict()
 
     def set_stream(self, hip_stream: int | None):
-        nat.check(nat.lib().mc_net_set_stream(self._h, ctypes.c_void_p(hip_stream or 0)))
+        """Route on an external hipStream_t (None / 0: the session's own).  Switching streams
+        synchronises the old one; setting the current stream again is free."""
+        h = int(hip_stream or 0)
+        if getattr(self, "_stream", None) == h:
+            return
+        nat.check(nat.lib().mc_net_set_stream(self._h, ctypes.c_void_p(h)))
+        self._stream = h
 
     def set_coeffs(self, alpha, beta, chi, gamma):
         a, b, c, g = f64(alpha), f64(beta), f64(chi), f64(gamma)

@@ -19,6 +19,9 @@ import torch
 import torch.distributed as dist
 
 
+_SIDE = {}      # device index -> the side stream analyses run on when the caller's is the null stream
+
+
 def _world(group):
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(group), dist.get_rank(group)
@@ -71,7 +74,11 @@ def distributed_analysis(net, gauges, y_local, R, device=None, group=None,
         # must not be the null stream (the session maps a NULL stream to its own, unordered one)
         caller = torch.cuda.current_stream(device)
         if caller.cuda_stream == 0:
-            side = torch.cuda.Stream(device)
+            # one side stream per device, kept: the session then stays on it from one analysis
+            # to the next (set_stream synchronises only when the stream changes)
+            side = _SIDE.get(device.index)
+            if side is None:
+                side = _SIDE[device.index] = torch.cuda.Stream(device)
             side.wait_stream(caller)
             with torch.cuda.stream(side):
                 distributed_analysis(net, gauges, y_local, R, group=group, device=device,
