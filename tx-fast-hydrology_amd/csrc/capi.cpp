@@ -177,8 +177,39 @@ struct Net {
     int64_t patience = mcr::kFlowPatience;   // dataflow waits (mc_set_flow_patience)
     int64_t reroutes = 0;            // horizons re-routed after a give-up (mc_net_reroutes)
 
-    // outputs of the last run are the {o, i} pairs of a member-dataflow step (Qm + nslots * E)
+    // outputs of the last run are the {o, i} pairs of a member-dataflow step (IOb, member windows)
     bool out_io = false;
+    // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
+    DBuf<int64_t> mwbase;
+    int64_t mw_E = 0, mw_cells = 0;
+    DBuf<double> IOb;                // staged {o, i} pairs, 2 doubles per member-window cell
+    // tick-major staging pays for large ensembles (EnKF256 member step 2.02 -> 0.85 ms, its
+    // staging kernels 0.73 -> 1.50 ms); small ones keep member-major cells (EnKF32 per horizon
+    // 25.2 ms member-major vs 27.4 tick-major)
+    static constexpr int64_t kSkewMembers = 128;
+    bool member_skew() const { return E >= kSkewMembers; }
+    mcr::MemberWin member_win() const {
+        return mcr::MemberWin{mwbase.p, G.p, wg_gmin.p, flags.p, (int64_t)row_width(),
+                              plan.nslots, member_skew()};
+    }
+    void ensure_member_windows() {
+        if (mw_E == E) return;
+        if (!member_skew()) {
+            mw_E = E;
+            mw_cells = plan.nslots * E;
+            return;
+        }
+        std::vector<int64_t> wb(std::max<int32_t>(plan.nwg, 1), 0);
+        int64_t total = 0;
+        for (int32_t w = 0; w < plan.nwg; ++w) {
+            wb[w] = total;
+            total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + E) * row_width();
+        }
+        mwbase.upload(wb.data(), wb.size(), stream);
+        sync();
+        mw_E = E;
+        mw_cells = total;
+    }
 
     // launch trace (mc_set_trace)
     bool trace = false;
@@ -783,12 +814,17 @@ struct Net {
                     epoch = 0;
                 }
                 ++epoch;
-                Qm.reserve((size_t)(plan.nslots * E * 3));     // IO [E][nslots][2] + Qm [E][nslots]
-                double* IOp = Qm.p + plan.nslots * E;
+                ensure_member_windows();
+                Qm.reserve((size_t)std::max<int64_t>(mw_cells, 1));
+                IOb.reserve((size_t)std::max<int64_t>(2 * mw_cells, 2));
+                double* IOp = IOb.p;
+                const mcr::MemberWin mw = member_win();
                 HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
-                                               st_i.p, IOp, Qm.p, E, stream));
+                                               st_i.p, IOp, Qm.p, E, mw, stream));
                 a.Qm = Qm.p;
                 a.IO = IOp;
+                a.wbase = mwbase.p;          // member windows (the launch stores no output rows)
+                a.mskew = member_skew() ? 1 : 0;
                 a.T = (int32_t)E;
                 a.XG = XG.p;
                 a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
@@ -807,8 +843,7 @@ struct Net {
                 HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, plan.p.chain, flds,
                                               stream));
                 if (timing) HIPC(hipEventRecord(events[1], stream));
-                HIPC(mcr::launch_member_unpack(IOp, flags.p, st_o.p, st_i.p, plan.nslots, E,
-                                               stream));
+                HIPC(mcr::launch_member_unpack(IOp, mw, st_o.p, st_i.p, plan.nslots, E, stream));
                 out_io = true;             // the step's outputs stay in IO (fetch)
                 ++flow_runs;
                 last_flow.valid = false;       // member runs update the state in place
@@ -969,8 +1004,8 @@ struct Net {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
             if (out_io)                    // T = 1: t0 = 0, t1 = 1
-                HIPC(mcr::launch_gather_io(Qm.p + plan.nslots * E, pos.p, c == 1, outT.p, n,
-                                           plan.nslots, E, stream));
+                HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, outT.p, n, E,
+                                           stream));
             else
                 HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p,
                                               in_list.p, c == 1, row_width(), outT.p, n, t0, t1,
@@ -992,8 +1027,8 @@ struct Net {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
             if (out_io)                    // T = 1: [j][0][e] is the step layout
-                HIPC(mcr::launch_gather_io(Qm.p + plan.nslots * E, pos.p, k == 1, outT.p, n,
-                                           plan.nslots, E, stream));
+                HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, k == 1, outT.p, n, E,
+                                           stream));
             else
                 HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p,
                                                in_list.p, k == 1, row_width(), outT.p, n, T_out,

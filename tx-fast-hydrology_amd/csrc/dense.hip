@@ -185,67 +185,44 @@ __device__ __forceinline__ int blk_col(int wave, int lane) {
     return (wave & 1) * 16 + (lane & 15);
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-
-// S = A^-1 of the SPD 32 x 32 block in `a` (LDS, rows of stride kL; its lower part is read)
-// by Gaussian elimination of [A | I] with symmetric pivots: the right part becomes Lu^-1
-// (A = Lu D Lu^T, Lu unit lower), T = D^-1/2 Lu^-1 = L^-1 for the Cholesky factor L, and
-// S = T^T T.  The elimination runs in ONE wave without barriers: lane l holds row l & 31 of A
-// (lanes 0-31) or of the identity / T (lanes 32-63) in registers.  At pivot j the A rows need
-// the pivot row's entries c > j and the T rows its entries c <= j (the others are zero or no
-// longer read), so every column takes ONE uniform scalar read of the pivot lane (readlane);
-// only the multipliers of the T rows cross the halves (one swap per pivot).  (A 256-thread
-// LDS form with a barrier per pivot took ~20 us per block, cross-lane permutes ~18 us.)
-// t: LDS scratch for T.  Returns the 1-based index of the first non-positive pivot (0 =
-// positive definite); all 256 threads call it.
-__device__ __forceinline__ int block_inverse(const double* a, double* t, double* s) {
-    __shared__ int bad_sh;
+// S = A^-1 of the SPD 32 x 32 block in `a` (LDS, rows of stride kL, lower part used; it is
+// overwritten), by Gaussian elimination of [A | I] with symmetric pivots: the right part becomes
+// Lu^-1 (A = Lu D Lu^T, Lu unit lower), T = D^-1/2 Lu^-1 = L^-1 for the Cholesky factor L, and
+// S = T^T T.  t: LDS scratch.  Returns the 1-based index of the first non-positive pivot (0 =
+// positive definite); all 256 threads call it.  One barrier per pivot: the 32 pivots are the
+// critical path of every elimination step (measured per block, MI355X, in ldl_first: this form
+// ~18 us; one wave holding the rows in registers with cross-lane permutes ~21 us, with scalar
+// reads of the pivot lane and a runtime pivot loop ~43 us -- the pivot chain is latency-bound
+// either way).
+__device__ __forceinline__ int block_inverse(double* a, double* t, double* s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (wave == 0) {
-        const int row = lane & 31;
-        const bool up = lane >= 32;
-        double r[kB];
-#pragma unroll
-        for (int c = 0; c < kB; ++c) {
-            const double v = row >= c ? a[row * kL + c] : a[c * kL + row];   // symmetric
-            r[c] = up ? (row == c ? 1.0 : 0.0) : v;
-        }
-        int bad = 0;
-        double mydiag = 1.0;
-        // runtime pivot loop (a fully unrolled 32 x 32 body sends the compiler's scheduler into
-        // tens of minutes); the pivot column is picked from the registers by a select chain
-#pragma unroll 1
-        for (int j = 0; j < kB; ++j) {
-            double rj = r[0];
-#pragma unroll
-            for (int c = 1; c < kB; ++c) rj = j == c ? r[c] : rj;
-            const double d = readlane_f64(rj, j);               // pivot of the Schur complement
-            if (!(d > 0.0) && bad == 0) bad = j + 1;
-            if (row == j) mydiag = d;
-            const double aj = __shfl_xor(rj, 32);               // T lanes: A[row][j]
-            const double m = row > j ? (up ? aj : rj) / d : 0.0;
-            const double mlo = up ? 0.0 : m, mup = up ? m : 0.0;
-#pragma unroll
-            for (int c = 0; c < kB; ++c) {
-                const bool a_part = c > j;                      // A rows: pivot row entries c > j
-                const double mm = a_part ? mlo : mup;           // T rows: entries c <= j
-                r[c] = r[c] - mm * readlane_f64(r[c], a_part ? j : j + 32);
-            }
-        }
-        if (up) {
-            const double sc = 1.0 / sqrt(mydiag);
-#pragma unroll
-            for (int c = 0; c < kB; ++c) t[row * kL + c] = c <= row ? r[c] * sc : 0.0;
-        }
-        if (lane == 0) bad_sh = bad;
+    for (int x = tid; x < kB * kB; x += 256) {
+        const int i = x / kB, c = x % kB;
+        t[i * kL + c] = i == c ? 1.0 : 0.0;
     }
     __syncthreads();
-    const int bad = bad_sh;
+    int bad = 0;
+    for (int j = 0; j < kB; ++j) {
+        const double d = a[j * kL + j];
+        if (!(d > 0.0)) {          // same value in every thread: a uniform exit
+            bad = j + 1;
+            break;
+        }
+        const double invd = 1.0 / d;
+        for (int x = tid; x < (kB - 1 - j) * kB; x += 256) {
+            const int i = j + 1 + x / kB, c = x % kB;
+            const double m = a[i * kL + j] * invd;
+            if (c <= j) t[i * kL + c] = t[i * kL + c] - m * t[j * kL + c];
+            else if (c <= i) a[i * kL + c] = a[i * kL + c] - m * a[c * kL + j];
+        }
+        __syncthreads();
+    }
     if (bad) return bad;
+    for (int x = tid; x < kB * kB; x += 256) {    // rows of Lu^-1 scaled by D^-1/2
+        const int i = x / kB, c = x % kB;
+        t[i * kL + c] = c <= i ? t[i * kL + c] / sqrt(a[i * kL + i]) : 0.0;
+    }
+    __syncthreads();
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     acc = mma32([&](int i, int k) { return t[k * kL + i]; },
                 [&](int k, int j) { return t[k * kL + j]; }, acc, wave, lane);

@@ -306,22 +306,37 @@ void wavefront_flow(WaveArgs a) {
     int64_t bar_cyc = 0;     // MCR_EXP_BARRIER_CLOCK: shader cycles this lane spent in tick barriers
     if constexpr (MEMB) {
         // ---- member dataflow: tick k runs member e = k - G of each slot.  Per-member inputs
-        // (state, lateral inflow) are prefetched kRing ticks ahead into a register ring.
-        const int E = T;
+        // (state, lateral inflow) are prefetched kRing ticks ahead into a register ring.  Large
+        // ensembles stage them TICK-major in the workgroup's member window
+        // (launch_member_inputs, a.mskew): the (slot, member) processed at tick k is in row
+        // k - gmin, so every load and store of a tick is one contiguous row per wave; member-
+        // major staging ([E][nslots]) scatters a wave's 64 lanes over ~19 member rows (lanes
+        // rarely share G) but is cheaper to stage, which wins for small ensembles.
+        const double* __restrict__ Qm = a.Qm;
+        double2* __restrict__ IO = reinterpret_cast<double2*>(const_cast<double*>(a.IO));
+        const bool skew = a.mskew != 0;
+        const int64_t mwb = skew ? a.wbase[w] : 0;      // member window of this workgroup
+        const int rows = wend - gminw;                  // its rows: ticks gmin .. gmax + E - 1
         const int64_t mS = a.mS;
         constexpr int kRing = 4;
         static_assert(kChunk % kRing == 0, "ring slots must be static in the unrolled chunk");
-        const double* __restrict__ Qm = a.Qm;
-        double2* __restrict__ IO = reinterpret_cast<double2*>(const_cast<double*>(a.IO));
+        auto cell = [&](int k, int p) -> int64_t {      // staging cell of tick k (clamped)
+            if (skew) {
+                int r = k - gminw;
+                r = r < 0 ? 0 : (r >= rows ? rows - 1 : r);
+                return mwb + (int64_t)r * RS + p * SLOTS + lid;
+            }
+            int e = k - S[p].G;
+            e = e < 0 ? 0 : (e >= T ? T - 1 : e);
+            return (int64_t)e * mS + S[p].d;
+        };
         double2 rIO[K][kRing];
         double rQ[K][kRing];
 #pragma unroll
         for (int r = 0; r < kRing; ++r)
 #pragma unroll
             for (int p = 0; p < K; ++p) {
-                int e = kb + r - S[p].G;
-                e = e < 0 ? 0 : (e >= E ? E - 1 : e);
-                const int64_t pa = (int64_t)e * mS + S[p].d;
+                const int64_t pa = cell(kb + r, p);
                 rIO[p][r] = IO[pa];
                 rQ[p][r] = Qm[pa];
             }
@@ -362,9 +377,7 @@ void wavefront_flow(WaveArgs a) {
                     *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
 #pragma unroll
                 for (int p = 0; p < K; ++p) {   // refill this ring slot with tick k + kRing
-                    int f = k + kRing - S[p].G;
-                    f = f < 0 ? 0 : (f >= E ? E - 1 : f);
-                    const int64_t pa = (int64_t)f * mS + S[p].d;
+                    const int64_t pa = cell(k + kRing, p);
                     rIO[p][r] = IO[pa];
                     rQ[p][r] = Qm[pa];
                 }
@@ -373,10 +386,8 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     const int e = k - S[p].G;
-                    const bool act = (unsigned)e < (unsigned)E;
-                    if (act)
-                        IO[(int64_t)e * mS + S[p].d] =
-                            make_double2(ov[p], Iv[p]);
+                    const bool act = (unsigned)e < (unsigned)T;
+                    if (act) IO[cell(k, p)] = make_double2(ov[p], Iv[p]);
                     if (S[p].xsrc && act) {
                         const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
                         const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
@@ -583,25 +594,34 @@ hipError_t occupancy_of(const void* fn, int slots, size_t lds, int* blocks_per_c
     return hipSuccess;
 }
 
-// IO[e][d] = {o, i} of the session state, Qm[e][d] = the lateral inflow of member e at the step
-// (same expression as the tick loop)
+// staging cell of (slot d, member e) in the tick-major member windows (kernels.hpp MemberWin)
+__device__ __forceinline__ int64_t member_cell(const MemberWin& mw, int64_t d, int64_t e) {
+    if (!mw.skew) return e * mw.ns + d;
+    const int64_t w = d / mw.rs;
+    return mw.wbase[w] + (mw.G[d] + e - mw.gmin[w]) * mw.rs + (d - w * mw.rs);
+}
+
+// IO = {o, i} of the session state, Qm = the lateral inflow of member e at the step (same
+// expression as the tick loop), both at the tick-major cell of (d, e); padding slots skipped
 __global__ void member_inputs(const double* __restrict__ F, int64_t mF, int64_t ns, int n_rows,
                               int4 ent, const double* __restrict__ st_o,
                               const double* __restrict__ st_i, double2* __restrict__ IO,
-                              double* __restrict__ Qm, int64_t cnt) {
+                              double* __restrict__ Qm, int64_t cnt, MemberWin mw) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= cnt) return;
     const int64_t e = idx / ns, d = idx - e * ns;
-    IO[idx] = make_double2(st_o[idx], st_i[idx]);
+    if (mw.flags[d] == kSlotPad) return;
+    const int64_t c = member_cell(mw, d, e);
+    IO[c] = make_double2(st_o[idx], st_i[idx]);
     const double* Fe = F + e * mF;
     const double lo = Fe[(int64_t)clamp_row(ent.x, n_rows) * ns + d];
     if (ent.y < 0) {
-        Qm[idx] = lo;
+        Qm[c] = lo;
         return;
     }
     const double hi = Fe[(int64_t)clamp_row(ent.y, n_rows) * ns + d];
     const double f = __hiloint2double(ent.w, ent.z);
-    Qm[idx] = (1.0 - f) * lo + f * hi;
+    Qm[c] = (1.0 - f) * lo + f * hi;
 }
 
 }  // namespace
@@ -635,14 +655,13 @@ hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain
 // After a member-dataflow step: the session state from the IO pairs.  The IO pairs themselves
 // stay the step's outputs (o, and the inflow fold i) until the next run: the fetches read them
 // there (launch_gather_io) instead of scattering them into the T = 1 output windows.
-__global__ void member_unpack(const double2* __restrict__ IO, const uint8_t* __restrict__ flags,
-                              double* __restrict__ st_o, double* __restrict__ st_i, int64_t ns,
-                              int64_t cnt) {
+__global__ void member_unpack(const double2* __restrict__ IO, double* __restrict__ st_o,
+                              double* __restrict__ st_i, int64_t ns, int64_t cnt, MemberWin mw) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= cnt) return;
-    const int64_t d = idx % ns;
-    if (flags[d] == kSlotPad) return;
-    const double2 v = IO[idx];
+    const int64_t e = idx / ns, d = idx - e * ns;
+    if (mw.flags[d] == kSlotPad) return;
+    const double2 v = IO[member_cell(mw, d, e)];
     st_o[idx] = v.x;
     st_i[idx] = v.y;
 }
@@ -650,39 +669,39 @@ __global__ void member_unpack(const double2* __restrict__ IO, const uint8_t* __r
 // out[j][e] = IO[e][pos[j]].x (outflow) or .y (inflow): the outputs of a member-dataflow step in
 // caller order, member innermost
 __global__ void gather_io(const double2* __restrict__ IO, const int64_t* __restrict__ pos,
-                          bool inflow, double* __restrict__ out, int64_t n, int64_t ns,
-                          int64_t E) {
+                          bool inflow, double* __restrict__ out, int64_t n, int64_t E,
+                          MemberWin mw) {
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= n * E) return;
     const int64_t j = x / E, e = x - j * E;
-    const double2 v = IO[e * ns + pos[j]];
+    const double2 v = IO[member_cell(mw, pos[j], e)];
     out[x] = inflow ? v.y : v.x;
 }
 
-hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, double* st_o,
+hipError_t launch_member_unpack(const double* IO, const MemberWin& mw, double* st_o,
                                 double* st_i, int64_t ns, int64_t E, hipStream_t s) {
     const int64_t cnt = ns * E;
     if (cnt == 0) return hipSuccess;
     hipLaunchKernelGGL(member_unpack, dim3((unsigned)((cnt + 255) / 256)), 256, 0, s,
-                       reinterpret_cast<const double2*>(IO), flags, st_o, st_i, ns, cnt);
+                       reinterpret_cast<const double2*>(IO), st_o, st_i, ns, cnt, mw);
     return hipGetLastError();
 }
 
-hipError_t launch_gather_io(const double* IO, const int64_t* pos, bool inflow, double* out,
-                            int64_t n, int64_t ns, int64_t E, hipStream_t s) {
+hipError_t launch_gather_io(const double* IO, const MemberWin& mw, const int64_t* pos,
+                            bool inflow, double* out, int64_t n, int64_t E, hipStream_t s) {
     if (n * E == 0) return hipSuccess;
     hipLaunchKernelGGL(gather_io, dim3((unsigned)((n * E + 255) / 256)), 256, 0, s,
-                       reinterpret_cast<const double2*>(IO), pos, inflow, out, n, ns, E);
+                       reinterpret_cast<const double2*>(IO), pos, inflow, out, n, E, mw);
     return hipGetLastError();
 }
 
 hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_rows, int4 ent,
                                 const double* st_o, const double* st_i, double* IO, double* Qm,
-                                int64_t E, hipStream_t s) {
+                                int64_t E, const MemberWin& mw, hipStream_t s) {
     const int64_t cnt = ns * E;
     if (cnt == 0) return hipSuccess;
     hipLaunchKernelGGL(member_inputs, dim3((unsigned)((cnt + 255) / 256)), 256, 0, s, F, mF, ns,
-                       n_rows, ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, cnt);
+                       n_rows, ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, cnt, mw);
     return hipGetLastError();
 }
 

@@ -93,7 +93,8 @@ struct WaveArgs {
     int32_t* status;              // set to 1 when a wait gave up
     int64_t patience;             // wall-clock (100 MHz) ticks a wait polls before giving up
     const double* Qm;             // member dataflow: lateral inflow [E][nslots] of the step
-    const double* IO;             // member dataflow: state {o, i} [E][nslots][2]
+    const double* IO;             // member dataflow: state {o, i} (staging cells, MemberWin)
+    int32_t mskew;                // member dataflow: tick-major member windows (in wbase)
     int64_t nslots;
     int32_t n_rows;
     int32_t T;
@@ -140,19 +141,33 @@ hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds_bytes, in
 hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain,
                                size_t lds_bytes, hipStream_t s);
 hipError_t flow_members_occupancy(int slots, int chain, size_t lds_bytes, int* blocks_per_cu);
-// Inputs of a member-dataflow step, member-major [E][nslots]: IO = {o, i} of the session state
-// (16 B per slot, one load per slot and tick) and Qm = the step's interpolated lateral inflow of
-// the member (the kernels' formula: (1 - frac) F[e][lo][d] + frac F[e][hi][d]).
+// Tick-major member windows of a member-dataflow step: workgroup w stages the (slot d, member
+// e) it processes at tick k = G[d] + e in row k - gmin[w] of its window, wbase[w] + row * rs +
+// (d - w rs) (rs = chain * slots node slots per row; rows gmin[w] .. gmax[w] + E - 1), so every
+// load and store of a tick in the member kernel is one contiguous row.
+// skew = false: member-major cells e * ns + d instead (small ensembles).
+struct MemberWin {
+    const int64_t* wbase;      // [nwg] window base (cells)
+    const int32_t* G;          // [nslots]
+    const int32_t* gmin;       // [nwg]
+    const uint8_t* flags;      // [nslots] (padding slots are not staged)
+    int64_t rs;
+    int64_t ns;
+    bool skew;
+};
+// Inputs of a member-dataflow step at the member-window cells: IO = {o, i} of the session
+// state (16 B per cell, one load per slot and tick) and Qm = the step's interpolated lateral
+// inflow of the member (the kernels' formula: (1 - frac) F[e][lo][d] + frac F[e][hi][d]).
 hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t nslots, int n_rows,
                                 int4 ent, const double* st_o, const double* st_i, double* IO,
-                                double* Qm, int64_t E, hipStream_t s);
+                                double* Qm, int64_t E, const MemberWin& mw, hipStream_t s);
 // After a member-dataflow step (which leaves each member's new {o, i} in IO): the session state
 // st_o / st_i.  IO keeps the step's outputs until the next run; launch_gather_io reads them in
 // caller order (out[j][e], the outflow or the inflow).
-hipError_t launch_member_unpack(const double* IO, const uint8_t* flags, double* st_o,
+hipError_t launch_member_unpack(const double* IO, const MemberWin& mw, double* st_o,
                                 double* st_i, int64_t nslots, int64_t E, hipStream_t s);
-hipError_t launch_gather_io(const double* IO, const int64_t* pos, bool inflow, double* out,
-                            int64_t n, int64_t nslots, int64_t E, hipStream_t s);
+hipError_t launch_gather_io(const double* IO, const MemberWin& mw, const int64_t* pos,
+                            bool inflow, double* out, int64_t n, int64_t E, hipStream_t s);
 // Session state after a one-step run from its step-0 outputs:
 // st_o[e][pos[j]] = O, st_i[e][pos[j]] = the inflow fold of j (as the output gathers compute it)
 hipError_t launch_state_from_step(const double* O, int64_t mO, const int64_t* jbase,
