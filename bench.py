@@ -13,7 +13,8 @@ Workloads (BASELINE.json configs, SURVEY §8d synthetic generators):
     value = reach·member·timesteps of the whole ensemble / max-over-ranks time.  The replicated
     deterministic run (every rank its own Texas replica, no collective, "weak") is measured
     after it and reported in the same line under "det_replicas".
-  * --members 64 (configs[2]), --conus (configs[4], one GPU's 16-member share), --enkf,
+  * --huc8 (configs[0]: one ~1k-reach HUC-8 sub-basin, deterministic, the reference's CPU
+    path; its cpu_baseline is that path's serial loop), --members 64 (configs[2]), --conus (configs[4], one GPU's 16-member share), --enkf,
     --det (N > 1: the replicated deterministic line as the headline).
 
 `--gpus N` without a launcher starts `torch.distributed.run --nproc-per-node N` on this script
@@ -87,6 +88,9 @@ def parse(argv=None, world=None):
                     help="BASELINE configs[4]: CONUS NWM-scale synthetic network (2.7M reaches, "
                          "4000 outlets, deepest path ~7000 reaches); --members per GPU (default "
                          "16: the 128-member ensemble over 8 GPUs, one 16-member shard per rank)")
+    ap.add_argument("--huc8", action="store_true",
+                    help="BASELINE configs[0]: one HUC-8 sub-basin (1000 reaches, one outlet, "
+                         "deepest path ~100 reaches), deterministic")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-api", action="store_true", help="skip the Muskingum.simulate timing")
@@ -98,6 +102,10 @@ def parse(argv=None, world=None):
 
 
 def apply_presets(args, world=1):
+    if args.huc8:
+        args.n, args.basins, args.depth = 1000, 1, 100
+        if args.members is None:
+            args.members = 1                       # configs[0] is deterministic
     if args.conus:
         args.n, args.basins, args.depth = 2_700_000, 4000, 7000
         if args.members is None:
@@ -175,7 +183,10 @@ def build_workload(args, rank=0, world=1):
 
     from tx_fast_hydrology_amd import engine, synthetic
 
-    end = synthetic.river_network(args.n, args.basins, args.depth, np.random.default_rng(0))
+    if getattr(args, "huc8", False):
+        end = synthetic.huc8(seed=0, n=args.n, max_depth=args.depth)
+    else:
+        end = synthetic.river_network(args.n, args.basins, args.depth, np.random.default_rng(0))
     n = end.size
     K, X, o0 = synthetic.model_arrays(n, seed=0)
     start = np.arange(n, dtype=np.int64)
@@ -256,6 +267,9 @@ def workload_name(wl, E):
     if wl.n > 1_000_000:
         return (f"conus-ens (BASELINE configs[4]): CONUS-scale synthetic network ({wl.n} "
                 f"reaches), {E} members per GPU (128 over 8 GPUs), 24 h @ 300 s")
+    if E == 1 and wl.n <= 10_000:
+        return (f"huc8-det (BASELINE configs[0]): one synthetic HUC-8 sub-basin ({wl.n} "
+                f"reaches, one outlet), deterministic, 24 h @ 300 s")
     if E == 1:
         return ("texas-det (BASELINE configs[1]): full-Texas synthetic network, deterministic, "
                 "24 h @ 300 s")

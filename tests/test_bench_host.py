@@ -36,6 +36,19 @@ def test_conus_preset_is_baseline_config_4():
     assert parse("--conus", world=8).members == 16
 
 
+def test_huc8_preset_is_baseline_config_0():
+    a = parse("--huc8")
+    assert (a.n, a.basins, a.depth, a.members) == (1000, 1, 100, 1) and not a.enkf
+    assert parse("--huc8", world=4).members == 1       # deterministic replicas, not the EnKF
+
+
+def test_huc8_network_is_one_sub_basin():
+    from tx_fast_hydrology_amd import synthetic
+    import numpy as np
+    end = synthetic.huc8(seed=0, n=1000, max_depth=100)
+    assert end.size == 1000 and int((end == np.arange(1000)).sum()) == 1
+
+
 def test_launch_plan():
     # no launcher: --gpus N > 1 spawns N ranks as a child, --gpus 1 runs here
     assert bench.launch_plan(8, {}) == ("spawn", 8)

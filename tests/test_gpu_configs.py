@@ -1,6 +1,10 @@
 """GPU parity at the BASELINE.json config shapes, on exactly the workloads bench.py measures
 (bench.build_workload: same synthetic network, plan shape, forcing, members, gauges).
 
+* configs[0] one HUC-8 sub-basin (1000 reaches, one outlet), deterministic, 24 h on the bench
+  plan: every step's outflows and inflows and the final state bit-identical to the oracle.
+* configs[1] full Texas deterministic: tests/test_gpu_routing.py (bit-exact at full size).
+
 * configs[2] Texas, 64 members, 24 h on the bench's ensemble plan (256 lanes, 64-tick
   launches): every member's final state bit-identical to its serial oracle run, and every step
   of 8 sampled members (nutils.py:64-89 per member).
@@ -30,6 +34,21 @@ def _coef(wl):
 
 def _member(a, e):
     return np.ascontiguousarray(a[..., e])
+
+
+def test_config0_huc8_bench_plan():
+    args = bench.parse(["--huc8"], world=1)
+    net, wl = bench.build_workload(args)
+    n, T = wl.n, wl.x.size
+    assert (n, T) == (1000, 288) and int((wl.end == wl.start).sum()) == 1
+    net.run(wl.x)
+    oo, ii = net.fetch_outputs(0, T)
+    so, si = net.get_state()
+    want_o, want_i, fo, fi = orc.simulate(wl.start, wl.end, wl.indeg, *_coef(wl), wl.o0, wl.i0,
+                                          wl.x, wl.xp, wl.fp)
+    assert np.array_equal(oo, want_o) and np.array_equal(ii, want_i)
+    assert np.array_equal(so, fo) and np.array_equal(si, fi)
+    net.close()
 
 
 def test_config2_texas_ens64_bench_plan():

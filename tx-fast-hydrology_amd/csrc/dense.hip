@@ -37,17 +37,21 @@ __device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
 // =============================================================================================
 // slice increments  G[e][d] = sum_f (X[f][d] - xbar[d]) Z[f][e]
 // MFMA rows = members e (A operand = Z^T), columns = slots d (B operand = X), k = member f.
-constexpr int kGM = 128;          // members per tile
+// MW wave rows of 64 members x 2 wave columns of 64 slots: a 64 MW x 128 tile, 128 MW threads
+// (launched with MW = 2; MW = 4 reads X once at Et = 256 but was slower, launcher).
 constexpr int kGN = 128;          // slots per tile
 constexpr int kGK = 16;           // K slice
-constexpr int kGStage = kGK * (kGM + kGN);   // doubles per LDS stage
+template <int MW>
+constexpr int slice_stage() { return kGK * (64 * MW + kGN); }   // doubles per LDS stage
 
-__global__ __launch_bounds__(256, 2) void slice_increments(const double* __restrict__ X,
-                                                           const double* __restrict__ Z,
-                                                           int64_t ldz,
-                                                           double* __restrict__ G, int64_t S,
-                                                           int Et, int n_slot_tiles,
-                                                           int n_member_tiles) {
+template <int MW>
+__global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
+        const double* __restrict__ X, const double* __restrict__ Z, int64_t ldz,
+        double* __restrict__ G, int64_t S, int Et, int n_slot_tiles, int n_member_tiles) {
+    constexpr int kGM = 64 * MW;           // members per tile
+    constexpr int XF = 2 * MW;             // X rows (f) staged per pass
+    constexpr int NXP = kGK / XF;          // X passes per K slice
+    constexpr int kStage = slice_stage<MW>();
     extern __shared__ __attribute__((aligned(16))) double sm[];
     // XCD-aware tile order: the member tiles of one slot tile share its X rows; consecutive
     // workgroups go to consecutive XCDs, so blocks b, b + 8, ... (same XCD) take them
@@ -62,14 +66,14 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
 
-    // global -> register staging of one K slice: Z^T (128 members x 16 f) and X (16 f x 128 d)
-    // Z: thread -> member e = tid >> 1, f pairs (tid & 1) * 8 + 2 p (p < 4)
-    // X: thread -> f = (tid >> 6) + 4 p, slot pair 2 (tid & 63)
+    // global -> register staging of one K slice: Z^T (kGM members x 16 f) and X (16 f x 128 d)
+    // Z: thread -> member e = tid >> 1, f = (tid & 1) * 8 + p (p < 8)
+    // X: thread -> f = (tid >> 6) + XF p (p < NXP), slot pair 2 (tid & 63)
     const int ze = tid >> 1, zf = (tid & 1) * 8;
     const int xf = tid >> 6, xd = 2 * (tid & 63);
     const bool zrow = e0 + ze < Et;
     const int64_t gd = d0 + xd;
-    double rz[8], rx[8];
+    double rz[8], rx[2 * NXP];
     double zsum = 0.0, xs0 = 0.0, xs1 = 0.0;     // partial sums for zs[e] and the mean of X
     auto load = [&](int f0) {
 #pragma unroll
@@ -78,8 +82,8 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
             rz[p] = (zrow && f < Et) ? Z[f + (int64_t)(e0 + ze) * ldz] : 0.0;
         }
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int f = f0 + xf + 4 * p;
+        for (int p = 0; p < NXP; ++p) {
+            const int f = f0 + xf + XF * p;
             const double* src = X + (int64_t)f * S + gd;
             const bool okf = f < Et;
             rx[2 * p] = (okf && gd < S) ? src[0] : 0.0;
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
         }
     };
     auto stage = [&](int buf) {
-        double* As = sm + buf * kGStage;          // As[f][e]
+        double* As = sm + buf * kStage;           // As[f][e]
         double* Bs = As + kGK * kGM;              // Bs[f][d]
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
@@ -95,8 +99,8 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
             zsum += rz[p];
         }
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int f = xf + 4 * p;
+        for (int p = 0; p < NXP; ++p) {
+            const int f = xf + XF * p;
             *reinterpret_cast<double2*>(Bs + f * kGN + xd) = make_double2(rx[2 * p], rx[2 * p + 1]);
             xs0 += rx[2 * p];
             xs1 += rx[2 * p + 1];
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
     for (int f0 = 0; f0 < Et; f0 += kGK) {
         const bool more = f0 + kGK < Et;
         if (more) load(f0 + kGK);                 // next slice in flight during the MFMAs
-        const double* As = sm + buf * kGStage;
+        const double* As = sm + buf * kStage;
         const double* Bs = As + kGK * kGM;
 #pragma unroll
         for (int kk = 0; kk < kGK; kk += 4) {
@@ -135,19 +139,22 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
         __syncthreads();
         buf ^= 1;
     }
-    // member sums of X (4 partials per slot pair) and column sums of Z (2 partials per member)
+    // member sums of X (XF partials per slot pair) and column sums of Z (2 partials per member)
     double* red = sm;                              // the K loop is over: reuse stage 0
     red[xf * kGN + xd] = xs0;
     red[xf * kGN + xd + 1] = xs1;
     const double zs_all = zsum + __shfl_xor(zsum, 1);
-    if ((tid & 1) == 0) red[4 * kGN + ze] = zs_all;
+    if ((tid & 1) == 0) red[XF * kGN + ze] = zs_all;
     __syncthreads();
     const double inv = 1.0 / (double)Et;
     // C/D of f64 16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int dl = wc + 16 * j + (lane & 15);
-        const double xbar = (((red[dl] + red[kGN + dl]) + red[2 * kGN + dl]) + red[3 * kGN + dl]) * inv;
+        double xsum = red[dl];
+#pragma unroll
+        for (int q = 1; q < XF; ++q) xsum += red[q * kGN + dl];
+        const double xbar = xsum * inv;
         const int64_t d = d0 + dl;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256, 2) void slice_increments(const double* __restr
             for (int r = 0; r < 4; ++r) {
                 const int el = wr + 16 * i + (lane >> 4) + 4 * r;
                 const int e = e0 + el;
-                if (e < Et && d < S) G[(int64_t)e * S + d] = acc[i][j][r] - red[4 * kGN + el] * xbar;
+                if (e < Et && d < S) G[(int64_t)e * S + d] = acc[i][j][r] - red[XF * kGN + el] * xbar;
             }
     }
 }
@@ -406,14 +413,17 @@ hipError_t launch_slice_increments(const double* X, const double* Z, int64_t ldz
                                    int64_t S, int64_t Et, hipStream_t s) {
     if (S <= 0) return hipSuccess;
     if (Et < 2 || Et > (1 << 20)) return hipErrorInvalidValue;
+    // 128-member tiles at every Et: 256-member tiles (slice_increments<4>, X read once at
+    // Et = 256) measured 559 vs 528 us per EnKF256 analysis (profiles/r03i_*)
+    constexpr int MW = 2;
+    constexpr int kGM = 64 * MW;
     const int64_t nst = (S + kGN - 1) / kGN;
     const int nmt = (int)((Et + kGM - 1) / kGM);
-    const int64_t groups = (nst + 7) / 8;
-    const int64_t grid = groups * 8 * nmt;
+    const int64_t grid = (nst + 7) / 8 * 8 * nmt;
     if (grid > 0x7fffffff || nst > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t lds = 2 * kGStage * sizeof(double);
-    hipLaunchKernelGGL(slice_increments, dim3((unsigned)grid), 256, lds, s, X, Z, ldz, G, S,
-                       (int)Et, (int)nst, nmt);
+    hipLaunchKernelGGL(slice_increments<MW>, dim3((unsigned)grid), 128 * MW,
+                       2 * slice_stage<MW>() * sizeof(double), s, X, Z, ldz, G, S, (int)Et,
+                       (int)nst, nmt);
     return hipGetLastError();
 }
 
