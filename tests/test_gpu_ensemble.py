@@ -33,13 +33,17 @@ def _case(n, basins, depth, seed, E, rows=7):
     return end, start, indeg, coef, xp, fpe, o0, i0
 
 
-@pytest.mark.parametrize("n,E,slots,T", [(3000, 5, 256, 60), (1200, 64, 128, 25),
-                                         (5000, 3, 448, 100)])
-def test_ensemble_members_bitexact(n, E, slots, T):
+@pytest.mark.parametrize("n,E,slots,T,chain", [(3000, 5, 256, 60, 0), (1200, 64, 128, 25, 0),
+                                               (5000, 3, 448, 100, 0), (1500, 4, 64, 40, 1),
+                                               (1500, 4, 64, 40, 3)])
+def test_ensemble_members_bitexact(n, E, slots, T, chain):
+    """Every member bit-identical to its serial oracle run on the multi-launch path (workgroup
+    output rows, kernels.hpp), including one-segment workgroups (64 lanes x 1 position) and odd
+    segment counts (64 lanes x 3 positions)."""
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4, 120, n + E, E)
     n = end.size
     x = xp[0] + 300e9 * np.arange(1, T + 1)
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=E)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=E, chain=chain)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
     got_o, got_i = net.simulate(x, xp, fpe)

@@ -94,7 +94,8 @@ def test_run_golden_ynet(golden, kw):
     assert np.array_equal(o, g["o"]) and np.array_equal(i, g["i"])
 
 
-@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=16), dict(slots=512, tile=32)])
+@pytest.mark.parametrize("kw", [{}, dict(slots=64, tile=16), dict(slots=512, tile=32),
+                                dict(slots=64, tile=16, chain=1)])
 def test_run_golden_huc8_every_step(golden, kw):
     g = golden("g2_huc8.npz")
     o, i = _golden_run(g, **kw)

@@ -89,7 +89,7 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, seg_gmin, seg_gmax, xid;
+    DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, xid;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
     DBuf<int64_t> slot_reach, pos;
@@ -102,9 +102,9 @@ struct Net {
     std::vector<double> xp;
     // per-step interpolation table {row_lo, row_hi, frac}
     DBuf<int4> stab;
-    // outputs in segment windows (kernels.hpp), their per-horizon index (window base of each
-    // output segment, step-0 index of each reach), a scratch for fetches and the dummy row of
-    // out-of-window ticks
+    // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
+    // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
+    // and the dummy row of out-of-window ticks
     DBuf<double> O, outT, dummy;
     DBuf<int64_t> in_off, in_list;   // inflow lists (plan.hpp), caller order
     // per-horizon schedules (active workgroups per launch, output windows), cached per T
@@ -113,7 +113,7 @@ struct Net {
         std::vector<int64_t> off;      // launch k runs list[off[k] .. off[k+1])
         std::vector<int32_t> list;
         DBuf<int32_t> active;
-        DBuf<int64_t> sbase, jbase;    // window base per output segment, step-0 cell per reach
+        DBuf<int64_t> wbase, jbase;    // window base per workgroup, step-0 cell per reach
         int64_t Otot = 0;              // output cells of one member
         uint64_t used = 0;
     };
@@ -273,10 +273,6 @@ struct Net {
         }
         wg_gmin.upload(plan.wg_gmin.data(), plan.wg_gmin.size(), stream);
         wg_gmax.upload(plan.wg_gmax.data(), plan.wg_gmax.size(), stream);
-        seg_gmin.upload(plan.seg_gmin.data(), plan.seg_gmin.size(), stream);
-        seg_gmax.upload(plan.seg_gmax.data(), plan.seg_gmax.size(), stream);
-        seg_gmin.reserve(1);
-        seg_gmax.reserve(1);
         for (DBuf<double>* b : {&alpha, &beta, &chi, &gamma, &st_o, &st_i}) {
             b->reserve(ns);
             HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
@@ -710,19 +706,17 @@ struct Net {
             hit->T = T;
             mcr::active_schedule(plan, T, hit->list, hit->off);
             hit->active.upload(hit->list.data(), hit->list.size(), stream);
-            const size_t nseg = plan.seg_gmin.size();
-            std::vector<int64_t> sb(std::max<size_t>(nseg, 1), 0);
+            std::vector<int64_t> wb(plan.nwg);
             int64_t total = 0;
-            for (size_t sg = 0; sg < nseg; ++sg) {
-                sb[sg] = total;
-                total += std::max<int64_t>(0, (int64_t)plan.seg_gmax[sg] - plan.seg_gmin[sg] + T) *
-                         mcr::kOutSegment;
+            for (int32_t w = 0; w < plan.nwg; ++w) {
+                wb[w] = total;
+                total += ((int64_t)plan.wg_gmax[w] - plan.wg_gmin[w] + T) * row_width();
             }
-            hit->sbase.upload(sb.data(), sb.size(), stream);
+            hit->wbase.upload(wb.data(), wb.size(), stream);
             hit->Otot = total;
             hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
-            HIPC(mcr::launch_window_index(pos.p, G.p, seg_gmin.p, hit->sbase.p, plan.n,
-                                          hit->jbase.p, stream));
+            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, row_width(),
+                                          plan.n, hit->jbase.p, stream));
             sync();
         }
         hit->used = ++use_clock;
@@ -789,9 +783,7 @@ struct Net {
         a.stab = stab.p;
         a.wg_gmin = wg_gmin.p;
         a.wg_gmax = wg_gmax.p;
-        a.seg_gmin = seg_gmin.p;
-        a.seg_gmax = seg_gmax.p;
-        a.sbase = cur->sbase.p;
+        a.wbase = cur->wbase.p;
         a.O = O.p;
         a.dummy = dummy.p;
         a.nslots = plan.nslots;
@@ -1016,7 +1008,7 @@ struct Net {
                                            stream));
             else
                 HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p,
-                                              in_list.p, c == 1, mcr::kOutSegment, outT.p, n, t0, t1,
+                                              in_list.p, c == 1, row_width(), outT.p, n, t0, t1,
                                               E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
@@ -1039,7 +1031,7 @@ struct Net {
                                            stream));
             else
                 HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p,
-                                               in_list.p, k == 1, mcr::kOutSegment, outT.p, n, T_out,
+                                               in_list.p, k == 1, row_width(), outT.p, n, T_out,
                                                E, stream));
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             sync();
@@ -1301,7 +1293,7 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         } guard{ev};
         HIPC(hipEventRecord(ev, S->stream));
         HIPC(hipStreamWaitEvent(D->stream, ev, 0));
-        HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, mcr::kOutSegment,
+        HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, S->row_width(),
                                             o_start, alpha, beta, gamma, D->F.p, D->plan.nslots,
                                             D->plan.pos[dst_reach], S->T_out, D->stream));
         HIPC(hipEventRecord(ev, D->stream));

@@ -69,41 +69,57 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
     // global -> register staging of one K slice: Z^T (kGM members x 16 f) and X (16 f x 128 d)
     // Z: thread -> member e = tid >> 1, f = (tid & 1) * 8 + p (p < 8)
     // X: thread -> f = (tid >> 6) + XF p (p < NXP), slot pair 2 (tid & 63)
+    // Two slices are in flight in registers (slice f + 2 loads while slice f's MFMAs run and
+    // slice f + 1 is staged); the loads are unconditional at clamped addresses and masked after
+    // (no branches, so the wait before staging counts only the older slice's loads).
     const int ze = tid >> 1, zf = (tid & 1) * 8;
-    const int xf = tid >> 6, xd = 2 * (tid & 63);
+    const int xf = __builtin_amdgcn_readfirstlane(tid >> 6), xd = 2 * (tid & 63);
     const bool zrow = e0 + ze < Et;
+    const int64_t zcol = zrow ? (int64_t)(e0 + ze) * ldz : 0;
     const int64_t gd = d0 + xd;
-    double rz[8], rx[2 * NXP];
+    struct Slice {
+        double z[8], x[2 * NXP];
+    };
     double zsum = 0.0, xs0 = 0.0, xs1 = 0.0;     // partial sums for zs[e] and the mean of X
-    auto load = [&](int f0) {
+    // buffer loads: an out-of-range offset (or an empty record) reads 0, so the edge masks are
+    // offsets, not branches around the loads
+    const int zrec = (int)(ldz * (int64_t)Et * 8 < 0x7fffffff ? ldz * (int64_t)Et * 8 : 0x7fffffff);
+    const auto zr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Z), (short)0, zrec,
+                                                      0x00020000);
+    auto load = [&](Slice& r, int f0) {
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
             const int f = f0 + zf + p;
-            rz[p] = (zrow && f < Et) ? Z[f + (int64_t)(e0 + ze) * ldz] : 0.0;
+            const bool ok = zrow && f < Et;
+            const unsigned off = ok ? (unsigned)((f + zcol) * 8) : (unsigned)zrec;
+            r.z[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, off, 0, 0));
         }
 #pragma unroll
         for (int p = 0; p < NXP; ++p) {
-            const int f = f0 + xf + XF * p;
-            const double* src = X + (int64_t)f * S + gd;
-            const bool okf = f < Et;
-            rx[2 * p] = (okf && gd < S) ? src[0] : 0.0;
-            rx[2 * p + 1] = (okf && gd + 1 < S) ? src[1] : 0.0;
+            const int f = f0 + xf + XF * p;     // wave-uniform: one X row per wave and pass
+            const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double*>(X + (int64_t)(f < Et ? f : 0) * S), (short)0,
+                f < Et ? (int)(S * 8) : 0, 0x00020000);
+            r.x[2 * p] = __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(xr, (unsigned)(gd * 8), 0, 0));
+            r.x[2 * p + 1] = __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(xr, (unsigned)(gd * 8 + 8), 0, 0));
         }
     };
-    auto stage = [&](int buf) {
+    auto stage = [&](const Slice& r, int buf) {
         double* As = sm + buf * kStage;           // As[f][e]
         double* Bs = As + kGK * kGM;              // Bs[f][d]
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
-            As[(zf + p) * kGM + ze] = rz[p];
-            zsum += rz[p];
+            As[(zf + p) * kGM + ze] = r.z[p];
+            zsum += r.z[p];
         }
 #pragma unroll
         for (int p = 0; p < NXP; ++p) {
             const int f = xf + XF * p;
-            *reinterpret_cast<double2*>(Bs + f * kGN + xd) = make_double2(rx[2 * p], rx[2 * p + 1]);
-            xs0 += rx[2 * p];
-            xs1 += rx[2 * p + 1];
+            *reinterpret_cast<double2*>(Bs + f * kGN + xd) = make_double2(r.x[2 * p], r.x[2 * p + 1]);
+            xs0 += r.x[2 * p];
+            xs1 += r.x[2 * p + 1];
         }
     };
 
@@ -113,13 +129,11 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
 
-    load(0);
-    stage(0);
-    __syncthreads();
-    int buf = 0;
-    for (int f0 = 0; f0 < Et; f0 += kGK) {
-        const bool more = f0 + kGK < Et;
-        if (more) load(f0 + kGK);                 // next slice in flight during the MFMAs
+    // one K slice: slice f0 from LDS buffer `buf`; `next` holds slice f0 + kGK (staged into the
+    // other buffer after the MFMAs), `fut` receives slice f0 + 2 kGK
+    auto step = [&](int f0, int buf, Slice& next, Slice& fut) {
+        load(fut, f0 + 2 * kGK);     // unconditional (past the end: out of range, reads 0), so
+                                     // the wait before the staging below is a count, not 0
         const double* As = sm + buf * kStage;
         const double* Bs = As + kGK * kGM;
 #pragma unroll
@@ -135,9 +149,17 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(a[i], bb[j], acc[i][j]);
         }
-        if (more) stage(buf ^ 1);
+        if (f0 + kGK < Et) stage(next, buf ^ 1);
         __syncthreads();
-        buf ^= 1;
+    };
+    Slice ra, rb;
+    load(ra, 0);
+    stage(ra, 0);
+    __syncthreads();
+    load(ra, kGK);
+    for (int f0 = 0; f0 < Et; f0 += 2 * kGK) {
+        step(f0, 0, ra, rb);
+        if (f0 + kGK < Et) step(f0 + kGK, 1, rb, ra);
     }
     // member sums of X (XF partials per slot pair) and column sums of Z (2 partials per member)
     double* red = sm;                              // the K loop is over: reuse stage 0
@@ -413,6 +435,7 @@ hipError_t launch_slice_increments(const double* X, const double* Z, int64_t ldz
                                    int64_t S, int64_t Et, hipStream_t s) {
     if (S <= 0) return hipSuccess;
     if (Et < 2 || Et > (1 << 20)) return hipErrorInvalidValue;
+    if (S * 8 >= 0x7fffffff) return hipErrorInvalidValue;   // one X row per buffer record
     // 128-member tiles at every Et: 256-member tiles (slice_increments<4>, X read once at
     // Et = 256) measured 559 vs 528 us per EnKF256 analysis (profiles/r03i_*)
     constexpr int MW = 2;

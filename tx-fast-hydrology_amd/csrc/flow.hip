@@ -223,35 +223,18 @@ void wavefront_flow(WaveArgs a) {
                  a.patience, false};
         const int nb = (h.nitems + kBatchItems - 1) / kBatchItems;   // <= 2 (host-checked)
         // the outputs of tick k (plane k & 7, written by the compute waves before the barrier
-        // that ends tick k, overwritten at tick k + 8) -> row k of each output segment's window
-        // (kernels.hpp) whose reaches run at tick k, 16 bytes per lane: lanes 0-31 store
-        // segment 2j, lanes 32-63 segment 2j + 1.  The compute waves issue no output stores.
+        // that ends tick k, overwritten at tick k + 8) -> row k of the workgroup's output window,
+        // 16 bytes per lane: the compute waves' tick loop issues no output stores
         const int hl = tid & 63;
-        constexpr int kSegs = RS / kOutSegment;
-        constexpr int kPairs = (kSegs + 1) / 2;
-        const int hs = hl >> 5;                         // segment parity of this lane
-        const int hc = (hl & 31) * 2;                   // first of its two columns
-        int hg0[kPairs], hg1[kPairs];
-        int64_t hgb[kPairs];
-#pragma unroll
-        for (int j = 0; j < kPairs; ++j) {
-            const int sj = 2 * j + hs < kSegs ? 2 * j + hs : kSegs - 1;
-            const int64_t sg = (int64_t)w * kSegs + sj;
-            hg0[j] = 2 * j + hs < kSegs ? a.seg_gmin[sg] : kNoSegment;
-            hg1[j] = a.seg_gmax[sg] + T;
-            hgb[j] = a.sbase[sg];
-        }
+        const int64_t wbh = a.wbase[w];
         auto copy_row = [&](int k) {
             if (MEMB || MCR_EXP_NO_STORES || k < gminw || k >= wend) return;   // wave-uniform
             const char* src = lds + XB + (unsigned)(k & 7) * PL;
+            double* dst = a.O + wbh + (int64_t)(k - gminw) * RS;
 #pragma unroll
-            for (int j = 0; j < kPairs; ++j)
-                if (k >= hg0[j] && k < hg1[j])
-                    __builtin_nontemporal_store(
-                        *reinterpret_cast<const f64x2*>(
-                            src + (unsigned)((2 * j + hs) * kOutSegment + hc) * 8u),
-                        reinterpret_cast<f64x2*>(a.O + hgb[j] + (int64_t)(k - hg0[j]) * kOutSegment +
-                                                 hc));
+            for (int c = 2 * hl; c < RS; c += 128)
+                __builtin_nontemporal_store(*reinterpret_cast<const f64x2*>(src + (unsigned)c * 8u),
+                                            reinterpret_cast<f64x2*>(dst + c));
         };
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();                     // EG staged (LDS) before the helper reads it

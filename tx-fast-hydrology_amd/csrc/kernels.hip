@@ -85,21 +85,15 @@ void wavefront_det(WaveArgs a) {
     const int64_t ns = a.nslots;
     const int nrow = a.n_rows;
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
+    const int64_t wb = a.wbase[w];
 
     // ---- per-slot registers (issued first: longest latency)
     Slot S[K];
     uint64_t up[K];
-    int sg0[K], sg1[K];                                 // output segment window (wave-uniform)
-    int64_t sgb[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + tid, mem, k0, tile, T);
         up[p] = a.up4[S[p].d];
-        const int64_t sg = ((int64_t)w * RS + p * SLOTS) / kOutSegment +
-                           __builtin_amdgcn_readfirstlane(tid) / kOutSegment;
-        sg0[p] = a.seg_gmin[sg];
-        sg1[p] = a.seg_gmax[sg] + T;
-        sgb[p] = a.sbase[sg];
     }
 
     // ---- step-table window of this workgroup -> LDS
@@ -165,6 +159,7 @@ void wavefront_det(WaveArgs a) {
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
+    const int wend = gmaxw + T;                         // end of this workgroup's window
     constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
@@ -261,17 +256,14 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p)
                 *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
-            // one contiguous 64-value row per segment and tick; ticks outside the segment's
-            // window: dummy row
+            // one contiguous row of RS values per tick; ticks outside the window: dummy row
+            const bool inwin = k >= gminw && k < wend;
+            double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
             if (!MCR_EXP_NO_STORES) {
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    const bool inwin = k >= sg0[p] && k < sg1[p];
-                    double* cell = inwin ? Om + sgb[p] + (int64_t)(k - sg0[p]) * kOutSegment +
-                                               (tid & (kOutSegment - 1))
-                                         : dum + p * SLOTS + tid;
                     // non-temporal: rows are written once and read only by later fetches
-                    __builtin_nontemporal_store(ov[p], cell);
+                    __builtin_nontemporal_store(ov[p], orow + p * SLOTS + tid);
                     if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T)
                         XSm[S[p].xs0 + k] = ov[p];
                 }
@@ -366,14 +358,14 @@ __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restri
 }
 
 __global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __restrict__ G,
-                             const int32_t* __restrict__ seg_gmin,
-                             const int64_t* __restrict__ sbase, int64_t n,
+                             const int32_t* __restrict__ wg_gmin,
+                             const int64_t* __restrict__ wbase, int slots, int64_t n,
                              int64_t* __restrict__ jbase) {
     for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
          j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t d = pos[j];
-        const int64_t sg = d / kOutSegment;
-        jbase[j] = sbase[sg] + (int64_t)(G[d] - seg_gmin[sg]) * kOutSegment + (d - sg * kOutSegment);
+        const int64_t w = d / slots;
+        jbase[j] = wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * slots + (d - w * slots);
     }
 }
 
@@ -389,6 +381,7 @@ __device__ __forceinline__ double inflow_at(const double* __restrict__ O,
     return s;
 }
 
+// out[t - t0][j][e]: consecutive threads take consecutive (j, e) (coalesced writes)
 __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
                              const int64_t* __restrict__ jbase,
                              const int64_t* __restrict__ in_off,
@@ -521,11 +514,12 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
     return hipGetLastError();
 }
 
-hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* seg_gmin,
-                               const int64_t* sbase, int64_t n, int64_t* jbase, hipStream_t s) {
+hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
+                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
+                               hipStream_t s) {
     if (n > 0)
-        hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, seg_gmin, sbase, n,
-                           jbase);
+        hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
+                           slots, n, jbase);
     return hipGetLastError();
 }
 

@@ -1,19 +1,17 @@
 // Device-side entry points of the Muskingum routing engine (gfx950).  Launchers are plain host
 // functions so the C-ABI layer (capi.cpp) stays free of kernel syntax.
 //
-// Output layout ("segment windows").  The node slots of a workgroup are cut into segments of
-// kOutSegment = 64 consecutive slots (one wave's lanes of one lane position, plan.hpp); segment
-// s owns the ticks [sgmin[s], sgmax[s] + T) over which its reaches run, and stores them
-// tick-major inside that window:
-//     O[sbase[s] + (tick - sgmin[s]) * 64 + (slot & 63)]
-// so a wave writes one contiguous 512-byte row per tick, and only for the ticks some reach of
-// ITS segment runs (a workgroup-wide row carried the ticks of every other segment too: Texas
-// det 1.26x, ens64 1.36x the outflow bytes, vs 1.12x / 1.14x per segment).  Inflows are not
-// stored: i[j][t] = ((0 + o[u1][t]) + o[u2][t]) + ... over j's inflow list (plan.hpp) is
-// recomputed bit-exactly wherever it is needed (fetches, final state).  A reach that feeds a
+// Output layout ("workgroup windows").  Workgroup w owns the ticks [gmin[w], gmax[w] + T) of the
+// space-time schedule; its outputs are stored tick-major inside that window:
+//     O[wbase[w] + (tick - gmin[w]) * RS + slot - w * RS]      (RS = chain * slots)
+// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  (Per-wave "segment"
+// windows that store only the ticks of a wave's own reaches wrote 10 % (det) / 30 % (ens64)
+// fewer bytes but ran 1-2 % / 4-6 % slower: DESIGN.md §6, round 3.)  Inflows are not stored:
+// i[j][t] = ((0 + o[u1][t]) + o[u2][t]) + ... over j's inflow list (plan.hpp) is recomputed
+// bit-exactly wherever it is needed (fetches, final state).  A reach that feeds a
 // reach of another cluster (an "external input" of the consumer's workgroup) also writes its
 // outflow to a step-contiguous stream XS[e][t], which the consumer reads coalesced.  Step t of
-// the reach in slot d lives at tick G[d] + t, i.e. at  jbase[j] + t * 64  for its caller index j
+// the reach in slot d lives at tick G[d] + t, i.e. at  jbase[j] + t * RS  for its caller index j
 // (jbase is computed per horizon by launch_window_index).
 #pragma once
 
@@ -82,11 +80,9 @@ struct WaveArgs {
     const int4* stab;             // per step {row_lo, row_hi, frac (f64)}; clamped: {r, r, 0}
     const int32_t* wg_gmin;       // [nwg] tick range of each workgroup
     const int32_t* wg_gmax;
-    const int64_t* wbase;         // member dataflow: [nwg] member-window base (MemberWin)
-    const int32_t* seg_gmin;      // [nslots / 64] tick range of each output segment
-    const int32_t* seg_gmax;
-    const int64_t* sbase;         // [nslots / 64] window base of each output segment in O
-    double* O;                    // segment windows of outflows (see above)
+    const int64_t* wbase;         // [nwg] window base of each workgroup in O (member dataflow:
+                                  // of its member window, MemberWin)
+    double* O;                    // workgroup windows of outflows (see above)
     // ensemble members (grid y; multi-launch kernel): element strides between members of the
     // member-major arrays F, O, XS and of st_o / st_i (in slots)
     int64_t mF, mO, mX, mS;
@@ -206,11 +202,12 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
                                    hipStream_t s);
-// jbase[j] = window index of step 0 of caller reach j (segment windows, row stride 64)
-hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* seg_gmin,
-                               const int64_t* sbase, int64_t n, int64_t* jbase, hipStream_t s);
+// jbase[j] = window index of step 0 of caller reach j
+hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
+                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
+                               hipStream_t s);
 // Output gathers (caller order, member innermost).  inflow = false: outflow O; true: the inflow
-// of reach j, summed from O over its inflow list.  `slots` = the window row stride (64).
+// of reach j, summed from O over its inflow list.
 // step-major out[t - t0][j][e] for t in [t0, t1)
 hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase,
                                const int64_t* in_off, const int64_t* in_list, bool inflow,

@@ -564,16 +564,6 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         P.max_span = std::max(P.max_span, P.wg_gmax[w] - P.wg_gmin[w]);
         if ((int64_t)P.wg_gmax[w] - P.wg_gmin[w] > scap) return "internal: workgroup G span";
     }
-    // output segments: the rows a segment stores are the ticks its reaches run (kernels.hpp)
-    const int64_t nseg = P.nslots / kOutSegment;
-    P.seg_gmin.assign(nseg, kNoSegment);
-    P.seg_gmax.assign(nseg, -kNoSegment);
-    for (int64_t d = 0; d < P.nslots; ++d)
-        if (P.flags[d] == kSlotRouted || P.flags[d] == kSlotUnrouted) {
-            const int64_t sg = d / kOutSegment;
-            P.seg_gmin[sg] = std::min(P.seg_gmin[sg], P.G[d]);
-            P.seg_gmax[sg] = std::max(P.seg_gmax[sg], P.G[d]);
-        }
     // input codes and external lists
     P.ext_off.assign(P.nwg + 1, 0);
     std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src node, consumer G)

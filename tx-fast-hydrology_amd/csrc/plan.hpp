@@ -50,9 +50,6 @@ constexpr int64_t kTableEntryBytes = 16;    // {int32 row_lo, int32 row_hi, f64 
 constexpr uint16_t kExtBit = 0x8000;
 // code of a chained input: the output of the lane's previous position in the same tick
 constexpr uint16_t kSelfCode = 0x7fff;
-// output rows are stored per segment of 64 consecutive node slots (kernels.hpp)
-constexpr int kOutSegment = 64;
-constexpr int32_t kNoSegment = 1 << 29;   // gmin of a segment without reaches (gmax = -it)
 constexpr int kUpInline = 4;  // upstream values one lane reads per tick (codes in registers)
 
 enum SlotFlags : uint8_t {
@@ -94,9 +91,6 @@ struct Plan {
 
     // per workgroup
     std::vector<int32_t> wg_gmin, wg_gmax;  // G range of the workgroup's real reaches
-    // per 64-slot output segment (slots 64 s .. 64 s + 63, one wave's lanes of one position):
-    // G range of its reach slots; a segment without reaches has gmin > gmax (no window)
-    std::vector<int32_t> seg_gmin, seg_gmax;
     std::vector<int32_t> ext_off;           // [nwg + 1]
     std::vector<int64_t> ext_src;           // source row: reach index, or n + slot (partial sum)
     std::vector<int32_t> ext_g;             // G of the consuming reach
