@@ -11,8 +11,8 @@
 //    augmented system [A | B]: step J eliminates block column J from every other block row
 //    (A_IC -= A_IJ S_J A_JC, B_I -= A_IJ S_J B_J, S_J = D_J^-1 the inverse of the pivot block),
 //    and a last launch scales B_I := S_I B_I.  Every step is one launch whose workgroups each
-//    update one block; the workgroup that updates the next pivot block inverts it (a Cholesky
-//    of the 32 x 32 block, which also detects a matrix that is not positive definite).  The
+//    update one block; the workgroup that updates the next pivot block inverts it (Gauss-Jordan
+//    on [D | I] in one wave, which also detects a matrix that is not positive definite).  The
 //    sequential chain is k / 32 + 2 launches and no separate substitution passes (a blocked
 //    LDL^T + forward / backward substitution took ~250 us at k = 256: ~20 dependent cross-XCD
 //    round trips).
@@ -214,60 +214,56 @@ __device__ __forceinline__ int blk_col(int wave, int lane) {
     return (wave & 1) * 16 + (lane & 15);
 }
 
-// S = A^-1 of the SPD 32 x 32 block in `a` (LDS, rows of stride kL, lower part used; it is
-// overwritten), by Gaussian elimination of [A | I] with symmetric pivots: the right part becomes
-// Lu^-1 (A = Lu D Lu^T, Lu unit lower), T = D^-1/2 Lu^-1 = L^-1 for the Cholesky factor L, and
-// S = T^T T.  t: LDS scratch.  Returns the 1-based index of the first non-positive pivot (0 =
-// positive definite); all 256 threads call it.  One barrier per pivot: the 32 pivots are the
-// critical path of every elimination step (measured per block, MI355X, in ldl_first: this form
-// ~18 us; one wave holding the rows in registers with cross-lane permutes ~21 us, with scalar
-// reads of the pivot lane and a runtime pivot loop ~43 us -- the pivot chain is latency-bound
-// either way).
-__device__ __forceinline__ int block_inverse(double* a, double* t, double* s) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int x = tid; x < kB * kB; x += 256) {
-        const int i = x / kB, c = x % kB;
-        t[i * kL + c] = i == c ? 1.0 : 0.0;
-    }
-    __syncthreads();
-    int bad = 0;
-    for (int j = 0; j < kB; ++j) {
-        const double d = a[j * kL + j];
-        if (!(d > 0.0)) {          // same value in every thread: a uniform exit
-            bad = j + 1;
-            break;
-        }
-        const double invd = 1.0 / d;
-        for (int x = tid; x < (kB - 1 - j) * kB; x += 256) {
-            const int i = j + 1 + x / kB, c = x % kB;
-            const double m = a[i * kL + j] * invd;
-            if (c <= j) t[i * kL + c] = t[i * kL + c] - m * t[j * kL + c];
-            else if (c <= i) a[i * kL + c] = a[i * kL + c] - m * a[c * kL + j];
-        }
-        __syncthreads();
-    }
-    if (bad) return bad;
-    for (int x = tid; x < kB * kB; x += 256) {    // rows of Lu^-1 scaled by D^-1/2
-        const int i = x / kB, c = x % kB;
-        t[i * kL + c] = c <= i ? t[i * kL + c] / sqrt(a[i * kL + i]) : 0.0;
-    }
-    __syncthreads();
-    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = mma32([&](int i, int k) { return t[k * kL + i]; },
-                [&](int k, int j) { return t[k * kL + j]; }, acc, wave, lane);
+// S = D^-1 for the SPD pivot block D (LDS, row stride kL) by Gauss-Jordan elimination on [D | I]
+// inside ONE wave, without workgroup barriers: lane j holds column j of the 32 x 64 augmented
+// matrix in registers; pivot k's column is broadcast through LDS (written by lane k, read by
+// every lane at one address; LDS operations of one wave complete in order).  S goes to dst
+// column-major (leading dimension kB) from lanes 32..63.  Returns 0, or k + 1 when pivot k is
+// not positive (D not SPD).  Called by wave 0 only; col: 32 doubles of LDS scratch.
+// Measured per EnKF256 elimination step (MI355X): 21.2 us vs 23.7 us for the 256-thread LDS
+// elimination with one barrier per pivot and S = T^T T on MFMA; earlier one-wave forms with
+// cross-lane permutes (~21 us per block) or scalar reads of the pivot lane in a runtime loop
+// (~43 us) were no faster -- the 32-pivot chain is latency-bound in every form.
+__device__ __forceinline__ int wave_block_inverse(const double* a, double* __restrict__ dst,
+                                                  double* col) {
+    const int lane = threadIdx.x & 63;
+    double x[kB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = acc[r];
-    __syncthreads();
+    for (int i = 0; i < kB; ++i)
+        x[i] = lane < kB ? a[i * kL + lane] : (i == lane - kB ? 1.0 : 0.0);
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+        if (lane == k) {
+#pragma unroll
+            for (int i = 0; i < kB; i += 2)
+                *reinterpret_cast<double2*>(col + i) = make_double2(x[i], x[i + 1]);
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);      // keep the write before the reads
+        double c[kB];
+#pragma unroll
+        for (int i = 0; i < kB; i += 2) {
+            const double2 v = *reinterpret_cast<const double2*>(col + i);
+            c[i] = v.x;
+            c[i + 1] = v.y;
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);      // and the reads before the next write
+        const double piv = c[k];
+        if (!(piv > 0.0)) return k + 1;               // the same value in every lane
+        const double xk = x[k] / piv;
+#pragma unroll
+        for (int i = 0; i < kB; ++i)
+            if (i != k) x[i] = x[i] - c[i] * xk;
+        x[k] = xk;
+    }
+    if (lane >= kB) {
+#pragma unroll
+        for (int i = 0; i < kB; i += 2)
+            *reinterpret_cast<double2*>(dst + (int64_t)(lane - kB) * kB + i) =
+                make_double2(x[i], x[i + 1]);
+    }
     return 0;
 }
 
-__device__ __forceinline__ void store_block(const double* src, double* dst, int64_t ld) {
-    // LDS block (row stride kL) -> column-major global block (leading dimension ld)
-    for (int x = threadIdx.x; x < kB * kB; x += 256) {
-        const int i = x % kB, c = x / kB;
-        dst[i + (int64_t)c * ld] = src[i * kL + c];
-    }
-}
 __device__ __forceinline__ void load_block(const double* src, int64_t ld, double* dst) {
     for (int x = threadIdx.x; x < kB * kB; x += 256) {
         const int i = x % kB, c = x / kB;
@@ -292,16 +288,13 @@ __global__ void pad_matrix(const double* __restrict__ src, int64_t rows, int64_t
 __global__ __launch_bounds__(256) void ldl_first(const double* __restrict__ P, int64_t kp,
                                                  double* __restrict__ Sd,
                                                  int32_t* __restrict__ info) {
-    __shared__ double a[kB * kL], t[kB * kL], s[kB * kL];
+    __shared__ double a[kB * kL], col[kB];
     if (threadIdx.x == 0) *info = 0;
     load_block(P, kp, a);
     __syncthreads();
-    const int bad = block_inverse(a, t, s);
-    if (bad) {
-        if (threadIdx.x == 0) *info = bad;
-        return;
-    }
-    store_block(s, Sd, kB);
+    if (threadIdx.x >= 64) return;
+    const int bad = wave_block_inverse(a, Sd, col);
+    if (bad && threadIdx.x == 0) *info = bad;
 }
 
 // Block Gauss-Jordan step J on [P | B] (P kp x kp, B kp x nrhs, both column-major with
@@ -355,12 +348,9 @@ __global__ __launch_bounds__(256) void gj_step(double* __restrict__ P, int64_t k
 #pragma unroll
         for (int r = 0; r < 4; ++r) sA[blk_row(wave, lane, r) * kL + blk_col(wave, lane)] = acc[r];
         __syncthreads();
-        const int bad = block_inverse(sA, sX, sS);
-        if (bad) {
-            if (tid == 0) *info = (int32_t)(co + bad);
-            return;
-        }
-        store_block(sS, Sd + (int64_t)C * kB * kB, kB);
+        if (wave != 0) return;
+        const int bad = wave_block_inverse(sA, Sd + (int64_t)C * kB * kB, sX);
+        if (bad && tid == 0) *info = (int32_t)(co + bad);
     }
 }
 
