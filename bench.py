@@ -489,6 +489,9 @@ def main():
     launch_ms = tm["kernel_ms"] / launches
     path = net.mode()[1]
     kernel = "wavefront_flow" if path == "dataflow" else "wavefront_det"
+    if wl.enkf is not None and len(nets) > 1:
+        # member steps on the member-dataflow kernel, the forecast on the multi-launch kernel
+        kernel = "wavefront_flow (member steps) + wavefront_det (forecast)"
     # 72 B per reach·timestep deterministic, 40 + 32/E per reach·member·timestep
     per_unit = BYTES_PER_UNIT if E == 1 else 40.0 + 32.0 / E
     bytes_per_launch = per_unit * n * E * args.T * args.timing_runs / launches
