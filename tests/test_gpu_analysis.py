@@ -146,6 +146,26 @@ def test_enkf_rejects_single_member_and_bad_R():
         net2.enkf_gain(np.array([3, 7]), -np.eye(2))                 # not SPD
 
 
+def test_enkf_failure_reported_after_a_later_success():
+    """The factorisation status of every analysis is kept until the next synchronising call: a
+    failed analysis followed by a successful one is still reported (once), and the failed
+    analysis left the members unchanged (zeroed increment)."""
+    from tx_fast_hydrology_amd import _native as nat
+    end = synthetic.river_network(500, 1, 30, np.random.default_rng(1))
+    n = end.size
+    net, start, indeg = _net(end, members=4)
+    X = np.ones((n, 4))
+    net.set_state(X, X)                                   # zero spread: HA = 0
+    s = np.array([3, 7])
+    y = np.ones((2, 4))
+    net.enkf_analysis(s, y, -np.eye(2))                   # C = R = -I: not SPD
+    net.enkf_analysis(s, y, np.eye(2))                    # fine
+    with pytest.raises(nat.RoutingError):
+        net.get_state()
+    o, i = net.get_state()                                # reported once
+    assert np.array_equal(o, X) and np.array_equal(i, X)
+
+
 def test_staged_driver_single_rank_equals_enkf_analysis():
     """ensemble.distributed_analysis with one rank runs the mc_ens_* stages on torch device
     buffers; it must reproduce RoutingNet.enkf_analysis exactly."""

@@ -141,8 +141,11 @@ struct Net {
     DBuf<double> Pf, Sd, Rhs;
     DBuf<int64_t> gslot;
     DBuf<int32_t> info;
-    int32_t* info_host = nullptr;      // pinned copy of the factorisation status, read at sync()
-    bool info_pending = false;
+    // pinned copies of the factorisation status of every analysis since the last sync(), one
+    // word each (a later successful analysis must not hide an earlier failure)
+    static constexpr int kInfoRing = 256;
+    int32_t* info_host = nullptr;
+    int info_count = 0;
 
     // pinned staging ring for asynchronous host -> device uploads (no stream sync per call)
     struct PinSlot {
@@ -318,10 +321,14 @@ struct Net {
     // Wait for the stream; report a dataflow run whose waits gave up.
     void sync() {
         HIPC(hipStreamSynchronize(stream));
-        if (info_pending) {
-            info_pending = false;
-            if (*info_host != 0) {
-                *info_host = 0;
+        if (info_count > 0) {
+            int32_t bad = 0;
+            for (int k = 0; k < info_count; ++k) {
+                if (info_host[k] != 0 && bad == 0) bad = info_host[k];
+                info_host[k] = 0;
+            }
+            info_count = 0;
+            if (bad != 0) {
                 throw Fail(MC_E_INVALID, "ensemble analysis: the analysis matrix (HPH^T + R, or "
                                          "its ensemble-space form) is not positive definite; "
                                          "the increment was zeroed, the member states are "
@@ -467,11 +474,15 @@ struct Net {
     }
     // the factorisation status, read back asynchronously and reported at the next sync()
     void info_async() {
-        if (!info_host)
-            HIPC(hipHostMalloc(reinterpret_cast<void**>(&info_host), sizeof(int32_t),
+        if (!info_host) {
+            HIPC(hipHostMalloc(reinterpret_cast<void**>(&info_host), kInfoRing * sizeof(int32_t),
                                hipHostMallocDefault));
-        HIPC(hipMemcpyAsync(info_host, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
-        info_pending = true;
+            std::memset(info_host, 0, kInfoRing * sizeof(int32_t));
+        }
+        if (info_count == kInfoRing) sync();      // report (and free) the ring before reuse
+        HIPC(hipMemcpyAsync(info_host + info_count, info.p, sizeof(int32_t),
+                            hipMemcpyDeviceToHost, stream));
+        ++info_count;
     }
 
     // C = HA HA^T / (E-1) + R (m x m) from the current member state (padded to

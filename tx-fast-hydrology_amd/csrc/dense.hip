@@ -83,7 +83,7 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
     double zsum = 0.0, xs0 = 0.0, xs1 = 0.0;     // partial sums for zs[e] and the mean of X
     // buffer loads: an out-of-range offset (or an empty record) reads 0, so the edge masks are
     // offsets, not branches around the loads
-    const int zrec = (int)(ldz * (int64_t)Et * 8 < 0x7fffffff ? ldz * (int64_t)Et * 8 : 0x7fffffff);
+    const int zrec = (int)(ldz * (int64_t)Et * 8);          // < 2^31 (launcher)
     const auto zr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Z), (short)0, zrec,
                                                       0x00020000);
     auto load = [&](Slice& r, int f0) {
@@ -425,7 +425,8 @@ hipError_t launch_slice_increments(const double* X, const double* Z, int64_t ldz
                                    int64_t S, int64_t Et, hipStream_t s) {
     if (S <= 0) return hipSuccess;
     if (Et < 2 || Et > (1 << 20)) return hipErrorInvalidValue;
-    if (S * 8 >= 0x7fffffff) return hipErrorInvalidValue;   // one X row per buffer record
+    // buffer records: one X row, and all of Z (their byte offsets are 32-bit)
+    if (S * 8 >= 0x7fffffff || ldz * Et * 8 >= 0x7fffffff) return hipErrorInvalidValue;
     // 128-member tiles at every Et: 256-member tiles (slice_increments<4>, X read once at
     // Et = 256) measured 559 vs 528 us per EnKF256 analysis (profiles/r03i_*)
     constexpr int MW = 2;
