@@ -140,8 +140,12 @@ int mc_apply_gain(void* net, const double* gain);
  * sample covariance, P H^T = X'(HX')^T / (E-1), H P H^T = HX'(HX')^T / (E-1):
  *     o_e += K (y_e - o_e[gauges]),  K = P H^T (H P H^T + R)^-1,   i_e += one-hop(gain_e)
  * gauges [m]: reach indices (caller order; H selects their outflow); y [m][E]: observations per
- * member (identical columns = no perturbation); R [m][m] SPD.  Dense products run on f64 MFMA,
- * the m x m solve on rocSOLVER.  mc_enkf_gain returns K as [n][m] (diagnostics / tests). */
+ * member (identical columns = no perturbation); R [m][m] SPD.  Every dense step runs on the
+ * library's f64 MFMA kernels: for diagonal R and E <= m the E x E ensemble-space system
+ * (I + HA^T R^-1 HA / (E-1)), else the m x m one, solved by block Gauss-Jordan.  A system that is
+ * not positive definite zeroes that analysis's increment (the members stay unchanged) and is
+ * reported by the next synchronising call (MC_E_INVALID), also when later analyses succeeded.
+ * mc_enkf_gain returns K as [n][m] (diagnostics / tests). */
 int mc_enkf_analysis(void* net, int64_t m, const int64_t* gauges, const double* y,
                      const double* R);
 int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, double* K_out);
