@@ -116,8 +116,8 @@ def test_ensemble_rejects_dataflow_and_bad_shapes():
 
 
 @pytest.mark.parametrize("n,E,slots,tile", [(3000, 33, 256, 0), (1200, 2, 128, 0),
-                                            (4000, 256, 384, 0), (190_000, 32, 384, 0),
-                                            (190_000, 32, 192, 16)])
+                                            (4000, 256, 384, 0), (2500, 137, 192, 0),
+                                            (190_000, 32, 384, 0), (190_000, 32, 192, 16)])
 def test_member_dataflow_single_steps(n, E, slots, tile):
     """One-step runs of an ensemble (the analysis cycle of the EnKF) as member-dataflow launches:
     member e of slot d at tick G[d] + e.  Several consecutive one-step runs (interpolated
