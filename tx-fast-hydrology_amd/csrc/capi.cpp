@@ -398,7 +398,9 @@ struct Net {
         lds = mcr::flow_lds_bytes(S, Kc, 0, plan.max_ext_wg);
         bool ok = mcr::flow_shape_ok(S, Kc) &&
                   plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
-                  E < (1 << 24) && xg < (size_t(1) << 31) && lds <= 160 * 1024;
+                  E < (1 << 24) && xg < (size_t(1) << 31) && lds <= 160 * 1024 &&
+                  // member-major cells are addressed by 32-bit buffer offsets (flow.hip MEMB)
+                  (member_skew() || plan.nslots * E * 16 < (1ll << 31));
         if (ok) {
             int bpc = 0;
             HIPC(mcr::flow_members_occupancy(S, Kc, lds, &bpc));

@@ -59,6 +59,7 @@ using dev::fold_values;
 using dev::read_inputs;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kHelperLanes = 64;                      // one helper wave per workgroup
@@ -176,10 +177,12 @@ struct Helper {
 //   | EG [kFlowMaxExt] i32 (consumer G)
 // Each tick a lane routes its K positions in order; position p may take the output of position
 // p - 1 of the same tick (a chained edge, plan.hpp "lane chains").
-// MEMB: member dataflow (kernels.hpp, launch_flow_members): T = E members in place of steps.
+// MEMB: member dataflow (kernels.hpp, launch_flow_members): T = E members in place of steps;
+// SKEW: its staging cells are tick-major member windows (else member-major), a compile-time
+// choice so that the tick computes one kind of cell address without branches.
 // Register budget: two waves per SIMD (256 VGPRs) up to 3 positions per lane; lanes of 4
 // positions need more (one wave per SIMD, so at most 3 compute waves + the helper).
-template <int SLOTS, int K, bool DENSE, bool MEMB>
+template <int SLOTS, int K, bool DENSE, bool MEMB, bool SKEW = false>
 __global__ __launch_bounds__(SLOTS + kHelperLanes)
 __attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
 void wavefront_flow(WaveArgs a) {
@@ -314,21 +317,43 @@ void wavefront_flow(WaveArgs a) {
         // rarely share G) but is cheaper to stage, which wins for small ensembles.
         const double* __restrict__ Qm = a.Qm;
         double2* __restrict__ IO = reinterpret_cast<double2*>(const_cast<double*>(a.IO));
-        const bool skew = a.mskew != 0;
+        constexpr bool skew = SKEW;
         const int64_t mwb = skew ? a.wbase[w] : 0;      // member window of this workgroup
         const int rows = wend - gminw;                  // its rows: ticks gmin .. gmax + E - 1
         const int64_t mS = a.mS;
         constexpr int kRing = 4;
         static_assert(kChunk % kRing == 0, "ring slots must be static in the unrolled chunk");
-        auto cell = [&](int k, int p) -> int64_t {      // staging cell of tick k (clamped)
-            if (skew) {
-                int r = k - gminw;
-                r = r < 0 ? 0 : (r >= rows ? rows - 1 : r);
-                return mwb + (int64_t)r * RS + p * SLOTS + lid;
-            }
-            int e = k - S[p].G;
-            e = e < 0 ? 0 : (e >= T ? T - 1 : e);
-            return (int64_t)e * mS + S[p].d;
+        // tick-major windows (SKEW): the staging cell of tick k (row clamped, wave-uniform)
+        auto cell = [&](int k, int p) -> int64_t {
+            int r = k - gminw;
+            r = r < 0 ? 0 : (r >= rows ? rows - 1 : r);
+            return mwb + (int64_t)(r * RS + p * SLOTS + lid);
+        };
+        // member-major cells (!SKEW): bounds-checked buffer accesses at 32-bit byte offsets that
+        // advance one member row (mS cells) per tick -- no clamp and no 64-bit index per access.
+        // An offset outside the buffer (ticks before / after the lane's members, modular
+        // arithmetic) reads 0 and is never used; the offsets of active ticks are exact
+        // (members_fit: nslots x E x 16 B < 2^31).
+        const int ioRec = SKEW ? 0 : (int)(mS * T * 16), qmRec = SKEW ? 0 : (int)(mS * T * 8);
+        const auto io_r = __builtin_amdgcn_make_buffer_rsrc(IO, (short)0, ioRec, 0x00020000);
+        const auto qm_r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Qm), (short)0,
+                                                            qmRec, 0x00020000);
+        const unsigned ioStep = (unsigned)mS * 16u, qmStep = (unsigned)mS * 8u;
+        unsigned ioB[K], qmB[K];                        // byte offsets of this tick's cells
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            const unsigned idx = (unsigned)(kb - S[p].G) * (unsigned)mS + (unsigned)S[p].d;
+            ioB[p] = idx * 16u;
+            qmB[p] = idx * 8u;
+        }
+        auto load_io = [&](unsigned off) -> double2 {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(io_r, off, 0, 0);
+            return make_double2(__hiloint2double((int)v.y, (int)v.x),
+                                __hiloint2double((int)v.w, (int)v.z));
+        };
+        auto load_q = [&](unsigned off) -> double {
+            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(qm_r, off, 0, 0);
+            return __hiloint2double((int)v.y, (int)v.x);
         };
         double2 rIO[K][kRing];
         double rQ[K][kRing];
@@ -336,9 +361,14 @@ void wavefront_flow(WaveArgs a) {
         for (int r = 0; r < kRing; ++r)
 #pragma unroll
             for (int p = 0; p < K; ++p) {
-                const int64_t pa = cell(kb + r, p);
-                rIO[p][r] = IO[pa];
-                rQ[p][r] = Qm[pa];
+                if constexpr (SKEW) {
+                    const int64_t pa = cell(kb + r, p);
+                    rIO[p][r] = IO[pa];
+                    rQ[p][r] = Qm[pa];
+                } else {
+                    rIO[p][r] = load_io(ioB[p] + (unsigned)r * ioStep);
+                    rQ[p][r] = load_q(qmB[p] + (unsigned)r * qmStep);
+                }
             }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();                                // prologue barrier (helper staged XE)
@@ -377,9 +407,14 @@ void wavefront_flow(WaveArgs a) {
                     *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
 #pragma unroll
                 for (int p = 0; p < K; ++p) {   // refill this ring slot with tick k + kRing
-                    const int64_t pa = cell(k + kRing, p);
-                    rIO[p][r] = IO[pa];
-                    rQ[p][r] = Qm[pa];
+                    if constexpr (SKEW) {
+                        const int64_t pa = cell(k + kRing, p);
+                        rIO[p][r] = IO[pa];
+                        rQ[p][r] = Qm[pa];
+                    } else {
+                        rIO[p][r] = load_io(ioB[p] + (unsigned)kRing * ioStep);
+                        rQ[p][r] = load_q(qmB[p] + (unsigned)kRing * qmStep);
+                    }
                 }
                 // the member's new state, in place of its inputs (read kRing ticks ago by this
                 // lane); launch_member_unpack forms the session state
@@ -387,7 +422,17 @@ void wavefront_flow(WaveArgs a) {
                 for (int p = 0; p < K; ++p) {
                     const int e = k - S[p].G;
                     const bool act = (unsigned)e < (unsigned)T;
-                    if (act) IO[cell(k, p)] = make_double2(ov[p], Iv[p]);
+                    if constexpr (SKEW) {
+                        if (act) IO[cell(k, p)] = make_double2(ov[p], Iv[p]);
+                    } else {
+                        const u32x4 v = {(unsigned)__double2loint(ov[p]),
+                                         (unsigned)__double2hiint(ov[p]),
+                                         (unsigned)__double2loint(Iv[p]),
+                                         (unsigned)__double2hiint(Iv[p])};
+                        if (act) __builtin_amdgcn_raw_buffer_store_b128(v, io_r, ioB[p], 0, 0);
+                        ioB[p] += ioStep;
+                        qmB[p] += qmStep;
+                    }
                     if (S[p].xsrc && act) {
                         const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
                         const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
@@ -549,7 +594,7 @@ void wavefront_flow(WaveArgs a) {
     }
 }
 
-template <bool DENSE, bool MEMB>
+template <bool DENSE, bool MEMB, bool SKEW = false>
 const void* flow_fn(int slots, int chain);
 
 }  // namespace
@@ -563,11 +608,11 @@ bool flow_shape_ok(int slots, int chain) {
 
 namespace {
 
-template <bool DENSE, bool MEMB>
+template <bool DENSE, bool MEMB, bool SKEW>
 const void* flow_fn(int slots, int chain) {
 #define MCR_CASE(S, K)                 \
     if (slots == S && chain == K)      \
-        return reinterpret_cast<const void*>(&wavefront_flow<S, K, DENSE, MEMB>);
+        return reinterpret_cast<const void*>(&wavefront_flow<S, K, DENSE, MEMB, SKEW>);
     MCR_FLOW_SHAPES(MCR_CASE)
 #undef MCR_CASE
     return nullptr;
@@ -654,7 +699,11 @@ hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds, int* blo
 }
 
 hipError_t flow_members_occupancy(int slots, int chain, size_t lds, int* blocks_per_cu) {
-    return occupancy_of(flow_fn<false, true>(slots, chain), slots, lds, blocks_per_cu);
+    int a = 0, b = 0;                        // both staging layouts must be resident
+    hipError_t e = occupancy_of(flow_fn<false, true, false>(slots, chain), slots, lds, &a);
+    if (e == hipSuccess) e = occupancy_of(flow_fn<false, true, true>(slots, chain), slots, lds, &b);
+    *blocks_per_cu = std::min(a, b);
+    return e;
 }
 
 hipError_t launch_flow(const WaveArgs& a, int grid, int slots, int chain, size_t lds, bool dense,
@@ -667,7 +716,8 @@ hipError_t launch_flow(const WaveArgs& a, int grid, int slots, int chain, size_t
 
 hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain, size_t lds,
                                hipStream_t s) {
-    const void* fn = flow_fn<false, true>(slots, chain);
+    const void* fn = a.mskew ? flow_fn<false, true, true>(slots, chain)
+                             : flow_fn<false, true, false>(slots, chain);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<WaveArgs*>(&a)};
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);
