@@ -82,6 +82,10 @@ def parse(argv=None, world=None):
     ap.add_argument("--one-plan", action="store_true",
                     help="EnKF: route the forecast on the analysis plan too (no hand-over)")
     ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--fslots", type=int, default=256,
+                    help="EnKF: lanes of the forecast plan (after the last analysis)")
+    ap.add_argument("--ftile", type=int, default=64,
+                    help="EnKF: launch length (ticks) of the forecast plan")
     ap.add_argument("--chain", type=int, default=0,
                     help="node slots per lane (plan.hpp lane chains); 0 = per workload")
     ap.add_argument("--conus", action="store_true",
@@ -248,7 +252,8 @@ def build_workload(args, rank=0, world=1):
     if enkf is not None and not args.one_plan:
         # the forecast after the last analysis runs on its own plan (256 lanes, 64-tick
         # launches: the multi-launch ensemble shape), the state handed over on the device
-        fnet = engine.RoutingNet(end, indeg, heads, slots=256, tile=64, members=E)
+        fnet = engine.RoutingNet(end, indeg, heads, slots=getattr(args, "fslots", 256),
+                                 tile=getattr(args, "ftile", 64), members=E)
         fnet.set_coeffs(alpha, beta, chi, gamma)
         fnet.load_forcing(xp, fp)
         enkf.fnet = fnet
