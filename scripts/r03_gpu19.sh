@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_gpu_analysis.py tests/test_gpu_dist.py tests/test_gpu_kalman.py "tests/test_gpu_configs.py::test_config3_texas_enkf256_member_step_and_analysis" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r03t_pytest.txt 2>&1
+MCROUTE_LIB=$PWD/tx-fast-hydrology_amd/tx_fast_hydrology_amd/lib/exp/lib_fuse.so timeout -k 10 700 python -u -m pytest tests/test_gpu_analysis.py tests/test_gpu_dist.py tests/test_gpu_kalman.py "tests/test_gpu_configs.py::test_config3_texas_enkf256_member_step_and_analysis" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r03t_pytest.txt 2>&1
 rc=$?; tail -2 gpurun_out/r03t_pytest.txt; [ $rc -ne 0 ] && exit $rc
 bash scripts/ab_lib.sh "cur fuse" "--steps 5 --warmup 1 --members 32 --enkf" > gpurun_out/r03t_ab_enkf32.txt 2>&1
 rc=$?; cat gpurun_out/r03t_ab_enkf32.txt; [ $rc -ne 0 ] && exit $rc
