@@ -103,9 +103,8 @@ struct Net {
     // per-step interpolation table {row_lo, row_hi, frac}
     DBuf<int4> stab;
     // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
-    // workgroup, step-0 index of each reach and of each external input), a scratch for fetches
-    // and the dummy row of out-of-window ticks
-    DBuf<double> O, outT, dummy;
+    // workgroup, step-0 index of each reach and of each external input) and a scratch for fetches
+    DBuf<double> O, outT;
     DBuf<int64_t> in_off, in_list;   // inflow lists (plan.hpp), caller order
     // per-horizon schedules (active workgroups per launch, output windows), cached per T
     struct Sched {
@@ -281,7 +280,6 @@ struct Net {
             HIPC(hipMemsetAsync(b->p, 0, ns * sizeof(double), stream));
         }
         stage.reserve(std::max<int64_t>(plan.n, 1));
-        dummy.reserve(mcr::kDummyPerMember);
         HIPC(hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device));
         {
             std::vector<int32_t> ids(std::max<int32_t>(plan.nwg, 1));
@@ -671,7 +669,6 @@ struct Net {
             b->reserve(ns * m);
             HIPC(hipMemsetAsync(b->p, 0, ns * m * sizeof(double), stream));
         }
-        dummy.reserve(mcr::kDummyPerMember * m);
         n_rows = 0;                    // forcing and outputs are per member: load again
         T_out = 0;
         sync();
@@ -798,7 +795,6 @@ struct Net {
         a.wg_gmax = wg_gmax.p;
         a.wbase = cur->wbase.p;
         a.O = O.p;
-        a.dummy = dummy.p;
         a.nslots = plan.nslots;
         a.n_rows = (int32_t)rows;
         a.T = (int32_t)T;

@@ -8,7 +8,7 @@
 // produced in an earlier launch and are staged in LDS in the launch prologue, together with the
 // window of the per-step interpolation table this workgroup needs.  The tick loop issues no
 // global loads except the per-chunk forcing-row prefetch; each tick's outputs leave as one
-// contiguous row per wave (workgroup windows, kernels.hpp).
+// row per wave, active cells only (workgroup windows, kernels.hpp).
 //
 // Arithmetic follows the reference exactly (FMA contraction is off for this file):
 //   I = ((0 + o[u1]) + o[u2]) + ...          upstream reaches in reference finalisation order
@@ -79,7 +79,6 @@ void wavefront_det(WaveArgs a) {
     const double* Fm = a.F + mem * a.mF;
     double* Om = a.O + mem * a.mO;
     double* XSm = a.XS + mem * a.mX;
-    double* dum = a.dummy + mem * kDummyPerMember;
     const int T = a.T;
     const int k0 = a.kappa0;
     const int64_t ns = a.nslots;
@@ -159,7 +158,6 @@ void wavefront_det(WaveArgs a) {
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
-    const int wend = gmaxw + T;                         // end of this workgroup's window
     constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
@@ -176,16 +174,21 @@ void wavefront_det(WaveArgs a) {
             frp[p] = FR + (unsigned)(p * SLOTS + tid) * 24 - (unsigned)rb[p] * 8;
             tp[p] = TAB + (unsigned)(kc - S[p].G - tw0) * 16u;
         }
-        // prefetch the forcing rows of the next chunk (unconditional, clamped rows)
+        // prefetch the forcing rows of the next chunk (clamped rows), only for slots that run a
+        // step in it (the rows of the others would feed ticks whose outputs are not kept)
         const int Tn = c + kChunk < tile ? T : 0;
+        const int kn = kc + kChunk;
         int rbn[K], nrn[K];
         double g0[K], g1[K], g2[K];
 #pragma unroll
         for (int p = 0; p < K; ++p) {
-            chunk_rows(tab, tw0, kc + kChunk, S[p].G, Tn, rbn[p], nrn[p]);
-            g0[p] = Fm[(int64_t)clamp_row(rbn[p], nrow) * ns + S[p].d];
-            g1[p] = Fm[(int64_t)clamp_row(rbn[p] + 1, nrow) * ns + S[p].d];
-            g2[p] = Fm[(int64_t)clamp_row(rbn[p] + 2, nrow) * ns + S[p].d];
+            chunk_rows(tab, tw0, kn, S[p].G, Tn, rbn[p], nrn[p]);
+            g0[p] = g1[p] = g2[p] = 0.0;
+            if (Tn > 0 && kn + kChunk > S[p].G && kn < S[p].G + T) {
+                g0[p] = Fm[(int64_t)clamp_row(rbn[p], nrow) * ns + S[p].d];
+                g1[p] = Fm[(int64_t)clamp_row(rbn[p] + 1, nrow) * ns + S[p].d];
+                g2[p] = Fm[(int64_t)clamp_row(rbn[p] + 2, nrow) * ns + S[p].d];
+            }
         }
         // per-chunk LDS cursors: input value of tick i at m[u] + 8 * ((i + 1) & 1)
         unsigned m[K][kUpInline];
@@ -238,16 +241,17 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
             double ov[K];
+            bool act[K];
             double prev = 0.0;
 #pragma unroll
             for (int p = 0; p < K; ++p) {
-                const bool act = (unsigned)(k - S[p].G) < (unsigned)T;
+                act[p] = (unsigned)(k - S[p].G) < (unsigned)T;
                 const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
                 const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
                                           S[p].ch * S[p].op) + S[p].ga * qv[p]);
                 const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
-                S[p].op = act ? o : S[p].op;
-                S[p].ip = act ? I : S[p].ip;
+                S[p].op = act[p] ? o : S[p].op;
+                S[p].ip = act[p] ? I : S[p].ip;
                 ov[p] = o;
                 prev = o;
             }
@@ -256,16 +260,19 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p)
                 *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
-            // one contiguous row of RS values per tick; ticks outside the window: dummy row
-            const bool inwin = k >= gminw && k < wend;
-            double* orow = inwin ? Om + wb + (int64_t)(k - gminw) * RS : dum;
+            // row k - gmin of the workgroup's window; only active (slot, tick) cells are stored
+            // (slots are sorted by G, so a wave's active lanes are a contiguous run and the
+            // masked rows stay whole 32-B sectors except at the run's ends): the window cells a
+            // slot does not run in are never read (window_index), so they are not written
             if (!MCR_EXP_NO_STORES) {
+                double* orow = Om + wb + (int64_t)(k - gminw) * RS;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     // non-temporal: rows are written once and read only by later fetches
-                    __builtin_nontemporal_store(ov[p], orow + p * SLOTS + tid);
-                    if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T)
-                        XSm[S[p].xs0 + k] = ov[p];
+                    if (act[p]) {
+                        __builtin_nontemporal_store(ov[p], orow + p * SLOTS + tid);
+                        if (S[p].xsrc) XSm[S[p].xs0 + k] = ov[p];
+                    }
                 }
             }
             if (!MCR_EXP_NO_BARRIER) __syncthreads();
@@ -279,13 +286,16 @@ void wavefront_det(WaveArgs a) {
             f2[p] = g2[p];
         }
     }
-    // state for the next launch (slots that did not run keep theirs); never-processed reaches
-    // hold o = 0 as in the reference's fresh o_t_next
+    // state for the next launch; never-processed reaches hold o = 0 as in the reference's fresh
+    // o_t_next.  Slots that did not run in this launch (load_slot: G = 1 << 29) keep theirs
+    // unchanged, so only the live ones are stored
     const int64_t sb = (int64_t)blockIdx.y * a.mS;
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        a.st_o[sb + S[p].d] = S[p].op;
-        a.st_i[sb + S[p].d] = S[p].ip;
+        if (S[p].G != (1 << 29)) {
+            a.st_o[sb + S[p].d] = S[p].op;
+            a.st_i[sb + S[p].d] = S[p].ip;
+        }
     }
     if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();

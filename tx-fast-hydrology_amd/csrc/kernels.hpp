@@ -4,9 +4,11 @@
 // Output layout ("workgroup windows").  Workgroup w owns the ticks [gmin[w], gmax[w] + T) of the
 // space-time schedule; its outputs are stored tick-major inside that window:
 //     O[wbase[w] + (tick - gmin[w]) * RS + slot - w * RS]      (RS = chain * slots)
-// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  (Per-wave "segment"
-// windows that store only the ticks of a wave's own reaches wrote 10 % (det) / 30 % (ens64)
-// fewer bytes but ran 1-2 % / 4-6 % slower: DESIGN.md §6, round 3.)  Inflows are not stored:
+// so the 64 lanes of a wave write one contiguous 512-byte row per tick.  Only the cells of
+// slots active at the tick are stored (the multi-launch kernel masks the rest: ens64 writes
+// -23 %, 5 % faster); the dataflow kernel's helper copies whole rows (masking its copies cost
+// 3 %).  (Per-wave "segment" windows wrote 10 % (det) / 30 % (ens64) fewer bytes but ran
+// 1-2 % / 4-6 % slower: DESIGN.md §6, round 3.)  Inflows are not stored:
 // i[j][t] = ((0 + o[u1][t]) + o[u2][t]) + ... over j's inflow list (plan.hpp) is recomputed
 // bit-exactly wherever it is needed (fetches, final state).  A reach that feeds a
 // reach of another cluster (an "external input" of the consumer's workgroup) also writes its
@@ -37,8 +39,6 @@ namespace mcr {
 // together).  Launch lengths (`tile`) are multiples of it.
 constexpr int kChunk = 8;
 
-// doubles of the out-of-window dummy row per ensemble member (>= the widest chain * slots)
-constexpr int64_t kDummyPerMember = 2048;
 
 // Dataflow kernel (flow.hip): external inputs per workgroup it supports, longest step table it
 // keeps in LDS, minimum cross-cluster slack (the helper stages the next chunk, so producers must
@@ -87,7 +87,6 @@ struct WaveArgs {
     // member-major arrays F, O, XS and of st_o / st_i (in slots)
     int64_t mF, mO, mX, mS;
     double* XS;                   // external-input streams [n_ext][T]: step t of each source
-    double* dummy;                // >= 2 * 1024 doubles: cells of out-of-window ticks
     int64_t* trace;               // optional launch trace, kTraceWords per workgroup (NULL = off)
     // dataflow kernel (flow.hip) only
     uint32_t* XG;                 // external-input granules [n_ext][T] x {lo, epoch, hi, epoch}
