@@ -160,6 +160,9 @@ int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, d
  *   3. mc_ens_slice_update: anomalies, C = HA HA^T/(Et-1) + R, W = C^-1 D, Z = HA^T W/(Et-1),
  *      increments of the slice Gs_dev = A Z [Et][S];    -> all-to-all back into [N][E][S]
  *   4. mc_ens_unpack_apply: local increments -> _apply_gain on the local members.
+ * Stage 3 in two halves: mc_ens_weights forms Z from the gathered gauge data only (kept in the
+ * session), mc_ens_increments the slice increments from Xs_dev and that Z, so the weights can be
+ * computed while the member -> slice all-to-all is in flight.  mc_ens_slice_update = both.
  * With N = 1 the stages are exactly mc_enkf_analysis.  Stages run on the session's stream. */
 int mc_ens_slice_size(const void* net, int64_t nranks, int64_t* S);
 int mc_ens_gauges(void* net, int64_t m, const int64_t* gauges, const double* y, double* HX_dev,
@@ -168,6 +171,9 @@ int mc_ens_pack(void* net, int64_t nranks, double* send_dev);
 int mc_ens_slice_update(void* net, int64_t nranks, int64_t m, const double* Xs_dev,
                         const double* HXall_dev, const double* Dall_dev, const double* R,
                         double* Gs_dev);
+int mc_ens_weights(void* net, int64_t nranks, int64_t m, const double* HXall_dev,
+                   const double* Dall_dev, const double* R);
+int mc_ens_increments(void* net, int64_t nranks, const double* Xs_dev, double* Gs_dev);
 int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv_dev);
 
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
@@ -196,6 +202,21 @@ int mc_load_forcing(void* net, int64_t n_rows, const double* xp, const double* f
 int mc_run(void* net, int64_t T, const double* x);
 /* Copy steps [t0, t1) of the last mc_run to the host, step-major: out_o[t - t0][j]. */
 int mc_fetch_outputs(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i);
+/* Asynchronous form of mc_fetch_outputs for the drop-in API's fused horizons (muskingum.py
+ * simulate_iter, :499-536, yields every step's fresh arrays): queues the copy of steps [t0, t1)
+ * into out_o / out_i (host, [t1 - t0][n]; pinned memory makes the copy asynchronous and full
+ * speed) and, when digest_o / digest_i are non-NULL, the row digest of every copied step
+ * (mc_host_digest of the same row) -- the caller detects an in-place edit of a yielded array by
+ * recomputing it on the host.  Returns at once with *ticket; the buffers are complete after
+ * mc_fetch_wait(ticket) (every ticket must be waited for once).  Any pointer but ticket may be
+ * NULL. */
+int mc_fetch_outputs_async(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i,
+                           uint64_t* digest_o, uint64_t* digest_i, int64_t* ticket);
+int mc_fetch_wait(void* net, int64_t ticket);
+/* Row digests of a host array [nrows][n]: out[r] = sum mod 2^64 over j of
+ * t ^ (t >> 29), t = (bits(rows[r][j]) ^ (j * 0x9E3779B97F4A7C15)) * 0xD6E8FEB86659FD93.  Changing
+ * any single element changes it.  Host code (no device needed), a few threads. */
+int mc_host_digest(const double* rows, int64_t nrows, int64_t n, uint64_t* out);
 /* Copy the full series of the last mc_run, reach-major: out_o[j][t] (either may be NULL). */
 int mc_fetch_series(void* net, double* out_o, double* out_i);
 /* Convenience: mc_load_forcing + mc_run + mc_fetch_outputs(0, T). */
@@ -233,7 +254,13 @@ int mc_set_flow_patience(void* net, int64_t wall_ticks);
  *   F[r] += alpha * I(r + 1) / gamma + beta * I(r) / gamma   (I(0) = o_start),
  * alpha / beta / gamma being the downstream reach's coefficients.  The destination's forcing
  * must have one row per source step.  Ordered on the streams (after the source's run, before
- * the destination's next call), no host synchronisation.  Single-member sessions. */
+ * the destination's next call), no host synchronisation.  Single-member sessions.
+ * The correction reads the source's outputs as its stream produced them.  If that horizon's
+ * dataflow waits gave up (mc_set_flow_patience), the source re-routes it at its next
+ * synchronising call and mc_net_reroutes(src) grows, but corrections already taken from it are
+ * not redone: a caller that chains sessions checks the sources' reroute counts after
+ * synchronising and re-routes the dependent horizons (simulation.py falls back to its host
+ * driver). */
 int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_net,
                               int64_t src_reach, double o_start, double alpha, double beta,
                               double gamma);

@@ -44,6 +44,18 @@ def run(model, df, **kw):
     return np.array(os_), np.array(is_), np.array(ts, dtype=np.int64)
 
 
+def digest_rows(a):
+    """NumPy restatement of the row digest (mcroute.h mc_host_digest, kernels.hpp digest_term):
+    sum mod 2^64 over j of t ^ (t >> 29), t = (bits(a[r, j]) ^ (j * K1)) * K2."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    a = a.reshape(1, -1) if a.ndim == 1 else a.reshape(a.shape[0], -1)
+    bits = a.view(np.uint64)
+    j = np.arange(a.shape[1], dtype=np.uint64)
+    t = (bits ^ (j * np.uint64(0x9E3779B97F4A7C15))) * np.uint64(0xD6E8FEB86659FD93)
+    t ^= t >> np.uint64(29)
+    return t.sum(axis=1, dtype=np.uint64)
+
+
 class OracleNet:
     """CPU stand-in for engine.RoutingNet (test double: the oracle routes)."""
 
@@ -78,6 +90,18 @@ class OracleNet:
 
     def fetch_outputs(self):
         return self.out_o.copy(), self.out_i.copy()
+
+    def fetch_outputs_async(self, t0, t1, out_o, out_i, digest_o=None, digest_i=None):
+        for dst, src, dg in ((out_o, self.out_o, digest_o), (out_i, self.out_i, digest_i)):
+            if dst is not None:
+                dst[...] = src[t0:t1]
+            if dg is not None:
+                dg[...] = digest_rows(src[t0:t1])
+        self.fetches = getattr(self, "fetches", 0) + 1
+        return self.fetches
+
+    def fetch_wait(self, ticket):
+        pass
 
     def close(self):
         pass

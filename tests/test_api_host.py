@@ -200,6 +200,76 @@ def test_fused_horizon_routes_in_place_edits(golden, monkeypatch):
     assert not np.array_equal(results[0][6:50], g["o"][6:])
 
 
+COEF_EDITS = {
+    "transmissive": lambda m: m.set_transmissive_boundary([2, 5]),
+    "element": lambda m: m.alpha.__setitem__(4, 0.25),
+    "inplace_ufunc": lambda m: m.beta.__imul__(1.01),
+    "copyto": lambda m: np.copyto(m.chi, m.chi * 0.99),
+    "ufunc_at": lambda m: np.add.at(m.gamma, [1, 1, 3], 1e-3),
+    "rebind": lambda m: setattr(m, "alpha", np.array(m.alpha) * 1.02),
+    "dt_recompute": lambda m: m.compute_muskingum_coeffs(dt=450.0),
+}
+
+
+@pytest.mark.parametrize("edit", sorted(COEF_EDITS))
+def test_fused_horizon_follows_coefficient_edits(golden, monkeypatch, edit):
+    """The reference reads alpha..gamma at every step (muskingum.py:450-453): a coefficient
+    change between two yields of a fused horizon applies from the next step, exactly as the
+    step-by-step path (and the reference) routes it."""
+    use_oracle_device(monkeypatch)
+    g = golden("g3_confluence.npz")
+    results = []
+    for fused in (True, False):
+        m = golden_model(g)
+        df = golden_frame(g, m.reach_ids)
+        if not fused:
+            m.bind_callback(BaseCallback(), key="noop")
+        out = []
+        for k, state in enumerate(m.simulate(df)):
+            out.append((np.array(state.o_t_next), np.array(state.i_t_next)))
+            if k == 9:
+                COEF_EDITS[edit](state)
+        results.append(out)
+    fo, so = (np.array([r[0] for r in res]) for res in results)
+    fi, si = (np.array([r[1] for r in res]) for res in results)
+    assert np.array_equal(fo, so) and np.array_equal(fi, si)
+    assert not np.array_equal(fo[10:50], g["o"][10:])      # the edit changed the routing
+    assert np.array_equal(fo[:10], g["o"][:10])
+
+
+def test_coefficient_tracking_is_per_model():
+    m = Muskingum(model_dict(np.array([2, 2, 3, 3]), np.full(4, 3600.0), np.full(4, 0.2),
+                             np.ones(4), T0, 300))
+    r0 = m._coef_rev[0]
+    c = m.copy()
+    c.alpha[0] = 9.0
+    assert m._coef_rev[0] == r0 and m.alpha[0] != 9.0      # copies track (and own) their own
+    m.alpha[1] = 0.5
+    assert m._coef_rev[0] == r0 + 1
+    view = m.beta[1:3]
+    view[0] = 0.0                                           # writes through views count
+    assert m._coef_rev[0] == r0 + 2
+    before = m._coef_rev[0]
+    _ = m.alpha * 2 + m.chi.sum()                           # reads never do
+    assert m._coef_rev[0] == before and type(m.alpha * 2) is np.ndarray
+    import pickle
+    p = pickle.loads(pickle.dumps(m))
+    p.gamma[0] = 1.0
+    assert m._coef_rev[0] == before and p.gamma[0] == 1.0
+
+
+def test_fused_horizon_final_state_owns_its_arrays(golden, monkeypatch):
+    """The last two yielded steps are copies: after the horizon the model's state arrays hold
+    no fetched block alive."""
+    use_oracle_device(monkeypatch)
+    g = golden("g3_confluence.npz")
+    m = golden_model(g)
+    for _ in m.simulate(golden_frame(g, m.reach_ids)):
+        pass
+    for key in ("o_t_next", "i_t_next", "o_t_prev", "i_t_prev"):
+        assert getattr(m, key).base is None, key
+
+
 def test_fused_horizon_early_break_leaves_writable_state(golden, monkeypatch):
     use_oracle_device(monkeypatch)
     g = golden("g3_confluence.npz")

@@ -223,3 +223,36 @@ def test_ensemble_space_solve_equals_observation_space(E, m):
     for e in range(0, E, 7):
         _, og = orc.apply_gain(start[indeg == 0], end, G[:, e], indeg)
         np.testing.assert_allclose(out[0][0][:, e] - X[:, e], og, rtol=0, atol=1e-10 * scale)
+
+
+def test_enkf256_large_mean_and_zero_spread_reaches():
+    """ADVICE r3 (slice_increments, E > 64): reaches whose members are identical get increments
+    of exactly 0 (their outflow is unchanged bit for bit, as the reference's X - mean gives), and
+    reaches with a large mean and a small spread keep their increments to spread-relative
+    accuracy -- the member mean is taken out before the products, not after."""
+    end = synthetic.river_network(3000, 4, 120, np.random.default_rng(33))
+    n = end.size
+    E, m = 256, 30
+    net, start, indeg = _net(end, members=E)
+    rng = np.random.default_rng(8)
+    X = rng.uniform(0.5, 5, n)[:, None] * rng.lognormal(0, 0.3, (n, E))
+    flat = rng.choice(n, 200, replace=False)               # zero spread
+    X[flat] = rng.uniform(1, 10, 200)[:, None]
+    big = np.setdiff1d(rng.choice(n, 300, replace=False), flat)   # mean 1e6, spread 1e-3
+    X[big] = 1e6 + 1e-3 * rng.standard_normal((big.size, E))
+    I0 = rng.uniform(0, 5, (n, E))
+    net.set_state(X, I0)
+    s = np.sort(rng.choice(np.setdiff1d(np.arange(n), np.concatenate([flat, big])), m,
+                           replace=False))
+    R = 1e-2 * np.eye(m)
+    Y = X[s].mean(1, keepdims=True) + 0.3 + rng.normal(0, 0.1, (m, E))
+    net.enkf_analysis(s, Y, R)
+    o, _ = net.get_state()
+    G = _numpy_enkf(X, s, Y, R)
+    assert np.array_equal(o[flat], X[flat])                # 0 + 0 increments: bit-identical
+    spread = np.abs(X[big] - X[big].mean(1, keepdims=True)).max()
+    assert spread < 1e-2
+    np.testing.assert_allclose(o[big] - X[big], G[big], rtol=0,
+                               atol=1e-9 * np.abs(G[big]).max() + 1e-7 * spread)
+    rest = np.setdiff1d(np.arange(n), np.concatenate([flat, big]))
+    np.testing.assert_allclose(o[rest] - X[rest], G[rest], rtol=0, atol=1e-10 * np.abs(G).max())

@@ -187,3 +187,70 @@ def test_async_simulation_device_dag_equals_host_driver(n, n_cuts):
         for a, b in zip(st_d[k][:3], st_h[k][:3]):
             assert np.array_equal(a, b), k
         assert st_d[k][3] == st_h[k][3], k
+
+
+@pytest.mark.parametrize("edit_step", [0, 40, 286])
+def test_fused_coefficient_edit_mid_horizon_bitexact(golden, edit_step):
+    """set_transmissive_boundary inside a simulate loop (reference muskingum.py:567-571): the
+    reference reads the coefficients at every step (:450-453), so the edit applies from the next
+    step.  The mirror's fused horizon notices it and routes the rest step by step: every step
+    bit-exact against the oracle's run with the coefficients changed after step `edit_step`."""
+    from oracle import oracle as orc
+    g = golden("g2_huc8.npz")
+    m = golden_model(g)
+    df = golden_frame(g, m.reach_ids)
+    cut = [3, 17, 250]
+    coef0 = [np.array(a) for a in (m.alpha, m.beta, m.chi, m.gamma)]
+    o0, i0 = np.array(m.o_t_next), np.array(m.i_t_next)
+    o, i, t = [], [], []
+    for k, state in enumerate(m.simulate(df)):
+        o.append(np.array(state.o_t_next))
+        i.append(np.array(state.i_t_next))
+        t.append(state.datetime.value)
+        if k == edit_step:
+            state.set_transmissive_boundary(cut)
+    o, i = np.array(o), np.array(i)
+    x = np.array(t, dtype=np.int64).astype(float)
+    xp = df.index.astype(np.int64).astype(float).values
+    fp = np.ascontiguousarray(df.values)
+    start = np.asarray(m.startnodes)
+    coef1 = [a.copy() for a in coef0]
+    for a, v in zip(coef1, (1.0, 0.0, 0.0, 0.0)):
+        a[cut] = v
+    e = edit_step + 1
+    wo1, wi1, fo, fi = orc.simulate(start, m.endnodes, m.indegree, *coef0, o0, i0, x[:e], xp, fp)
+    wo2, wi2, _, _ = orc.simulate(start, m.endnodes, m.indegree, *coef1, fo, fi, x[e:], xp, fp)
+    assert np.array_equal(o, np.concatenate([wo1, wo2]))
+    assert np.array_equal(i, np.concatenate([wi1, wi2]))
+    assert isinstance(m._device.net, engine.RoutingNet)
+
+
+def test_device_dag_give_up_falls_back_to_host_driver():
+    """an upstream sub-basin's dataflow horizon that gives up (patience < 0) is
+    re-routed by its session at the fetch, but the corrections already taken from it used
+    incomplete outflows -- the device DAG detects the re-route and routes the collection with
+    the host driver instead: still bit-identical to the host driver's run."""
+    res = []
+    rerouted = 0
+    for device in (True, False):
+        whole, df, cuts = _split_case(20000, 60, 7 + 20000)
+        coll = whole.split(cuts, create_state_space=False)
+        if device:
+            for m in coll.models.values():
+                m._device.session(m).set_flow_patience(-1)
+        else:
+            for m in coll.models.values():
+                m.bind_callback(_Idle(), key="idle")
+        sim = AsyncSimulation(coll, df)
+        outputs = asyncio.run(sim.simulate())
+        if device:
+            rerouted = sum(m._device.net.reroutes() for m in coll.models.values())
+        res.append((outputs, sim.inputs,
+                    {k: (m.o_t_next, m.i_t_next, m.o_t_prev) for k, m in coll.models.items()}))
+    assert rerouted > 0                      # some horizon gave up and was re-routed
+    (o_d, in_d, st_d), (o_h, in_h, st_h) = res
+    for k in o_h:
+        assert np.array_equal(o_d[k].values, o_h[k].values), k
+        assert np.array_equal(in_d[k].values, in_h[k].values), k
+        for a, b in zip(st_d[k], st_h[k]):
+            assert np.array_equal(a, b), k

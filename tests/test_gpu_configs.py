@@ -113,6 +113,66 @@ def test_config3_texas_enkf256_member_step_and_analysis():
     net.close()
 
 
+@pytest.mark.timeout(600)
+def test_config3_eight_shards_emulated_bitexact():
+    """configs[3] in its SHARDED form: 8 sessions of 32 members (the 8-GPU layout of the
+    256-member EnKF) on one GPU, driven by ensemble.emulated_analysis -- every mc_ens_* stage
+    with nranks = 8 exactly as on 8 GPUs, the all-gathers and all-to-alls as device copies.
+    Two analyses: bit-identical to the one-session 256-member analysis, and within 1e-10 of
+    max|G| of the NumPy restatement of da.py:112-126 with the sample covariance."""
+    import torch
+
+    from tx_fast_hydrology_amd import engine, ensemble
+    N = 8
+    args = bench.parse(["--members", "256", "--enkf", "--one-plan"], world=1)
+    full, wl = bench.build_workload(args)
+    ek = wl.enkf
+    E, El = wl.E, wl.E // N
+    heads = wl.start[wl.indeg == 0]
+    info = full.info
+    shards = []
+    for r in range(N):
+        s = engine.RoutingNet(wl.end, wl.indeg, heads, slots=info["slots"], tile=info["tile"],
+                              members=El)
+        s.set_coeffs(*_coef(wl))
+        cols = slice(r * El, (r + 1) * El)
+        s.set_state(np.ascontiguousarray(wl.o0[:, cols]), np.ascontiguousarray(wl.i0[:, cols]))
+        shards.append(s)
+    X, I = full.get_state()
+    for k in range(2):
+        Y = ek.Y[k]                                  # [m, 256]: shard r holds columns r*32..
+        stage_ms = {}
+        ensemble.emulated_analysis(shards, ek.gauges,
+                                   [np.ascontiguousarray(Y[:, r * El:(r + 1) * El])
+                                    for r in range(N)], ek.R, stage_ms=stage_ms)
+        full.enkf_analysis(ek.gauges, Y, ek.R)
+        o_full, i_full = full.get_state()
+        parts = [s.get_state() for s in shards]
+        o_sh = np.concatenate([p[0] for p in parts], axis=1)
+        i_sh = np.concatenate([p[1] for p in parts], axis=1)
+        assert np.array_equal(o_sh, o_full) and np.array_equal(i_sh, i_full), k
+        # the NumPy restatement (sample covariance in da.py:119-126)
+        g = ek.gauges
+        A = X - X.mean(1, keepdims=True)
+        HA = A[g]
+        W = np.linalg.solve(HA @ HA.T / (E - 1) + ek.R, Y - X[g])
+        G = A @ (HA.T @ W) / (E - 1)
+        scale = np.abs(G).max()
+        assert scale > 1e-3
+        for e in range(0, E, 37):
+            ig, og = orc.apply_gain(heads, wl.end, np.ascontiguousarray(G[:, e]), wl.indeg)
+            np.testing.assert_allclose(o_full[:, e] - X[:, e], og, rtol=0, atol=1e-10 * scale)
+            np.testing.assert_allclose(i_full[:, e] - I[:, e], ig, rtol=0,
+                                       atol=1e-10 * scale * 8)
+        print("per-shard stage ms", {kk: [round(v, 3) for v in vv]
+                                     for kk, vv in stage_ms.items()})
+        X, I = o_full, i_full
+    torch.cuda.synchronize()
+    for s in shards:
+        s.close()
+    full.close()
+
+
 def test_config4_conus_16_members_full_horizon():
     args = bench.parse(["--conus"], world=1)
     net, wl = bench.build_workload(args)

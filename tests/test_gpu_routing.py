@@ -497,3 +497,36 @@ def test_dataflow_give_up_then_state_changes(exec_mode):
     net.run(x)
     w3_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp2)
     assert np.array_equal(net.fetch_outputs()[0], w3_o)
+
+
+@pytest.mark.parametrize("n,T,block", [(3000, 50, 7), (6000, 96, 96), (1, 5, 2)])
+def test_async_fetch_and_device_digests(n, T, block):
+    """mc_fetch_outputs_async: blocks of steps copied into pinned host rows with the device's row
+    digests (the drop-in API's edit detector) -- the rows equal mc_fetch_outputs and the oracle,
+    every device digest equals mc_host_digest of the copied row."""
+    import torch
+    end, K, X = _random_case(n, 3 * n + T, 0.9, max(1, n // 500))
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=n)
+    xp, fp = synthetic.forcing(n, rows=6, seed=n)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0)
+    net.load_forcing(xp, fp)
+    net.run(x)
+    got = []
+    for b0 in range(0, T, block):
+        b1 = min(T, b0 + block)
+        oo = torch.empty((b1 - b0, n), dtype=torch.float64, pin_memory=True).numpy()
+        ii = torch.empty((b1 - b0, n), dtype=torch.float64, pin_memory=True).numpy()
+        dg = torch.zeros((2, b1 - b0), dtype=torch.uint64, pin_memory=True).numpy()
+        got.append((b0, oo, ii, dg, net.fetch_outputs_async(b0, b1, oo, ii, dg[0], dg[1])))
+    for b0, oo, ii, dg, tk in got:
+        net.fetch_wait(tk)
+        assert np.array_equal(oo, want_o[b0:b0 + oo.shape[0]])
+        assert np.array_equal(ii, want_i[b0:b0 + ii.shape[0]])
+        assert np.array_equal(dg[0], engine.host_digest(oo))
+        assert np.array_equal(dg[1], engine.host_digest(ii))
+    oo2, ii2 = net.fetch_outputs()
+    assert np.array_equal(oo2, want_o) and np.array_equal(ii2, want_i)
+    net.close()

@@ -154,3 +154,23 @@ def test_plan_rejects_bad_input():
 def test_plan_empty_network():
     P = Plan(np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64))
     assert P.info["n"] == 0
+
+
+@pytest.mark.parametrize("rows,n", [(1, 1), (1, 7), (3, 1000), (2, 190_001), (5, 0)])
+def test_host_digest_matches_restatement(rows, n):
+    """mc_host_digest (the edit detector of the drop-in API's fused horizons, also formed on the
+    device for every fetched row) equals its NumPy restatement, with NaN / Inf / -0.0 rows."""
+    from api_helpers import digest_rows
+    from tx_fast_hydrology_amd import engine
+    rng = np.random.default_rng(rows * 7 + n)
+    a = rng.normal(0, 10, (rows, n))
+    if n > 3:
+        a[0, :3] = [np.nan, -np.inf, -0.0]
+    got = engine.host_digest(a)
+    assert got.dtype == np.uint64 and got.shape == (rows,)
+    assert np.array_equal(got, digest_rows(a) if n else np.zeros(rows, np.uint64))
+    if n:
+        b = a.copy()
+        b[-1, n // 2] = np.nextafter(b[-1, n // 2], np.inf)   # one ulp in one element
+        assert engine.host_digest(b)[-1] != got[-1]
+        assert np.array_equal(engine.host_digest(b)[:-1], got[:-1])

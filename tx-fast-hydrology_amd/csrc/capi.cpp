@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -12,6 +15,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "analysis.hpp"
@@ -228,6 +232,8 @@ struct Net {
             if (ps.ev) (void)hipEventDestroy(ps.ev);
         }
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
+        if (fetch_pending > 0 && stream) (void)hipStreamSynchronize(stream);
+        for (hipEvent_t e : fetch_ev) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
     }
 
@@ -546,11 +552,21 @@ struct Net {
     }
 
     // this rank's reach slice of ALL members (Xs [Et][S]) + all members' gauge values / innovations
-    // ([Et][m]) -> the slice of the increments G = A Z (Gs [Et][S]);  Et = E * N
+    // ([Et][m]) -> the slice of the increments G = A Z (Gs [Et][S]);  Et = E * N.  Two halves:
+    // the weights Z need only the gathered gauge data, so a caller can form them while the
+    // member -> slice all-to-all of Xs is still in flight (ensemble.py)
     void ens_slice_update(int64_t N, int64_t m, const double* Xs, const double* HXall,
                           const double* Dall, const double* R, double* Gs) {
-        REQUIRE(N >= 1 && m >= 1 && Xs && HXall && Dall && R && Gs, "bad update arguments");
-        const int64_t Et = E * N, S = slice_size(N);
+        ens_weights(N, m, HXall, Dall, R);
+        ens_increments(N, Xs, Gs);
+    }
+    // the analysis weights Z [Et][Et] (kept in the session's buffers for ens_increments)
+    const double* Zw = nullptr;
+    int64_t Zld = 0, Zet = 0;
+    void ens_weights(int64_t N, int64_t m, const double* HXall, const double* Dall,
+                     const double* R) {
+        REQUIRE(N >= 1 && m >= 1 && HXall && Dall && R, "bad weight arguments");
+        const int64_t Et = E * N;
         REQUIRE(Et >= 2, "the ensemble analysis needs at least 2 members");
         const double inv = 1.0 / (double)(Et - 1);
         // gauge anomalies HA = HX - mean over members
@@ -600,6 +616,17 @@ struct Net {
             Z = Zn.p;
             ldz = Et;
         }
+        Zw = Z;
+        Zld = ldz;
+        Zet = Et;
+    }
+    void ens_increments(int64_t N, const double* Xs, double* Gs) {
+        REQUIRE(N >= 1 && Xs && Gs, "bad increment arguments");
+        const int64_t Et = E * N, S = slice_size(N);
+        REQUIRE(Zw != nullptr && Zet == Et,
+                "mc_ens_increments: no analysis weights of this ensemble (mc_ens_weights first)");
+        const double* Z = Zw;
+        const int64_t ldz = Zld;
         // slice increments G = A Z (= K D per member): one fused pass for the per-GPU ensemble
         // sizes, the 128 x 128 MFMA tile with the member mean folded in beyond (dense.hip)
         if (Et <= mcr::kFusedIncrementsMax)
@@ -1025,6 +1052,68 @@ struct Net {
         }
     }
 
+    // ---- asynchronous fetches (mc_fetch_outputs_async / mc_fetch_wait): the drop-in API yields
+    // the steps of a block while the next blocks are still being copied.  Each call gathers the
+    // block's outflows and inflows into their own scratch, forms their row digests and queues
+    // the copies; a ticket (an event) marks the end.  Scratch is reused stream-ordered: the next
+    // block's gathers run after this block's copies.
+    DBuf<double> outT2;
+    DBuf<uint64_t> dig;
+    std::vector<hipEvent_t> fetch_ev;     // ticket -> event
+    std::vector<char> fetch_live;
+    int64_t fetch_pending = 0;
+    int64_t fetch_async(int64_t t0, int64_t t1, double* oo, double* io, uint64_t* dgo,
+                        uint64_t* dgi) {
+        settle();
+        REQUIRE(T_out > 0, "no outputs: call mc_run first");
+        REQUIRE(0 <= t0 && t0 <= t1 && t1 <= T_out, "step range out of bounds");
+        const int64_t n = plan.n, k = t1 - t0;
+        const size_t cells = (size_t)std::max<int64_t>(n * k * E, 1);
+        if ((outT.cap < cells || outT2.cap < cells || dig.cap < (size_t)(2 * k)) &&
+            fetch_pending > 0)
+            HIPC(hipStreamSynchronize(stream));   // a pending copy may still read the scratch
+        outT.reserve(cells);
+        outT2.reserve(cells);
+        dig.reserve((size_t)std::max<int64_t>(2 * k, 1));
+        for (int c = 0; c < 2 && n > 0 && k > 0; ++c) {
+            double* dst = c == 0 ? oo : io;
+            uint64_t* dg = c == 0 ? dgo : dgi;
+            if (!dst && !dg) continue;
+            double* buf = c == 0 ? outT.p : outT2.p;
+            if (out_io)
+                HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, buf, n, E, stream));
+            else
+                HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
+                                              c == 1, row_width(), buf, n, t0, t1, E, stream));
+            if (dg) {
+                HIPC(mcr::launch_row_digests(buf, k, n * E, dig.p + c * k, stream));
+                HIPC(hipMemcpyAsync(dg, dig.p + c * k, (size_t)k * sizeof(uint64_t),
+                                    hipMemcpyDeviceToHost, stream));
+            }
+            if (dst)
+                HIPC(hipMemcpyAsync(dst, buf, (size_t)(n * k * E) * sizeof(double),
+                                    hipMemcpyDeviceToHost, stream));
+        }
+        int64_t t = 0;
+        while (t < (int64_t)fetch_ev.size() && fetch_live[t]) ++t;
+        if (t == (int64_t)fetch_ev.size()) {
+            hipEvent_t e;
+            HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            fetch_ev.push_back(e);
+            fetch_live.push_back(0);
+        }
+        HIPC(hipEventRecord(fetch_ev[t], stream));
+        fetch_live[t] = 1;
+        ++fetch_pending;
+        return t;
+    }
+    void fetch_wait(int64_t t) {
+        REQUIRE(t >= 0 && t < (int64_t)fetch_ev.size() && fetch_live[t], "unknown fetch ticket");
+        fetch_live[t] = 0;
+        --fetch_pending;
+        HIPC(hipEventSynchronize(fetch_ev[t]));
+    }
+
     void fetch_series(double* oo, double* io) {
         settle();
         REQUIRE(T_out > 0, "no outputs: call mc_run first");
@@ -1052,6 +1141,103 @@ Net* as_net(void* h) {
     if (!h) throw Fail(MC_E_INVALID, "null session handle");
     return static_cast<Net*>(h);
 }
+
+// Host row digests (mc_host_digest): the device's row_digests sum, formed over column blocks
+// by a small persistent pool.  The drop-in API checks two Texas rows (3 MB) after every yielded
+// step; workers spin briefly between jobs (the next step's check follows within ~0.1 ms), then
+// sleep on a condition variable.
+class DigestPool {
+  public:
+    static DigestPool& get() {
+        static DigestPool pool;
+        return pool;
+    }
+    void run(const double* a, int64_t nrows, int64_t n, uint64_t* out) {
+        std::lock_guard<std::mutex> call(call_mu_);
+        const int parts = (nrows * n < (1 << 15) || workers_.empty())
+                              ? 1 : (int)workers_.size() + 1;
+        a_ = a;
+        nrows_ = nrows;
+        n_ = n;
+        parts_ = parts;
+        partial_.assign((size_t)parts * (size_t)nrows, 0);
+        if (parts > 1) {
+            pending_.store(parts - 1, std::memory_order_relaxed);
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                gen_.fetch_add(1, std::memory_order_release);
+            }
+            cv_.notify_all();
+        }
+        block(0);
+        while (parts > 1 && pending_.load(std::memory_order_acquire) != 0) {
+        }
+        for (int64_t r = 0; r < nrows; ++r) {
+            uint64_t h = 0;
+            for (int p = 0; p < parts; ++p) h += partial_[(size_t)p * nrows + r];
+            out[r] = h;
+        }
+    }
+    ~DigestPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        for (std::thread& t : workers_) t.join();
+    }
+
+  private:
+    DigestPool() {
+        int want = 8;
+        if (const char* e = std::getenv("MCR_DIGEST_THREADS")) want = std::atoi(e);
+        else if (const char* e2 = std::getenv("OMP_NUM_THREADS")) want = std::min(8, std::atoi(e2));
+        const int hw = (int)std::thread::hardware_concurrency();
+        want = std::max(1, std::min(want, hw > 0 ? hw : 1));
+        for (int t = 1; t < want; ++t) workers_.emplace_back([this, t] { work(t); });
+    }
+    void block(int p) {
+        const int64_t j0 = n_ * p / parts_, j1 = n_ * (p + 1) / parts_;
+        for (int64_t r = 0; r < nrows_; ++r) {
+            const uint64_t* row = reinterpret_cast<const uint64_t*>(a_ + r * n_);
+            uint64_t h = 0;
+            for (int64_t j = j0; j < j1; ++j) h += mcr::digest_term(row[j], (uint64_t)j);
+            partial_[(size_t)p * nrows_ + r] = h;
+        }
+    }
+    void work(int p) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g = gen_.load(std::memory_order_acquire);
+            if (g == seen) {
+                const auto t0 = std::chrono::steady_clock::now();
+                while ((g = gen_.load(std::memory_order_acquire)) == seen &&
+                       std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(300)) {
+                }
+                if (g == seen) {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                    g = gen_.load(std::memory_order_acquire);
+                }
+            }
+            seen = g;
+            if (stop_) return;
+            if (p < parts_) block(p);
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_;
+    std::vector<std::thread> workers_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    bool stop_ = false;
+    const double* a_ = nullptr;
+    int64_t nrows_ = 0, n_ = 0;
+    int parts_ = 1;
+    std::vector<uint64_t> partial_;
+};
 
 // cache for the stateless mc_ax_bu_f64 mirror: recompiled only when the topology changes
 struct AxBuCache {
@@ -1215,6 +1401,15 @@ int mc_ens_slice_update(void* net, int64_t nranks, int64_t m, const double* Xs,
     return guarded([&] { as_net(net)->ens_slice_update(nranks, m, Xs, HXall, Dall, R, Gs); });
 }
 
+int mc_ens_weights(void* net, int64_t nranks, int64_t m, const double* HXall,
+                   const double* Dall, const double* R) {
+    return guarded([&] { as_net(net)->ens_weights(nranks, m, HXall, Dall, R); });
+}
+
+int mc_ens_increments(void* net, int64_t nranks, const double* Xs, double* Gs) {
+    return guarded([&] { as_net(net)->ens_increments(nranks, Xs, Gs); });
+}
+
 int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv) {
     return guarded([&] { as_net(net)->ens_unpack_apply(nranks, Grecv); });
 }
@@ -1336,6 +1531,31 @@ int mc_run(void* net, int64_t T, const double* x) {
 
 int mc_fetch_outputs(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i) {
     return guarded([&] { as_net(net)->fetch(t0, t1, out_o, out_i); });
+}
+
+int mc_fetch_outputs_async(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i,
+                           uint64_t* digest_o, uint64_t* digest_i, int64_t* ticket) {
+    return guarded([&] {
+        REQUIRE(ticket, "ticket must not be NULL");
+        *ticket = as_net(net)->fetch_async(t0, t1, out_o, out_i, digest_o, digest_i);
+    });
+}
+
+int mc_fetch_wait(void* net, int64_t ticket) {
+    return guarded([&] { as_net(net)->fetch_wait(ticket); });
+}
+
+int mc_host_digest(const double* rows, int64_t nrows, int64_t n, uint64_t* out) {
+    return guarded([&] {
+        REQUIRE(nrows >= 0 && n >= 0 && (nrows == 0 || (out && (n == 0 || rows))),
+                "bad digest arguments");
+        if (nrows == 0) return;
+        if (n == 0) {
+            std::fill(out, out + nrows, 0);
+            return;
+        }
+        DigestPool::get().run(rows, nrows, n, out);
+    });
 }
 
 int mc_fetch_series(void* net, double* out_o, double* out_i) {

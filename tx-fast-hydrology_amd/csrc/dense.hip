@@ -5,8 +5,9 @@
 //  * slice_increments: G = (X - mean_e X) Z for a member-major reach slice X [Et][S] and the
 //    Et x Et analysis weights Z -- the largest product of the analysis (S x Et x Et,
 //    2 S Et^2 flops).  128 x 128 output tiles, 4 waves of 64 x 64, K slices double-buffered in
-//    LDS, the member mean folded in as a rank-1 epilogue correction (G = X Z - xbar zs^T) so
-//    X is read once and no anomaly array is materialised.
+//    LDS, the member mean folded in as a rank-1 epilogue correction (G = X' Z - xbar' zs^T with
+//    X' = X shifted by member 0 of each slot, so the products are spread-sized) so X is read once
+//    and no anomaly array is materialised.
 //  * SPD solves B := A^-1 B by block Gauss-Jordan elimination with 32 x 32 pivot blocks on the
 //    augmented system [A | B]: step J eliminates block column J from every other block row
 //    (A_IC -= A_IJ S_J A_JC, B_I -= A_IJ S_J B_J, S_J = D_J^-1 the inverse of the pivot block),
@@ -81,6 +82,16 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
         double z[8], x[2 * NXP];
     };
     double zsum = 0.0, xs0 = 0.0, xs1 = 0.0;     // partial sums for zs[e] and the mean of X
+    // X is staged shifted by member 0's value of its slot (X - x0 1^T): the rank-1 mean
+    // correction then works on spread-sized numbers, so reaches whose members agree get
+    // increments of exactly 0 and a large mean with a small spread loses no digits (ADVICE r3;
+    // the increments are (X - x0 1^T) Z - (xbar - x0) zs^T = (X - xbar 1^T) Z exactly in reals)
+    const auto x0r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(X), (short)0,
+                                                       (int)(S * 8), 0x00020000);
+    const double x0a = __builtin_bit_cast(
+        double, __builtin_amdgcn_raw_buffer_load_b64(x0r, (unsigned)(gd * 8), 0, 0));
+    const double x0b = __builtin_bit_cast(
+        double, __builtin_amdgcn_raw_buffer_load_b64(x0r, (unsigned)(gd * 8 + 8), 0, 0));
     // buffer loads: an out-of-range offset (or an empty record) reads 0, so the edge masks are
     // offsets, not branches around the loads
     const int zrec = (int)(ldz * (int64_t)Et * 8);          // < 2^31 (launcher)
@@ -106,7 +117,7 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
                 double, __builtin_amdgcn_raw_buffer_load_b64(xr, (unsigned)(gd * 8 + 8), 0, 0));
         }
     };
-    auto stage = [&](const Slice& r, int buf) {
+    auto stage = [&](const Slice& r, int buf, int fb) {
         double* As = sm + buf * kStage;           // As[f][e]
         double* Bs = As + kGK * kGM;              // Bs[f][d]
 #pragma unroll
@@ -117,9 +128,12 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
 #pragma unroll
         for (int p = 0; p < NXP; ++p) {
             const int f = xf + XF * p;
-            *reinterpret_cast<double2*>(Bs + f * kGN + xd) = make_double2(r.x[2 * p], r.x[2 * p + 1]);
-            xs0 += r.x[2 * p];
-            xs1 += r.x[2 * p + 1];
+            const bool live = fb + f < Et;          // wave-uniform; rows past Et stage 0
+            const double v0 = live ? r.x[2 * p] - x0a : 0.0;
+            const double v1 = live ? r.x[2 * p + 1] - x0b : 0.0;
+            *reinterpret_cast<double2*>(Bs + f * kGN + xd) = make_double2(v0, v1);
+            xs0 += v0;
+            xs1 += v1;
         }
     };
 
@@ -149,12 +163,12 @@ __global__ __launch_bounds__(128 * MW, MW == 2 ? 2 : 1) void slice_increments(
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(a[i], bb[j], acc[i][j]);
         }
-        if (f0 + kGK < Et) stage(next, buf ^ 1);
+        if (f0 + kGK < Et) stage(next, buf ^ 1, f0 + kGK);
         __syncthreads();
     };
     Slice ra, rb;
     load(ra, 0);
-    stage(ra, 0);
+    stage(ra, 0, 0);
     __syncthreads();
     load(ra, kGK);
     for (int f0 = 0; f0 < Et; f0 += 2 * kGK) {

@@ -543,6 +543,32 @@ hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase
     return hipGetLastError();
 }
 
+// one workgroup per row: strided partial sums, then an LDS tree (sums mod 2^64 are exact, so
+// the order does not matter)
+__global__ __launch_bounds__(256) void row_digests(const double* __restrict__ rows, int64_t n,
+                                                   uint64_t* __restrict__ out) {
+    __shared__ uint64_t part[256];
+    const double* row = rows + (int64_t)blockIdx.x * n;
+    uint64_t h = 0;
+    for (int64_t j = threadIdx.x; j < n; j += 256)
+        h += digest_term((uint64_t)__double_as_longlong(row[j]), (uint64_t)j);
+    part[threadIdx.x] = h;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = part[0];
+}
+
+hipError_t launch_row_digests(const double* rows, int64_t nrows, int64_t n, uint64_t* out,
+                              hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    if (nrows > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(row_digests, dim3((unsigned)nrows), 256, 0, s, rows, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbase,
                                 const int64_t* in_off, const int64_t* in_list, bool inflow,
                                 int slots, double* out, int64_t n, int64_t T, int64_t E,

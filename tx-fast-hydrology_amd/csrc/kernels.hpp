@@ -213,6 +213,22 @@ hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase
                                int slots, double* out, int64_t n, int64_t t0, int64_t t1,
                                int64_t E, hipStream_t s);
 // reach-major out[j][t][e] for t in [0, T)
+// Row digest of fetched outputs (edit detection of the drop-in API's fused horizons,
+// mc_fetch_outputs_async / mc_host_digest): the sum mod 2^64 over j of
+//     t = (bits(row[j]) ^ (j * K1)) * K2;  t ^ (t >> 29)
+// The term is a bijection of the element's bits for a fixed j, so changing any one element
+// always changes the digest; the sum is order-free, so the device (one workgroup per row) and
+// the host (threads over column blocks) form the same value.
+constexpr uint64_t kDigestK1 = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kDigestK2 = 0xD6E8FEB86659FD93ull;
+__host__ __device__ inline uint64_t digest_term(uint64_t bits, uint64_t j) {
+    uint64_t t = (bits ^ (j * kDigestK1)) * kDigestK2;
+    return t ^ (t >> 29);
+}
+// out[r] = digest of row r of rows [nrows][n] (row stride n)
+hipError_t launch_row_digests(const double* rows, int64_t nrows, int64_t n, uint64_t* out,
+                              hipStream_t s);
+
 hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbase,
                                 const int64_t* in_off, const int64_t* in_list, bool inflow,
                                 int slots, double* out, int64_t n, int64_t T, int64_t E,

@@ -255,6 +255,16 @@ class RoutingNet:
             ctypes.c_void_p(HXall.data_ptr()), ctypes.c_void_p(Dall.data_ptr()), ptr(RR),
             ctypes.c_void_p(Gs.data_ptr())))
 
+    def ens_weights(self, nranks, m, HXall, Dall, R):
+        RR = f64(R)
+        nat.check(nat.lib().mc_ens_weights(
+            self._h, int(nranks), int(m), ctypes.c_void_p(HXall.data_ptr()),
+            ctypes.c_void_p(Dall.data_ptr()), ptr(RR)))
+
+    def ens_increments(self, nranks, Xs, Gs):
+        nat.check(nat.lib().mc_ens_increments(self._h, int(nranks), ctypes.c_void_p(Xs.data_ptr()),
+                                              ctypes.c_void_p(Gs.data_ptr())))
+
     def ens_unpack_apply(self, nranks, Grecv):
         nat.check(nat.lib().mc_ens_unpack_apply(self._h, int(nranks),
                                                 ctypes.c_void_p(Grecv.data_ptr())))
@@ -279,6 +289,33 @@ class RoutingNet:
         out_i = np.empty(self._shape(t1 - t0))
         nat.check(nat.lib().mc_fetch_outputs(self._h, t0, t1, ptr(out_o), ptr(out_i)))
         return out_o, out_i
+
+    def fetch_outputs_async(self, t0, t1, out_o, out_i, digest_o=None, digest_i=None) -> int:
+        """Queue the copy of steps [t0, t1) into the host arrays out_o / out_i ([t1 - t0, n(, E)]
+        float64, C-contiguous; pinned memory for an asynchronous full-speed copy) and their row
+        digests (uint64 [t1 - t0], see host_digest).  Returns a ticket; the arrays are complete
+        after fetch_wait(ticket)."""
+        shape = self._shape(t1 - t0)
+        for a in (out_o, out_i):
+            if a is not None and (a.dtype != np.float64 or a.shape != shape or
+                                  not a.flags.c_contiguous):
+                raise ValueError(f"output arrays must be C-contiguous float64 {shape}")
+        for d in (digest_o, digest_i):
+            if d is not None and (d.dtype != np.uint64 or d.shape != (t1 - t0,) or
+                                  not d.flags.c_contiguous):
+                raise ValueError(f"digest arrays must be C-contiguous uint64 [{t1 - t0}]")
+        ticket = ctypes.c_int64()
+        nat.check(nat.lib().mc_fetch_outputs_async(self._h, int(t0), int(t1), ptr(out_o),
+                                                   ptr(out_i), ptr(digest_o), ptr(digest_i),
+                                                   ctypes.byref(ticket)))
+        # the buffers must outlive the queued copies
+        self._fetching = getattr(self, "_fetching", {})
+        self._fetching[ticket.value] = (out_o, out_i, digest_o, digest_i)
+        return ticket.value
+
+    def fetch_wait(self, ticket: int):
+        nat.check(nat.lib().mc_fetch_wait(self._h, int(ticket)))
+        self._fetching.pop(int(ticket), None)
 
     def fetch_series(self):
         """Reach-major host copies (O[j][t](e), I[j][t](e)) of the last run."""
@@ -353,6 +390,19 @@ class RoutingNet:
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
+
+
+def host_digest(a) -> np.ndarray:
+    """Row digests (uint64) of a C-contiguous float64 array [rows, n] (a 1-D array is one row):
+    the value mc_fetch_outputs_async forms on the device for the same row (mcroute.h
+    mc_host_digest).  Host code, no GPU needed."""
+    if a.dtype != np.float64 or not a.flags.c_contiguous:
+        raise ValueError("host_digest needs a C-contiguous float64 array")
+    rows = 1 if a.ndim == 1 else a.shape[0]
+    n = a.size // max(rows, 1) if rows else 0
+    out = np.empty(rows, dtype=np.uint64)
+    nat.check(nat.lib().mc_host_digest(ptr(a), rows, n, ptr(out)))
+    return out
 
 
 def probe_tick_floor(slots=192, chain=2, ticks=8192) -> float:

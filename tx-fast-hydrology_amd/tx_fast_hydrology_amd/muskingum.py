@@ -40,26 +40,114 @@ OPTIONAL_FIELDS = frozenset({"paths", "dx"})
 
 _log = logging.getLogger(__name__)
 
-# Largest number of state values (steps x reaches) one fused horizon call keeps on the host:
-# 2 arrays x 8 B x 2^25 = 512 MiB of fetched outputs per chunk.
+# Largest number of state values (steps x reaches) one fused device call routes before its
+# outputs are fetched: 2 arrays x 8 B x 2^25 = 512 MiB of outputs per chunk.
 _HORIZON_CHUNK_VALUES = 1 << 25
-
-
-try:
-    import xxhash as _xxhash
-except ImportError:       # pragma: no cover - the image ships xxhash; keep the mirror importable
-    _xxhash = None
-
-
-def _digest(a):
-    """Content digest of a fetched state row (C-contiguous float64): the fused horizon's edit
-    detector (one read of the row instead of a copy plus a full comparison)."""
-    return _xxhash.xxh3_128_intdigest(memoryview(a).cast("B"))
+# Steps of a chunk are fetched in blocks of about this many values per array (32 MiB): the
+# first block's steps are yielded while the later blocks are still being copied.
+_FETCH_BLOCK_VALUES = 1 << 22
 
 
 def _fire(callbacks, hook):
     for callback in list(callbacks.values()):
         getattr(callback, hook)()
+
+
+class _CoefArray(np.ndarray):
+    """A model's alpha / beta / chi / gamma (reference ``muskingum.py:332-360``): a plain float64
+    array that counts writes.  The reference reads the coefficients at every step
+    (``muskingum.py:450-453``), so a fused horizon must notice a change made between two yields
+    (``set_transmissive_boundary``, ``compute_muskingum_coeffs``, ``model.alpha[j] = ...``,
+    ``model.beta *= ...``, ``np.copyto(model.chi, ...)``) and route the rest step by step.
+    Element writes, in-place ufuncs, ``ufunc.at`` and the in-place array methods and functions
+    bump the shared revision counter ``_rev`` (views share it).  Results of other operations are
+    plain arrays."""
+
+    _rev = None
+
+    def __array_finalize__(self, obj):
+        self._rev = getattr(obj, "_rev", None)
+
+    def _touch(self):
+        if self._rev is not None:
+            self._rev[0] += 1
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        self._touch()
+
+    def __array_ufunc__(self, ufunc, method, *inputs, out=None, **kwargs):
+        args = [x.view(np.ndarray) if isinstance(x, _CoefArray) else x for x in inputs]
+        if out is not None:
+            kwargs["out"] = tuple(o.view(np.ndarray) if isinstance(o, _CoefArray) else o
+                                  for o in out)
+        result = getattr(ufunc, method)(*args, **kwargs)
+        if method == "at" and isinstance(inputs[0], _CoefArray):
+            inputs[0]._touch()
+        if out is not None:
+            for o in out:
+                if isinstance(o, _CoefArray):
+                    o._touch()
+            return out[0] if len(out) == 1 else out
+        return result
+
+    def __array_function__(self, func, types, args, kwargs):
+        if func in _COEF_INPLACE_FUNCS and args and isinstance(args[0], _CoefArray):
+            args[0]._touch()
+        return super().__array_function__(func, types, args, kwargs)
+
+    def fill(self, value):
+        super().fill(value)
+        self._touch()
+
+    def put(self, *a, **k):
+        super().put(*a, **k)
+        self._touch()
+
+    def sort(self, *a, **k):
+        super().sort(*a, **k)
+        self._touch()
+
+    def partition(self, *a, **k):
+        super().partition(*a, **k)
+        self._touch()
+
+    def __reduce__(self):
+        # pickles / copies as a plain array; the owning model re-wraps it (_own_coefs)
+        return self.view(np.ndarray).__reduce__()
+
+    def __deepcopy__(self, memo):
+        return np.array(self.view(np.ndarray), copy=True)
+
+
+_COEF_INPLACE_FUNCS = frozenset({np.copyto, np.put, np.place, np.putmask, np.fill_diagonal,
+                                 np.put_along_axis})
+
+
+def _coef_property(name):
+    attr = "_" + name
+
+    def fget(self):
+        return self.__dict__.get(attr)
+
+    def fset(self, value):
+        self.__dict__[attr] = self._coef_view(value)
+
+    return property(fget, fset, doc=f"Muskingum coefficient {name} (per reach; tracked writes)")
+
+
+def _host_array(shape, dtype):
+    """Host array for fetched outputs: pinned (torch's caching host allocator, so a block freed
+    by the caller is reused by the next horizon without a new page-locking) when a GPU is
+    present, so the device copies run asynchronously at full PCIe speed."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            tdt = {np.dtype(np.float64): torch.float64, np.dtype(np.uint64): torch.uint64}
+            return torch.empty(shape, dtype=tdt[np.dtype(dtype)], pin_memory=True).numpy()
+    except (ImportError, KeyError, RuntimeError, TypeError):
+        pass
+    return np.empty(shape, dtype=dtype)
 
 
 class _DeviceRouting:
@@ -112,6 +200,11 @@ class Muskingum:
     Texas scale.
     """
 
+    alpha = _coef_property("alpha")
+    beta = _coef_property("beta")
+    chi = _coef_property("chi")
+    gamma = _coef_property("gamma")
+
     def __init__(self, data, load_optional=True, create_state_space=False, sparse=False):
         self.sparse = sparse
         self.callbacks = {}
@@ -153,6 +246,7 @@ class Muskingum:
     def __setstate__(self, state):
         self.__dict__.update(state)
         self._device = _DeviceRouting()
+        self._own_coefs()
 
     def __deepcopy__(self, memo):
         clone = self.__class__.__new__(self.__class__)
@@ -160,9 +254,26 @@ class Muskingum:
         for key, value in self.__dict__.items():
             if key == "_device":
                 continue
-            setattr(clone, key, copy.deepcopy(value, memo))
+            clone.__dict__[key] = copy.deepcopy(value, memo)
         clone._device = _DeviceRouting()
+        clone._own_coefs()
         return clone
+
+    # -- coefficient write tracking (see _CoefArray) ------------------------------------------
+    def _coef_view(self, value):
+        rev = self.__dict__.setdefault("_coef_rev", [0])
+        rev[0] += 1
+        v = np.asarray(value).view(_CoefArray)
+        v._rev = rev
+        return v
+
+    def _own_coefs(self):
+        """A revision counter of this model's own (after a copy or unpickling)."""
+        self.__dict__["_coef_rev"] = [0]
+        for name in ("alpha", "beta", "chi", "gamma"):
+            a = self.__dict__.get("_" + name)
+            if a is not None:
+                setattr(self, name, a)
 
     def close(self):
         """Release the device session (it is recreated by the next routing call)."""
@@ -414,7 +525,8 @@ class Muskingum:
         yielding fresh writable copies of the fetched outputs.  Editing a state array in place,
         replacing it, rebinding ``datetime`` or binding a non-idle callback between two yields
         switches the rest of the horizon to step-by-step routing from the state found, as the
-        reference would route it.  Coefficients and topology are read when a fused call starts.
+        reference would route it; so does changing a coefficient array (``_CoefArray`` counts
+        writes).  Topology is read when a fused call starts.
         """
         assert isinstance(dataframe.index, pd.DatetimeIndex)
         assert dataframe.index.tz == _dt.timezone.utc
@@ -466,43 +578,67 @@ class Muskingum:
             xs.append(float(t.value))
         if not xs:
             return
+        from . import engine
         net = self._device.session(self)
         net.load_forcing(xp, np.ascontiguousarray(dataframe.values, dtype=np.float64))
         net.set_state(self.o_t_next, self.i_t_next)
-        chunk = max(1, _HORIZON_CHUNK_VALUES // max(self.n, 1))
+        n, T = self.n, len(xs)
+        chunk = max(1, _HORIZON_CHUNK_VALUES // max(n, 1))
+        block = max(1, _FETCH_BLOCK_VALUES // max(n, 1))
         timedelta = self.timedelta
-        for c0 in range(0, len(xs), chunk):
-            x = np.asarray(xs[c0:c0 + chunk])
-            net.run(x)
-            out_o, out_i = net.fetch_outputs()
-            for k in range(x.size):
-                # a writable array of its own each step, as the reference allocates them
-                # (nutils.py:68-70): row k of the freshly fetched chunk (no other step and no
-                # later fetch shares its memory).  A caller may edit it in place
-                # (state.o_t_next[j] = obs) or replace it; either is detected below (identity,
-                # and the content digest taken before the yield) and the rest of the horizon is
-                # routed step by step from the state found
-                o_next, i_next = out_o[k], out_i[k]
-                if _xxhash is not None:
-                    sig = (_digest(o_next), _digest(i_next))
-                else:
-                    sig = (o_next.copy(), i_next.copy())
-                self.o_t_prev, self.i_t_prev = self.o_t_next, self.i_t_next
-                self.o_t_next, self.i_t_next = o_next, i_next
-                self.datetime += timedelta
-                self.logger.debug(f"Stepped to time {self.datetime}")
-                expected_time = self.datetime
-                yield self
-                if _xxhash is not None:
-                    edited = (_digest(o_next), _digest(i_next)) != sig
-                else:
-                    edited = not (np.array_equal(o_next, sig[0], equal_nan=True) and
-                                  np.array_equal(i_next, sig[1], equal_nan=True))
-                if (self.o_t_next is not o_next or self.i_t_next is not i_next or edited
-                        or not self._callbacks_idle() or self.datetime != expected_time
-                        or self.timedelta != timedelta):
-                    yield from self._simulate_steps(dataframe, xp, end_time, kwargs)
-                    return
+        rev = self._coef_rev[0]
+        pending = []          # fetch tickets not yet waited for
+        try:
+            for c0 in range(0, T, chunk):
+                x = np.asarray(xs[c0:c0 + chunk])
+                net.run(x)
+                # the chunk's steps in blocks: every block's copy (pinned host rows + the
+                # device's row digests) is queued now; the steps of block b are yielded while
+                # blocks b + 1, ... are still being copied
+                blocks = []
+                digests = _host_array((2, x.size), np.uint64)
+                for b0 in range(0, x.size, block):
+                    b1 = min(x.size, b0 + block)
+                    oo = _host_array((b1 - b0, n), np.float64)
+                    ii = _host_array((b1 - b0, n), np.float64)
+                    tk = net.fetch_outputs_async(b0, b1, oo, ii, digests[0, b0:b1],
+                                                 digests[1, b0:b1])
+                    pending.append(tk)
+                    blocks.append((b0, oo, ii, tk))
+                for b0, oo, ii, tk in blocks:
+                    net.fetch_wait(tk)
+                    pending.remove(tk)
+                    for k in range(oo.shape[0]):
+                        # a writable array of its own each step, as the reference allocates
+                        # them (nutils.py:68-70): row k of a freshly fetched block (no other
+                        # step shares its memory).  The last two steps of the horizon are
+                        # copies, so the model's final state keeps no block alive.  A caller
+                        # may edit a yielded array in place (state.o_t_next[j] = obs) or replace
+                        # it, or change a coefficient; either is detected below (identity, the
+                        # row digest the device formed before the copy, the coefficient
+                        # revision) and the rest of the horizon is routed step by step from
+                        # the state found
+                        step = c0 + b0 + k
+                        o_next, i_next = oo[k], ii[k]
+                        if step >= T - 2:
+                            o_next, i_next = o_next.copy(), i_next.copy()
+                        self.o_t_prev, self.i_t_prev = self.o_t_next, self.i_t_next
+                        self.o_t_next, self.i_t_next = o_next, i_next
+                        self.datetime += timedelta
+                        self.logger.debug(f"Stepped to time {self.datetime}")
+                        expected_time = self.datetime
+                        yield self
+                        edited = (engine.host_digest(o_next)[0] != digests[0, b0 + k] or
+                                  engine.host_digest(i_next)[0] != digests[1, b0 + k])
+                        if (self.o_t_next is not o_next or self.i_t_next is not i_next or edited
+                                or self._coef_rev[0] != rev or not self._callbacks_idle()
+                                or self.datetime != expected_time
+                                or self.timedelta != timedelta):
+                            yield from self._simulate_steps(dataframe, xp, end_time, kwargs)
+                            return
+        finally:
+            for tk in pending:
+                net.fetch_wait(tk)
 
     def simulate(self, dataframe, start_time=None, end_time=None, o_t_init=None, **kwargs):
         """Route over a time range; returns the ``simulate_iter`` generator (yields ``self``).

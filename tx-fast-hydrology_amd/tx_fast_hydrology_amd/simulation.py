@@ -179,7 +179,8 @@ def _step_times(model, end_time):
 def _device_dag(sim):
     """Route the collection as a device DAG (module docstring).  Returns False, having changed
     nothing, when the host driver must run it: callbacks bound, a session that is not a device
-    session, an empty horizon, or forcing rows that do not match the upstream horizon."""
+    session, an empty horizon, forcing rows that do not match the upstream horizon, or a
+    sub-basin horizon that was re-routed after its dataflow waits gave up."""
     models = sim.models
     if any(m.callbacks for m in models.values()):
         return False
@@ -224,8 +225,14 @@ def _device_dag(sim):
         net.run(np.array([float(t.value) for t in steps[name]]))
     outs = {name: nets[name].fetch_outputs() for name in runs}
     if any(nets[name].reroutes() != before[name] for name in runs):
-        raise RuntimeError("a sub-basin horizon was re-routed after a dataflow wait gave up; "
-                           "the device DAG's corrections used incomplete outflows")
+        # a horizon whose dataflow waits gave up (the device was shared) was re-routed by its
+        # own session at the fetch, but the corrections its downstream sub-basins took from it
+        # on the device used incomplete outflows (mcroute.h mc_net_lateral_correction).  Nothing
+        # of this pass has reached the models or the frames yet: route the collection with the
+        # host driver instead, which reloads every session's forcing and state
+        logger.warning("device DAG: a sub-basin horizon gave up waiting and was re-routed; "
+                       "routing the collection with the host driver")
+        return False
     for name in runs:
         m, inputs = models[name], sim.inputs[name]
         t0, o0, i0 = start[name]
