@@ -174,3 +174,17 @@ def test_host_digest_matches_restatement(rows, n):
         b[-1, n // 2] = np.nextafter(b[-1, n // 2], np.inf)   # one ulp in one element
         assert engine.host_digest(b)[-1] != got[-1]
         assert np.array_equal(engine.host_digest(b)[:-1], got[:-1])
+
+
+def test_library_needs_no_vendor_blas_or_solver():
+    """Every dense kernel (EnKF analysis, full-covariance KF gain, RTS solve) is the library's
+    own: libmcroute.so links the HIP runtime only (no rocBLAS / rocSOLVER)."""
+    import shutil
+    import subprocess
+
+    from tx_fast_hydrology_amd import _native
+    if shutil.which("ldd") is None:
+        pytest.skip("ldd not available")
+    out = subprocess.run(["ldd", _native.lib_path()], capture_output=True, text=True).stdout
+    assert "libamdhip64" in out
+    assert "rocblas" not in out and "rocsolver" not in out, out

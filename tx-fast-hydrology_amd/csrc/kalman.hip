@@ -18,11 +18,10 @@
 // staged form (ax_columns_staged: everything a level reads is in LDS).
 // Results are bit-identical to the reference walk: same operations, same association, same
 // summation order, FMA contraction off.  The dense update products run on the f64 MFMA GEMM
-// (analysis.hip); the m x m solve is rocSOLVER LU (getrf / getrs), as np.linalg.inv is LU.
+// (analysis.hip); the m x m gain system P-[s, s] + R and the n x n RTS system P_p1 are SPD and
+// are solved by the library's block Gauss-Jordan elimination (dense.hip, launch_spd_solve; no
+// vendor solver).  numpy's inv / solve are LU: results agree to rounding (g5 / g11 tests).
 #include <hip/hip_runtime.h>
-
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
 
 #include <cstdint>
 #include <cstring>
@@ -220,19 +219,47 @@ __global__ void apply_gain_gather(GraphArgs a, const uint8_t* __restrict__ route
 
 // S (column-major m x m) = P[s][:, s] + R (R row-major, as numpy);
 // Bt (column-major m x n) = P[:, s]^T;  Ps (column-major m x n) = P[s, :]
+// Gathers of the KF update for the padded SPD solve (kp = spd_padded(m), column-major):
+//   St (kp x kp) = (P[s, s] + R)^T with an identity block beyond m  (getrs(transpose) of the
+//                  reference's K = P[:, s] inv(P[s, s] + R): K^T solves St Y = P[s, :])
+//   Bt (kp x n)  = P[:, s]^T, padding rows 0;   Ps (m x n) = P[s, :]
 __global__ void kf_gather(const double* __restrict__ P, const int64_t* __restrict__ s,
-                          const double* __restrict__ R, double* __restrict__ S,
+                          const double* __restrict__ R, double* __restrict__ St,
                           double* __restrict__ Bt, double* __restrict__ Ps, int64_t n,
-                          int64_t m) {
+                          int64_t m, int64_t kp) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < kp * n) {
+        const int64_t g = idx % kp, j = idx / kp;
+        Bt[idx] = g < m ? P[j * n + s[g]] : 0.0;
+    }
     if (idx < m * n) {
         const int64_t g = idx % m, j = idx / m;
-        Bt[idx] = P[j * n + s[g]];
         Ps[idx] = P[s[g] * n + j];
     }
-    if (idx < m * m) {
-        const int64_t a = idx % m, b = idx / m;
-        S[idx] = P[s[a] * n + s[b]] + R[a * m + b];
+    if (idx < kp * kp) {
+        const int64_t a = idx % kp, b = idx / kp;
+        St[idx] = (a < m && b < m) ? P[s[b] * n + s[a]] + R[b * m + a] : (a == b ? 1.0 : 0.0);
+    }
+}
+
+// dst (kp x ncols, column-major, ld kp) = the column-major form of the row-major n x n src
+// (dst[i + j kp] = src[i n + j]), `diag` on the diagonal beyond n and 0 elsewhere; 32 x 32
+// tiles through LDS (coalesced on both sides)
+__global__ __launch_bounds__(256) void colmajor_padded(const double* __restrict__ src, int64_t n,
+                                                       double* __restrict__ dst, int64_t kp,
+                                                       int64_t ncols, double diag) {
+    __shared__ double t[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+    const int64_t i0 = (int64_t)blockIdx.x * 32, j0 = (int64_t)blockIdx.y * 32;
+    for (int k = ty; k < 32; k += 8) {                       // rows i0 + k of src, columns j0..
+        const int64_t i = i0 + k, j = j0 + tx;
+        t[k][tx] = (i < n && j < n) ? src[i * n + j] : 0.0;
+    }
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8) {                       // column j0 + k of dst, rows i0..
+        const int64_t j = j0 + k, i = i0 + tx;
+        if (i < kp && j < ncols)
+            dst[i + j * kp] = (i < n && j < n) ? t[tx][k] : (i == j ? diag : 0.0);
     }
 }
 
@@ -261,11 +288,10 @@ struct Cov {
     DBuf<double2> Tm;                  // chain-independent terms of the staged sweep
     DBuf<int4> lvx;                    // staged sweep: {reach, q0, q1, up[q0]} per level slot
     DBuf<int64_t> sdev;
-    DBuf<rocblas_int> ipiv, info;
-    rocblas_handle blas = nullptr;
+    DBuf<double> Sd;                   // pivot-block inverses of the Gauss-Jordan solve
+    DBuf<int32_t> info;
 
     ~Cov() {
-        if (blas) rocblas_destroy_handle(blas);
         if (own) (void)hipStreamDestroy(own);
     }
 
@@ -368,14 +394,6 @@ struct Cov {
         return a;
     }
 
-    rocblas_handle solver() {
-        if (!blas && rocblas_create_handle(&blas) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocblas_create_handle failed");
-        if (rocblas_set_stream(blas, stream) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocblas_set_stream failed");
-        return blas;
-    }
-
     // Y = A X (square n x n, row-major); X and Y must not alias
     void ax(const double* X, double* Y) {
         REQUIRE(coeffs_set, "mc_cov_set_coeffs has not been called");
@@ -433,100 +451,90 @@ struct Cov {
         REQUIRE(m >= 1 && m <= n, "need 1 <= m <= n gauges");
         for (int64_t g = 0; g < m; ++g)
             REQUIRE(s[g] >= 0 && s[g] < n, "gauge index out of range");
-        S.reserve((size_t)m * m);
-        Bt.reserve((size_t)m * n);
+        const int64_t kp = spd_padded(m);
+        S.reserve((size_t)(kp * kp));
+        Bt.reserve((size_t)(kp * n));
         Ps.reserve((size_t)m * n);
+        Sd.reserve((size_t)(kp * 32));
         Rdev.upload(R, (size_t)m * m, stream);
         ddev.upload(dz, (size_t)m, stream);
         sdev.upload(s, (size_t)m, stream);
         gdev.reserve((size_t)std::max<int64_t>(3 * n, 1));
-        ipiv.reserve((size_t)m);
         info.reserve(1);
-        hipLaunchKernelGGL(kf_gather, blocks_for(std::max(m * n, m * m), 256), 256, 0, stream,
-                           Pp, sdev.p, Rdev.p, S.p, Bt.p, Ps.p, n, m);
+        hipLaunchKernelGGL(kf_gather, blocks_for(std::max(kp * n, kp * kp), 256), 256, 0,
+                           stream, Pp, sdev.p, Rdev.p, S.p, Bt.p, Ps.p, n, m, kp);
         HIPC(hipGetLastError());
-        rocblas_handle h = solver();
-        if (rocsolver_dgetrf(h, (rocblas_int)m, (rocblas_int)m, S.p, (rocblas_int)m, ipiv.p,
-                             info.p) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dgetrf failed");
-        // (S^T) Y = P-[:, s]^T  ->  Y = K^T (column-major m x n = K row-major n x m)
-        if (rocsolver_dgetrs(h, rocblas_operation_transpose, (rocblas_int)m, (rocblas_int)n,
-                             S.p, (rocblas_int)m, ipiv.p, Bt.p, (rocblas_int)m) !=
-            rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dgetrs failed");
-        HIPC(launch_dgemm(true, false, n, 1, m, 1.0, Bt.p, m, ddev.p, m, 0.0, gdev.p, n,
+        // St Y = P-[s, :]  ->  Y = K^T (column-major m x n, leading dimension kp)
+        HIPC(launch_spd_solve(S.p, kp, Bt.p, n, Sd.p, info.p, stream));
+        HIPC(launch_dgemm(true, false, n, 1, m, 1.0, Bt.p, kp, ddev.p, m, 0.0, gdev.p, n,
                           stream));
         if (Pq != Pp)
             HIPC(hipMemcpyAsync(Pq, Pp, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice,
                                 stream));
         // column-major view Pc = P^T:  Pc+ = Pc - Ps^T Y
-        HIPC(launch_dgemm(true, false, n, n, m, -1.0, Ps.p, m, Bt.p, m, 1.0, Pq, n, stream));
-        rocblas_int info_h = 0;
-        HIPC(hipMemcpyAsync(&info_h, info.p, sizeof(rocblas_int), hipMemcpyDeviceToHost,
-                            stream));
+        HIPC(launch_dgemm(true, false, n, n, m, -1.0, Ps.p, m, Bt.p, kp, 1.0, Pq, n, stream));
+        int32_t info_h = 0;
+        HIPC(hipMemcpyAsync(&info_h, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         HIPC(hipMemcpyAsync(gain_out, gdev.p, n * sizeof(double), hipMemcpyDeviceToHost,
                             stream));
-        if (K_out)
-            HIPC(hipMemcpyAsync(K_out, Bt.p, (size_t)m * n * sizeof(double),
-                                hipMemcpyDeviceToHost, stream));
+        if (K_out)      // K row-major n x m = Y column-major m x n: drop the padding rows
+            HIPC(hipMemcpy2DAsync(K_out, (size_t)m * sizeof(double), Bt.p,
+                                  (size_t)kp * sizeof(double), (size_t)m * sizeof(double),
+                                  (size_t)n, hipMemcpyDeviceToHost, stream));
         HIPC(hipStreamSynchronize(stream));
         if (info_h != 0)
-            throw Fail(MC_E_STATE, "P-[s, s] + R is singular (getrf info " +
+            throw Fail(MC_E_STATE, "P-[s, s] + R is not positive definite (elimination pivot " +
                                        std::to_string(info_h) + ")");
     }
 
     // RTS step (da.py:241-251): J = (P_p1^-1 A P_f)^T, P_s = P_f + J (P_s1 - P_p1),
     // x_s = x_f + J d for nvec host vectors d = x_s1 - x_p1.  Row-major buffers are read as
-    // column-major transposes: solving with getrs(transpose) on the LU of P_p1's buffer and the
-    // transposed A P_f leaves a buffer whose row-major view is J.
+    // column-major transposes: X = P_p1^-1 (A P_f) in column-major form (padded to kp, SPD block
+    // Gauss-Jordan) is a buffer whose row-major view is J.
     void ks_step(const double* Pf, const double* Pp1, const double* Ps1, double* Ps_out,
                  int64_t nvec, const double* xf, const double* d, double* xs_out) {
         if (n == 0) return;
         REQUIRE(nvec >= 0 && (nvec == 0 || (xf && d && xs_out)), "bad vector arguments");
         const size_t nn = (size_t)n * n;
+        const int64_t kp = spd_padded(n);
         T1.reserve(nn);
-        T2.reserve(nn);
-        T3.reserve(nn);
-        ipiv.reserve((size_t)n);
+        T2.reserve((size_t)(kp * n));
+        T3.reserve((size_t)(kp * kp));
+        Sd.reserve((size_t)(kp * 32));
         info.reserve(1);
-        ax(Pf, T1.p);                                               // A P_f
-        const dim3 tg((unsigned)((n + 31) / 32), (unsigned)((n + 31) / 32));
-        hipLaunchKernelGGL(transpose, tg, 256, 0, stream, T1.p, T2.p, n);
+        ax(Pf, T1.p);                                               // A P_f (row-major)
+        const dim3 tp((unsigned)((kp + 31) / 32), (unsigned)((kp + 31) / 32));
+        const dim3 tb((unsigned)((kp + 31) / 32), (unsigned)((n + 31) / 32));
+        hipLaunchKernelGGL(colmajor_padded, tp, 256, 0, stream, Pp1, n, T3.p, kp, kp, 1.0);
         HIPC(hipGetLastError());
-        HIPC(hipMemcpyAsync(T3.p, Pp1, nn * sizeof(double), hipMemcpyDeviceToDevice, stream));
-        rocblas_handle h = solver();
-        if (rocsolver_dgetrf(h, (rocblas_int)n, (rocblas_int)n, T3.p, (rocblas_int)n, ipiv.p,
-                             info.p) != rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dgetrf failed");
-        if (rocsolver_dgetrs(h, rocblas_operation_transpose, (rocblas_int)n, (rocblas_int)n,
-                             T3.p, (rocblas_int)n, ipiv.p, T2.p, (rocblas_int)n) !=
-            rocblas_status_success)
-            throw Fail(MC_E_HIP, "rocsolver_dgetrs failed");
+        hipLaunchKernelGGL(colmajor_padded, tb, 256, 0, stream, T1.p, n, T2.p, kp, n, 0.0);
+        HIPC(hipGetLastError());
+        HIPC(launch_spd_solve(T3.p, kp, T2.p, n, Sd.p, info.p, stream));   // T2 := X (ld kp)
         hipLaunchKernelGGL(sub_into, blocks_for((int64_t)nn, 256), 256, 0, stream, T1.p, Ps1,
                            Pp1, (int64_t)nn);                      // D = P_s1 - P_p1
         HIPC(hipGetLastError());
         if (Ps_out != Pf)
             HIPC(hipMemcpyAsync(Ps_out, Pf, nn * sizeof(double), hipMemcpyDeviceToDevice,
                                 stream));
-        HIPC(launch_dgemm(false, false, n, n, n, 1.0, T1.p, n, T2.p, n, 1.0, Ps_out, n, stream));
+        HIPC(launch_dgemm(false, false, n, n, n, 1.0, T1.p, n, T2.p, kp, 1.0, Ps_out, n,
+                          stream));
         if (nvec > 0) {
             gdev.reserve((size_t)std::max<int64_t>(2 * nvec * n, 3 * n));
             HIPC(hipMemcpyAsync(gdev.p, d, nvec * n * sizeof(double), hipMemcpyHostToDevice,
                                 stream));
             HIPC(hipMemcpyAsync(gdev.p + nvec * n, xf, nvec * n * sizeof(double),
                                 hipMemcpyHostToDevice, stream));
-            HIPC(launch_dgemm(true, false, n, nvec, n, 1.0, T2.p, n, gdev.p, n, 1.0,
+            HIPC(launch_dgemm(true, false, n, nvec, n, 1.0, T2.p, kp, gdev.p, n, 1.0,
                               gdev.p + nvec * n, n, stream));
             HIPC(hipMemcpyAsync(xs_out, gdev.p + nvec * n, nvec * n * sizeof(double),
                                 hipMemcpyDeviceToHost, stream));
         }
-        rocblas_int info_h = 0;
-        HIPC(hipMemcpyAsync(&info_h, info.p, sizeof(rocblas_int), hipMemcpyDeviceToHost,
-                            stream));
+        int32_t info_h = 0;
+        HIPC(hipMemcpyAsync(&info_h, info.p, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         HIPC(hipStreamSynchronize(stream));
         if (info_h != 0)
-            throw Fail(MC_E_STATE, "the predicted covariance is singular (getrf info " +
-                                       std::to_string(info_h) + ")");
+            throw Fail(MC_E_STATE, "the predicted covariance is not positive definite "
+                                   "(elimination pivot " + std::to_string(info_h) + ")");
     }
 };
 

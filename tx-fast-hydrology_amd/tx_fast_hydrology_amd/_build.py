@@ -6,7 +6,8 @@ lands next to this file (``lib/libmcroute.so``) so it travels with the repositor
 roundings to match the reference bit for bit.
 
 Every source compiles to its own object (``lib/obj/``) in parallel; an object is rebuilt when
-its source or any header is newer, then the objects are linked.
+its source or any header is newer, then the objects are linked.  The library needs only the HIP
+runtime (no rocBLAS / rocSOLVER: every dense kernel is the library's own).
 """
 from __future__ import annotations
 
@@ -28,7 +29,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libmcroute.so")
 ARCH = os.environ.get("MCROUTE_ARCH", "gfx950")
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-function"]
-LIBS = ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
+LIBS = ["-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _hipcc() -> str:
@@ -64,11 +65,20 @@ def _obj(src: str) -> str:
     return os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
 
 
+STAMP_PATH = LIB_PATH + ".stamp"
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB_PATH):
+    """The library is rebuilt when it is missing, when any source or header is newer, or when
+    the build identity changed (a source added or deleted, other flags): the stamp written next
+    to it holds the source_hash() it was built from."""
+    if not os.path.exists(LIB_PATH) or not os.path.exists(STAMP_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(p) > t for p in sources() + _headers())
+    if any(os.path.getmtime(p) > t for p in sources() + _headers()):
+        return True
+    with open(STAMP_PATH) as f:
+        return f.read().strip() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -100,6 +110,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
     os.replace(tmp, LIB_PATH)
+    with open(STAMP_PATH, "w") as f:
+        f.write(source_hash() + "\n")
     return LIB_PATH
 
 
