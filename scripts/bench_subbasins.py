@@ -98,6 +98,7 @@ def main():
     data, df, cuts = build(a.cuts, a.T)
     times = {}
     res = {}
+    phases = None
     for device in (True, False):
         coll = collection(data, cuts, device)
         ts = []
@@ -105,6 +106,8 @@ def main():
             dt, outputs, sim = run(coll, df)
             if r:
                 ts.append(dt)
+                if device and (phases is None or dt <= min(ts)):
+                    phases = {k: round(v, 2) for k, v in getattr(sim, "dag_phases", {}).items()}
         times[device] = min(ts)
         res[device] = (outputs, sim, coll)
     (o_d, s_d, c_d), (o_h, s_h, c_h) = res[True], res[False]
@@ -120,7 +123,8 @@ def main():
                     f"({len(cuts)} cuts), 24 h @ 300 s ({a.T} steps), AsyncSimulation",
         "sub_basins": len(sizes), "largest": sizes[-1], "median": sizes[len(sizes) // 2],
         "device_dag_s": round(times[True], 4), "host_driver_s": round(times[False], 4),
-        "speedup": round(times[False] / times[True], 2), "bit_identical": bool(same)}),
+        "speedup": round(times[False] / times[True], 2), "bit_identical": bool(same),
+        "device_dag_phases_ms": phases}),
         flush=True)
     if not same:
         sys.exit(1)

@@ -103,6 +103,15 @@ class OracleNet:
     def fetch_wait(self, ticket):
         pass
 
+    def add_lateral_correction(self, reach, src, src_reach, o_start, alpha, beta, gamma):
+        """mcroute.h mc_net_lateral_correction: F[r] += alpha I(r+1) / gamma + beta I(r) / gamma
+        with I the source reach's outflow series of its last horizon (I(0) = o_start)."""
+        series = np.concatenate([[o_start], src.out_o[:, src_reach]])
+        self.fp[:, reach] += alpha * series[1:] / gamma + beta * series[:-1] / gamma
+
+    def reroutes(self):
+        return 0
+
     def close(self):
         pass
 

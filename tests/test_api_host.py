@@ -115,6 +115,11 @@ def test_nhd_geojson(tmp_path):
     assert m.indegree.tolist() == [0, 0, 2]
 
 
+class _IdleCb(BaseCallback):
+    def __idle_steps__(self):
+        return True
+
+
 # ------------------------------------------------------------------ routing host logic
 @pytest.mark.parametrize("callback", [False, True])
 def test_simulate_paths_golden(golden, monkeypatch, callback):
@@ -313,14 +318,22 @@ def test_split_topology_golden(golden):
     assert np.array_equal(whole.endnodes, g["endnodes"])
 
 
-def test_async_simulation_golden(golden, monkeypatch):
+@pytest.mark.parametrize("driver", ["device_dag", "host"])
+def test_async_simulation_golden(golden, monkeypatch, driver):
+    """Both AsyncSimulation drivers against the reference's own split + AsyncSimulation run:
+    the device DAG (no callbacks; OracleNet stands in for the sessions and their on-device
+    lateral corrections) and the host driver (an idle callback on every sub-basin)."""
     use_oracle_device(monkeypatch)
     g = golden("g4_split_async.npz")
     whole = golden_model(g)
     df = golden_frame(g, whole.reach_ids)
     coll = whole.split(g["cuts"], create_state_space=False)
+    if driver == "host":
+        for m in coll.models.values():
+            m.bind_callback(_IdleCb(), key="idle")
     sim = AsyncSimulation(coll, df)
     outputs = asyncio.run(sim.simulate())
+    assert hasattr(sim, "dag_phases") == (driver == "device_dag")
     for name in g["names"]:
         p = f"sub{name}_"
         assert np.array_equal(outputs[str(name)].values, g[p + "o"]), name

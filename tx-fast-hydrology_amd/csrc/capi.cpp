@@ -414,13 +414,14 @@ struct Net {
     }
 
     // caller-order host array [n][m] -> member-major slot-order device array [m][nslots]
-    void to_slots(const double* host, DBuf<double>& dst, int64_t m = 1) {
+    void to_slots(const double* host, DBuf<double>& dst, int64_t m = 1,
+                  DBuf<double>* via = nullptr) {
         const int64_t n = plan.n;
         if (n == 0) return;
-        stage.reserve((size_t)(n * m));
-        HIPC(hipMemcpyAsync(stage.p, host, n * m * sizeof(double), hipMemcpyHostToDevice,
-                            stream));
-        HIPC(mcr::launch_scatter_to_slots(stage.p, dst.p, slot_reach.p, plan.nslots, m, stream));
+        DBuf<double>& sb = via ? *via : stage;
+        sb.reserve((size_t)(n * m));
+        HIPC(hipMemcpyAsync(sb.p, host, n * m * sizeof(double), hipMemcpyHostToDevice, stream));
+        HIPC(mcr::launch_scatter_to_slots(sb.p, dst.p, slot_reach.p, plan.nslots, m, stream));
     }
     // Resolve pending dataflow runs (status word, re-run on give-up) before results are read.
     void settle() {
@@ -719,8 +720,7 @@ struct Net {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
         settle_state();
         to_slots(o, st_o, E);
-        sync();
-        to_slots(i, st_i, E);
+        to_slots(i, st_i, E, &stage2);   // its own staging: one synchronisation for both
         sync();
     }
 
@@ -985,12 +985,18 @@ struct Net {
         n_rows = rows;
         F.reserve((size_t)(rows * plan.nslots * E));
         if (n == 0) return;
+        // caller-order staging: kept between calls when small (sub-basin sessions reload their
+        // forcing every horizon; a device allocation per call cost more than the copy)
+        const size_t cells = (size_t)(rows * n * E);
         DBuf<double> tmp;
-        tmp.upload(fp, (size_t)(rows * n * E), stream);
-        HIPC(mcr::launch_forcing_to_slots(tmp.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
+        DBuf<double>& st = cells <= kKeepStage ? fstage : tmp;
+        st.upload(fp, cells, stream);
+        HIPC(mcr::launch_forcing_to_slots(st.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
                                           stream));
         sync();
     }
+    static constexpr size_t kKeepStage = (size_t)1 << 23;   // 64 MiB
+    DBuf<double> fstage, stage2;
 
     void run(int64_t T, const double* x) {
         REQUIRE(n_rows > 0, "mc_load_forcing must be called before mc_run");

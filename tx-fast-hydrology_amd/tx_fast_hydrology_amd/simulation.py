@@ -168,19 +168,41 @@ def _task_order(sim):
     return runs, corrections
 
 
-def _step_times(model, end_time):
-    xs, t = [], model.datetime
-    while t < end_time:
-        t = t + model.timedelta
-        xs.append(t)
-    return xs
+def _step_ns(model, end_time):
+    """Step times of simulate_iter's loop (``while t < end_time: t = t + timedelta``,
+    muskingum.py:527-533) as int64 ns: Timestamp arithmetic is exact integer nanoseconds, so the
+    k-th step is t0 + k * dt for k = 1 .. ceil((end - t0) / dt)."""
+    t0 = int(model.datetime.value)
+    dt = int(model.timedelta.value)
+    end = int(pd.Timestamp(end_time).value)
+    if dt <= 0:
+        raise ValueError("the model timedelta must be positive")
+    k = -(-(end - t0) // dt) if end > t0 else 0
+    return t0 + dt * np.arange(1, k + 1, dtype=np.int64)
+
+
+class _Phases:
+    """Wall-clock breakdown of one device-DAG pass (``AsyncSimulation.dag_phases``)."""
+
+    def __init__(self):
+        import time
+        self._clock = time.perf_counter
+        self._t = self._clock()
+        self.ms = {}
+
+    def __call__(self, name):
+        t = self._clock()
+        self.ms[name] = self.ms.get(name, 0.0) + 1e3 * (t - self._t)
+        self._t = t
 
 
 def _device_dag(sim):
     """Route the collection as a device DAG (module docstring).  Returns False, having changed
     nothing, when the host driver must run it: callbacks bound, a session that is not a device
     session, an empty horizon, forcing rows that do not match the upstream horizon, or a
-    sub-basin horizon that was re-routed after its dataflow waits gave up."""
+    sub-basin horizon that was re-routed after its dataflow waits gave up.  The wall-clock
+    phases of the pass are left in ``sim.dag_phases`` (ms)."""
+    ph = _Phases()
     models = sim.models
     if any(m.callbacks for m in models.values()):
         return False
@@ -192,12 +214,12 @@ def _device_dag(sim):
         inputs = sim.inputs[name]
         if not isinstance(inputs.index, pd.DatetimeIndex) or inputs.index.tz is None:
             return False
-        steps[name] = _step_times(models[name], inputs.index.max())
-        if not steps[name]:
+        steps[name] = _step_ns(models[name], inputs.index.max())
+        if not steps[name].size:
             return False
     for name in runs:
         for link in corrections[name]:
-            if len(sim.inputs[name]) != len(steps[link.upstream_model.name]):
+            if len(sim.inputs[name]) != steps[link.upstream_model.name].size:
                 return False
     nets = {}
     for name in runs:
@@ -205,14 +227,16 @@ def _device_dag(sim):
         if not hasattr(net, "add_lateral_correction"):
             return False
         nets[name] = net
+    ph("sessions")
     before = {name: nets[name].reroutes() for name in runs}
     start = {name: (models[name].datetime, models[name].o_t_next, models[name].i_t_next)
              for name in runs}
     for name in runs:
         m, inputs, net = models[name], sim.inputs[name], nets[name]
-        xp = inputs.index.astype(int).astype(float).values
+        xp = inputs.index.asi8.astype(float)
         net.load_forcing(xp, np.ascontiguousarray(inputs.values, dtype=np.float64))
         net.set_state(m.o_t_next, m.i_t_next)
+    ph("upload")
     # enqueue: corrections then the horizon of every sub-basin, in the reference's order
     for name in runs:
         m, net = models[name], nets[name]
@@ -222,8 +246,23 @@ def _device_dag(sim):
             net.add_lateral_correction(j, nets[up.name], link.upstream_index,
                                        start[up.name][1][link.upstream_index], m.alpha[j],
                                        m.beta[j], m.gamma[j])
-        net.run(np.array([float(t.value) for t in steps[name]]))
-    outs = {name: nets[name].fetch_outputs() for name in runs}
+        net.run(steps[name].astype(float))
+    ph("enqueue")
+    # outflow series straight into the frames' arrays (row 0: the start state); of the inflows
+    # only the last two steps (the final state) are needed
+    series, last_i, tickets = {}, {}, []
+    for name in runs:
+        T = steps[name].size
+        o = np.empty((T + 1, models[name].n))
+        o[0] = start[name][1]
+        k = min(T, 2)
+        li = np.empty((k, models[name].n))
+        tickets.append((nets[name], nets[name].fetch_outputs_async(0, T, o[1:], None)))
+        tickets.append((nets[name], nets[name].fetch_outputs_async(T - k, T, None, li)))
+        series[name], last_i[name] = o, li
+    for net, tk in tickets:
+        net.fetch_wait(tk)
+    ph("fetch")
     if any(nets[name].reroutes() != before[name] for name in runs):
         # a horizon whose dataflow waits gave up (the device was shared) was re-routed by its
         # own session at the fetch, but the corrections its downstream sub-basins took from it
@@ -232,28 +271,36 @@ def _device_dag(sim):
         # host driver instead, which reloads every session's forcing and state
         logger.warning("device DAG: a sub-basin horizon gave up waiting and was re-routed; "
                        "routing the collection with the host driver")
+        sim.dag_phases = ph.ms
         return False
+    indexes = {}
     for name in runs:
         m, inputs = models[name], sim.inputs[name]
         t0, o0, i0 = start[name]
-        out_o, out_i = outs[name]
-        T = len(steps[name])
-        # the state simulate_iter leaves (muskingum.py:458-464 per step)
-        m.o_t_prev, m.i_t_prev = (out_o[-2], out_i[-2]) if T > 1 else (o0, i0)
-        m.o_t_next, m.i_t_next = out_o[-1].copy(), out_i[-1].copy()
-        m.datetime = steps[name][-1]
-        index = pd.to_datetime([t0] + steps[name], utc=True)
-        sim.outputs[name] = pd.DataFrame(np.vstack([o0[None, :], out_o]), index=index,
-                                         columns=inputs.columns)
+        o, li = series[name], last_i[name]
+        T = steps[name].size
+        # the state simulate_iter leaves (muskingum.py:458-464 per step): arrays of its own
+        m.o_t_prev, m.i_t_prev = (o[-2].copy(), li[-2].copy()) if T > 1 else (o0, i0)
+        m.o_t_next, m.i_t_next = o[-1].copy(), li[-1].copy()
+        m.datetime = pd.Timestamp(int(steps[name][-1]), tz="UTC")
+        key = (int(t0.value), T, int(steps[name][0]), int(steps[name][-1]))
+        index = indexes.get(key)
+        if index is None:
+            ns = np.concatenate([[int(t0.value)], steps[name]])
+            index = indexes[key] = pd.DatetimeIndex(ns.view("datetime64[ns]")).tz_localize("UTC")
+        sim.outputs[name] = pd.DataFrame(o, index=index, columns=inputs.columns, copy=False)
+    ph("frames")
     # the corrected input frames, as the reference's += leaves them (same arithmetic)
     for name in runs:
         frame = sim.inputs[name]
         for link in corrections[name]:
             up = link.upstream_model
-            series = sim.outputs[up.name][up.reach_ids[link.upstream_index]]
+            series_ = sim.outputs[up.name][up.reach_ids[link.upstream_index]]
             column = models[name].reach_ids[link.downstream_index]
             frame.loc[:, column] += _lateral_correction(models[name], link.downstream_index,
-                                                        series)
+                                                        series_)
+    ph("corrections")
+    sim.dag_phases = ph.ms
     return True
 
 
