@@ -196,6 +196,9 @@ int mc_step(void* net, const double* o_prev, const double* i_prev, const double*
 /* Forcing table for mc_run: n_rows timestamps xp (float64 ns, sorted) and values fp
  * [n_rows][n] (the simulate_iter DataFrame, muskingum.py:526-531). */
 int mc_load_forcing(void* net, int64_t n_rows, const double* xp, const double* fp);
+/* Same, with the forcing in series layout fp [n][n_rows] ([n][n_rows][E]): the block a pandas
+ * frame of the sub-basin's inputs already holds (simulation.py uploads it without a transpose). */
+int mc_load_forcing_series(void* net, int64_t n_rows, const double* xp, const double* fp);
 /* Horizon of T steps from the session state, all on the device: step t interpolates the
  * forcing at x[t] = float(next_timestep.value) (muskingum.py:528-531) and routes the network.
  * Outputs stay resident (reach-major); the session state becomes the state after step T-1. */

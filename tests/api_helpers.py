@@ -79,6 +79,9 @@ class OracleNet:
     def load_forcing(self, xp, fp):
         self.xp, self.fp = np.array(xp), np.array(fp)
 
+    def load_forcing_series(self, xp, fp_series):
+        self.xp, self.fp = np.array(xp), np.array(np.asarray(fp_series).T)
+
     def set_state(self, o, i):
         self.o, self.i = np.array(o, dtype=np.float64), np.array(i, dtype=np.float64)
 

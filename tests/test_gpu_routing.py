@@ -530,3 +530,21 @@ def test_async_fetch_and_device_digests(n, T, block):
     oo2, ii2 = net.fetch_outputs()
     assert np.array_equal(oo2, want_o) and np.array_equal(ii2, want_i)
     net.close()
+
+
+def test_load_forcing_series_layout():
+    """mc_load_forcing_series (reach-major forcing, a pandas frame's own block) routes exactly as
+    mc_load_forcing with the step-major array."""
+    n, T = 4000, 40
+    end, K, X = _random_case(n, 77, 0.9, 8)
+    indeg, heads, coef, o0, i0 = _model(end, K, X, 300.0, seed=5)
+    xp, fp = synthetic.forcing(n, rows=5, seed=3)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0)
+    net.load_forcing_series(xp, np.ascontiguousarray(fp.T))
+    net.run(x)
+    got_o, got_i = net.fetch_outputs()
+    assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
+    net.close()

@@ -974,7 +974,8 @@ struct Net {
         T_out = T;
     }
 
-    void load_forcing(int64_t rows, const double* xps, const double* fp) {
+    void load_forcing(int64_t rows, const double* xps, const double* fp,
+                      bool reach_major = false) {
         REQUIRE(rows >= 1 && rows < (1ll << 31), "n_rows must be >= 1");
         REQUIRE(xps && (plan.n == 0 || fp), "xp/fp must not be NULL");
         for (int64_t r = 1; r < rows; ++r)
@@ -992,7 +993,7 @@ struct Net {
         DBuf<double>& st = cells <= kKeepStage ? fstage : tmp;
         st.upload(fp, cells, stream);
         HIPC(mcr::launch_forcing_to_slots(st.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
-                                          stream));
+                                          stream, reach_major));
         sync();
     }
     static constexpr size_t kKeepStage = (size_t)1 << 23;   // 64 MiB
@@ -1529,6 +1530,10 @@ int mc_step(void* net, const double* o_prev, const double* i_prev, const double*
 
 int mc_load_forcing(void* net, int64_t n_rows, const double* xp, const double* fp) {
     return guarded([&] { as_net(net)->load_forcing(n_rows, xp, fp); });
+}
+
+int mc_load_forcing_series(void* net, int64_t n_rows, const double* xp, const double* fp) {
+    return guarded([&] { as_net(net)->load_forcing(n_rows, xp, fp, true); });
 }
 
 int mc_run(void* net, int64_t T, const double* x) {

@@ -352,9 +352,11 @@ __global__ void gather_from_slots(const double* __restrict__ src, double* __rest
     }
 }
 
+// F [e][r][slot] from the caller's forcing: step-major fp [r][j][e] or, reach_major, the
+// series layout fp [j][r][e] (a pandas frame's own block, no host transpose)
 __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restrict__ F,
                                  const int64_t* __restrict__ slot_reach, int64_t n,
-                                 int64_t nslots, int64_t n_rows, int64_t E) {
+                                 int64_t nslots, int64_t n_rows, int64_t E, bool reach_major) {
     const int64_t total = nslots * n_rows * E;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * blockDim.x) {
@@ -363,7 +365,7 @@ __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restri
         const int64_t e = er / n_rows;
         const int64_t r = er - e * n_rows;
         const int64_t j = slot_reach[d];
-        F[x] = j >= 0 ? fp[(r * n + j) * E + e] : 0.0;
+        F[x] = j >= 0 ? fp[(reach_major ? j * n_rows + r : r * n + j) * E + e] : 0.0;
     }
 }
 
@@ -518,9 +520,9 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
-                                   hipStream_t s) {
+                                   hipStream_t s, bool reach_major) {
     hipLaunchKernelGGL(forcing_to_slots, grid_for(nslots * n_rows * E, 256), 256, 0, s, fp, F,
-                       slot_reach, n, nslots, n_rows, E);
+                       slot_reach, n, nslots, n_rows, E, reach_major);
     return hipGetLastError();
 }
 

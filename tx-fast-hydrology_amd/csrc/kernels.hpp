@@ -200,7 +200,7 @@ hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_
 // F[e][r][d] = fp[r][slot_reach[d]][e]  (forcing table to slot order; 0 for padding slots)
 hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* slot_reach,
                                    int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
-                                   hipStream_t s);
+                                   hipStream_t s, bool reach_major = false);
 // jbase[j] = window index of step 0 of caller reach j
 hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
                                const int64_t* wbase, int slots, int64_t n, int64_t* jbase,

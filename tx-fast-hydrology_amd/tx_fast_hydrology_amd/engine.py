@@ -276,6 +276,16 @@ class RoutingNet:
             raise ValueError(f"forcing must be {self._shape(xp.size)}, got {fp.shape}")
         nat.check(nat.lib().mc_load_forcing(self._h, xp.size, ptr(xp), ptr(fp)))
 
+    def load_forcing_series(self, xp, fp_series):
+        """load_forcing with the forcing reach-major: fp_series [n, n_rows] (or [n, n_rows, E]),
+        e.g. the transpose view of a frame's values that is C-contiguous without a copy."""
+        xp = f64(xp)
+        fp = f64(fp_series)
+        want = (self.n, xp.size) if self.E == 1 else (self.n, xp.size, self.E)
+        if fp.shape != want:
+            raise ValueError(f"forcing series must be {want}, got {fp.shape}")
+        nat.check(nat.lib().mc_load_forcing_series(self._h, xp.size, ptr(xp), ptr(fp)))
+
     def run(self, x):
         """Route len(x) steps on the device (asynchronous; outputs stay resident)."""
         x = f64(x)

@@ -150,6 +150,19 @@ def _host_array(shape, dtype):
     return np.empty(shape, dtype=dtype)
 
 
+def _upload_forcing(net, xp, dataframe):
+    """Forcing frame -> the session (mc_load_forcing): a frame whose float64 block is stored
+    reach-major (any frame pandas copied or built column by column) goes up in its own layout
+    (mc_load_forcing_series, no host transpose copy), else step-major."""
+    vals = dataframe.values
+    series = vals.T
+    if vals.dtype == np.float64 and series.flags.c_contiguous and \
+            hasattr(net, "load_forcing_series"):
+        net.load_forcing_series(xp, series)
+    else:
+        net.load_forcing(xp, np.ascontiguousarray(vals, dtype=np.float64))
+
+
 class _DeviceRouting:
     """Device session of one model: a ``RoutingNet`` plus the host snapshot of the topology and
     coefficients it was built from (rebuilt / re-uploaded when they change)."""
@@ -580,7 +593,7 @@ class Muskingum:
             return
         from . import engine
         net = self._device.session(self)
-        net.load_forcing(xp, np.ascontiguousarray(dataframe.values, dtype=np.float64))
+        _upload_forcing(net, xp, dataframe)
         net.set_state(self.o_t_next, self.i_t_next)
         n, T = self.n, len(xs)
         chunk = max(1, _HORIZON_CHUNK_VALUES // max(n, 1))

@@ -27,6 +27,7 @@ import numpy as np
 import pandas as pd
 
 from .callbacks import BaseCallback
+from .muskingum import _upload_forcing
 
 logger = logging.getLogger(__name__)
 
@@ -233,8 +234,7 @@ def _device_dag(sim):
              for name in runs}
     for name in runs:
         m, inputs, net = models[name], sim.inputs[name], nets[name]
-        xp = inputs.index.asi8.astype(float)
-        net.load_forcing(xp, np.ascontiguousarray(inputs.values, dtype=np.float64))
+        _upload_forcing(net, inputs.index.asi8.astype(float), inputs)
         net.set_state(m.o_t_next, m.i_t_next)
     ph("upload")
     # enqueue: corrections then the horizon of every sub-basin, in the reference's order
