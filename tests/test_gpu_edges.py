@@ -97,3 +97,51 @@ def test_enkf_extreme_shapes_vs_numpy(E, m):
         ig, og = orc.apply_gain(heads, end, G[:, e], indeg)
         np.testing.assert_allclose(o[:, e] - X[:, e], og, rtol=0, atol=1e-9 * scale)
         np.testing.assert_allclose(i[:, e] - I0[:, e], ig, rtol=0, atol=1e-8 * scale)
+
+
+@pytest.mark.parametrize("mode", ["launches", "auto"])
+def test_non_finite_inputs_documented_behaviour(mode):
+    """Non-finite inputs are outside the bit-exact contract (mcroute.h header): the kernels
+    evaluate a clamped forcing step as (1 - 0) f + 0 f and give unrouted reaches zero
+    coefficients, so where the reference (nutils.py:24-27 row copy, :68 fresh zeros) yields
+    +-Inf or keeps o = 0, the device yields NaN.  Pinned here: every cell the reference computes
+    finite is bit-identical on the device except the outflows of unrouted reaches with
+    non-finite inputs (NaN instead of 0); every cell the reference computes non-finite is
+    non-finite on the device (NaN where the reference has +-Inf)."""
+    # 0 -> 1 <-> 2 (cycle: 1 and 2 are never processed), 6 -> 1, 3, 4 -> 5 (outlet), 7 -> 3
+    end = np.array([1, 2, 1, 5, 5, 5, 1, 3], dtype=np.int64)
+    n = end.size
+    start = np.arange(n, dtype=np.int64)
+    indeg = orc.compute_indegree(start, end)
+    heads = start[indeg == 0]
+    K = np.full(n, 3600.0)
+    X = np.full(n, 0.2)
+    coef = orc.muskingum_coeffs(K, X, 300.0)
+    o0 = np.linspace(1.0, 2.0, n)
+    o0[2] = np.nan                                   # unrouted reach: state never read
+    i0 = orc.init_inflows(start, end, np.nan_to_num(o0))
+    xp = (1.7e18 + 3600e9 * np.arange(4)).astype(float)
+    fp = np.full((4, n), 0.5)
+    fp[1, 1] = np.nan                                # unrouted reach forcing
+    fp[3, 7] = np.inf                                # last row: clamped steps copy it
+    x = xp[0] + 300e9 * np.arange(1, 61)             # 60 steps: the last 24 beyond xp[-1]
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16)
+    net.set_mode(mode)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fp)
+    net.run(x)
+    got_o, got_i = net.fetch_outputs()
+    unrouted = np.zeros(n, bool)
+    unrouted[[1, 2]] = True
+    for got, want, is_o in ((got_o, want_o, True), (got_i, want_i, False)):
+        fin = np.isfinite(want)
+        cell_ok = got == want
+        if is_o:            # documented: unrouted outflows may be NaN where the reference has 0
+            cell_ok |= unrouted[None, :] & np.isnan(got) & (want == 0)
+        assert cell_ok[fin].all()
+        assert (~np.isfinite(got[~fin])).all()
+    assert np.isinf(want_o[-1, 7]) and np.isnan(got_o[-1, 7])     # the clamped Inf row
+    assert (want_o[:, 1] == 0).all() and np.isnan(got_o[-1, 1])    # unrouted, NaN forcing
+    net.close()

@@ -217,6 +217,33 @@ struct Net {
         mw_cells = total;
     }
 
+    // identity of this session (slot maps of state hand-overs are cached per source session)
+    const uint64_t uid = next_uid();
+    static uint64_t next_uid() {
+        static std::atomic<uint64_t> c{1};
+        return c.fetch_add(1);
+    }
+    struct SlotMap {
+        uint64_t src_uid = 0;
+        DBuf<int32_t> map;
+    };
+    std::vector<std::unique_ptr<SlotMap>> slot_maps;
+    // map[d] = the slot of the source plan holding the reach of this plan's slot d (-1: none)
+    const int32_t* slot_map_from(const Net& S) {
+        for (auto& m : slot_maps)
+            if (m->src_uid == S.uid) return m->map.p;
+        std::vector<int32_t> mp((size_t)std::max<int64_t>(plan.nslots, 1), -1);
+        for (int64_t d = 0; d < plan.nslots; ++d) {
+            const int64_t j = plan.slot_reach[d];
+            if (j >= 0) mp[d] = (int32_t)S.plan.pos[j];
+        }
+        if (slot_maps.size() >= 4) slot_maps.erase(slot_maps.begin());
+        slot_maps.push_back(std::make_unique<SlotMap>());
+        slot_maps.back()->src_uid = S.uid;
+        slot_maps.back()->map.upload(mp.data(), mp.size(), stream);
+        return slot_maps.back()->map.p;
+    }
+
     // launch trace (mc_set_trace)
     bool trace = false;
     DBuf<int64_t> trace_buf;
@@ -439,6 +466,7 @@ struct Net {
         const int64_t n = plan.n;
         if (n == 0) return;
         settle();
+        settle_gain();
         stage.reserve((size_t)(n * m));
         HIPC(mcr::launch_gather_from_slots(src.p, stage.p, pos.p, n, plan.nslots, m, stream));
         HIPC(hipMemcpyAsync(host, stage.p, n * m * sizeof(double), hipMemcpyDeviceToHost,
@@ -447,10 +475,23 @@ struct Net {
     }
 
     // ---- ensemble analysis ----------------------------------------------
+    // The increments of the last analysis (Gn) are applied lazily: the EnKF cycle's next call
+    // is the one-step member run, whose input staging applies them on the way
+    // (launch_member_inputs, PendingGain); anything else that reads the state settles them
+    // first with the apply_gain kernel (same arithmetic, bit-identical).
+    bool gain_pending = false;
+    void settle_gain() {
+        if (!gain_pending) return;
+        gain_pending = false;
+        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, plan.nslots,
+                                    E, stream));
+    }
+
     void apply_gain(const double* gain) {
         REQUIRE(plan.n == 0 || gain, "gain must not be NULL");
         if (plan.n == 0) return;
         settle_state();
+        settle_gain();
         const size_t ns = (size_t)plan.nslots;
         Gn.reserve(ns * E);
         to_slots(gain, Gn, E);
@@ -498,6 +539,7 @@ struct Net {
         REQUIRE(E >= 2, "the ensemble analysis needs at least 2 members");
         REQUIRE(m >= 1 && m < (1ll << 31) && gauges && R, "bad gauge arguments");
         settle_state();
+        settle_gain();
         const int64_t n = plan.n, ns = plan.nslots;
         std::vector<int64_t> gs(m);
         for (int64_t g = 0; g < m; ++g) {
@@ -540,6 +582,7 @@ struct Net {
     void ens_gauges(int64_t m, const int64_t* gauges, const double* y, double* HX, double* D) {
         REQUIRE(y && HX && D, "null argument");
         settle_state();
+        settle_gain();
         upload_gauges(m, gauges);
         upload_async(Yb, y, (size_t)(m * E));
         HIPC(mcr::launch_gauge_values(st_o.p, gslot.p, Yb.p, HX, D, m, plan.nslots, E, stream));
@@ -549,6 +592,7 @@ struct Net {
     void ens_pack(int64_t N, double* send) {
         REQUIRE(N >= 1 && send, "bad pack arguments");
         settle_state();
+        settle_gain();
         HIPC(mcr::launch_pack_slices(st_o.p, send, plan.nslots, E, slice_size(N), N, stream));
     }
 
@@ -642,9 +686,9 @@ struct Net {
         settle_state();
         const int64_t ns = plan.nslots;
         Gn.reserve((size_t)(ns * E));
+        settle_gain();
         HIPC(mcr::launch_unpack_slices(Grecv, Gn.p, ns, E, slice_size(N), N, stream));
-        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, ns, E,
-                                    stream));
+        gain_pending = true;             // applied by the next state reader (settle_gain)
     }
 
     void enkf_analysis(int64_t m, const int64_t* gauges, const double* y, const double* R) {
@@ -659,8 +703,7 @@ struct Net {
         // one rank: the slice of every member IS the member-major state (slice_size(1) = ns),
         // so the pack / unpack stages are identities
         ens_slice_update(1, m, st_o.p, HXb.p, Db.p, R, Gn.p);
-        HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, ns, E,
-                                    stream));
+        gain_pending = true;             // applied by the next state reader (settle_gain)
     }
 
     // K = (A HA^T / (E-1)) C2^-1  as [n][m] in caller order
@@ -691,6 +734,7 @@ struct Net {
         REQUIRE(m >= 1 && m <= 65535, "members must be in [1, 65535]");
         settle_state();
         sync();
+        gain_pending = false;            // the state is zeroed
         E = m;
         const size_t ns = (size_t)std::max<int64_t>(plan.nslots, 1);
         for (DBuf<double>* b : {&st_o, &st_i}) {
@@ -719,6 +763,7 @@ struct Net {
     void set_state(const double* o, const double* i) {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
         settle_state();
+        gain_pending = false;            // replaced
         to_slots(o, st_o, E);
         to_slots(i, st_i, E, &stage2);   // its own staging: one synchronisation for both
         sync();
@@ -839,7 +884,9 @@ struct Net {
         {
             if (E > 1 && mode == 2 && T != 1)
                 throw Fail(MC_E_STATE, "dataflow mode routes one member, or one step of an ensemble");
-            if (E > 1 && T == 1 && members_fit(flds)) {
+            const bool memb = E > 1 && T == 1 && members_fit(flds);
+            if (!memb) settle_gain();
+            if (memb) {
                 // ---- one step of all members as one dataflow launch (flow.hip, MEMB): member e
                 // of slot d at tick G[d] + e
                 const size_t words = plan.ext_src.size() * (size_t)E * 4;
@@ -855,8 +902,11 @@ struct Net {
                 IOb.reserve((size_t)std::max<int64_t>(2 * mw_cells, 2));
                 double* IOp = IOb.p;
                 const mcr::MemberWin mw = member_win();
+                mcr::PendingGain pg;
+                if (gain_pending) pg = mcr::PendingGain{Gn.p, sup_off.p, sup.p};
                 HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
-                                               st_i.p, IOp, Qm.p, E, mw, stream));
+                                               st_i.p, IOp, Qm.p, E, mw, stream, pg));
+                gain_pending = false;
                 a.Qm = Qm.p;
                 a.IO = IOp;
                 a.wbase = mwbase.p;          // member windows (the launch stores no output rows)
@@ -1453,7 +1503,9 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         const int64_t n = D->plan.n, E = D->E;
         if (n == 0) return;
         S->settle();
+        S->settle_gain();
         D->settle_state();
+        D->gain_pending = false;         // its state is replaced
         // order: after the source's pending work, on the destination's stream; the source waits
         // for the copy before it may overwrite its state again
         hipEvent_t ev;
@@ -1464,15 +1516,15 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         } guard{ev};
         HIPC(hipEventRecord(ev, S->stream));
         HIPC(hipStreamWaitEvent(D->stream, ev, 0));
-        D->stage.reserve((size_t)(n * E));
+        // one direct slot -> slot permutation per array (the map of this pair of plans is
+        // built once and cached on the destination): was a gather into reach order and a
+        // scatter, each a full pass (EnKF256: 8.4 ms of hand-overs per horizon)
+        const int32_t* map = D->slot_map_from(*S);
         for (int k = 0; k < 2; ++k) {
             const DBuf<double>& from = k ? S->st_i : S->st_o;
             DBuf<double>& to = k ? D->st_i : D->st_o;
-            // reach-order staging [n][E]: source slots -> reaches -> destination slots
-            HIPC(mcr::launch_gather_from_slots(from.p, D->stage.p, S->pos.p, n, S->plan.nslots, E,
-                                               D->stream));
-            HIPC(mcr::launch_scatter_to_slots(D->stage.p, to.p, D->slot_reach.p, D->plan.nslots, E,
-                                              D->stream));
+            HIPC(mcr::launch_permute_slots(from.p, to.p, map, S->plan.nslots, D->plan.nslots, E,
+                                           D->stream));
         }
         HIPC(hipEventRecord(ev, D->stream));
         HIPC(hipStreamWaitEvent(S->stream, ev, 0));

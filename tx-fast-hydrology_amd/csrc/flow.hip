@@ -665,18 +665,27 @@ __device__ __forceinline__ RunCells member_run(const MemberWin& mw, int64_t d, i
 
 // IO = {o, i} of the session state, Qm = the lateral inflow of member e at the step (same
 // expression as the tick loop), both at the staging cell of (d, e); padding slots skipped
+// gain.G: pending analysis increments, applied as apply_gain (analysis.hip) would have applied
+// them to st_o / st_i first -- the same operations in the same order, so bit-identical.
+template <bool GAIN>
 __global__ __launch_bounds__(256) void member_inputs(
         const double* __restrict__ F, int64_t mF, int64_t ns, int n_rows, int4 ent,
         const double* __restrict__ st_o, const double* __restrict__ st_i,
-        double2* __restrict__ IO, double* __restrict__ Qm, int64_t E, MemberWin mw) {
+        double2* __restrict__ IO, double* __restrict__ Qm, int64_t E, MemberWin mw,
+        PendingGain gain) {
     const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= ns || mw.flags[d] == kSlotPad) return;
+    if (d >= ns) return;
+    const uint8_t fl = mw.flags[d];
+    if (fl == kSlotPad) return;
     const int64_t e0 = (int64_t)blockIdx.y * kMemberRun;
     const int ne = (int)(E - e0 < kMemberRun ? E - e0 : kMemberRun);
     const RunCells rc = member_run(mw, d, e0);
     const double f = __hiloint2double(ent.w, ent.z);
     const int64_t rlo = (int64_t)clamp_row(ent.x, n_rows) * ns + d;
     const int64_t rhi = (int64_t)clamp_row(ent.y < 0 ? ent.x : ent.y, n_rows) * ns + d;
+    // partial sums keep their state; unrouted reaches get no outflow gain (nutils.py:116-134)
+    const bool gained = GAIN && (fl == kSlotRouted || fl == kSlotUnrouted);
+    const int32_t u0 = GAIN ? gain.up_off[d] : 0, u1 = GAIN ? gain.up_off[d + 1] : 0;
 #pragma unroll 4
     for (int k = 0; k < ne; ++k) {
         const int64_t e = e0 + k;
@@ -685,7 +694,16 @@ __global__ __launch_bounds__(256) void member_inputs(
         const double lo = Fe[rlo];
         const double hi = Fe[rhi];
         const int64_t c = rc.c0 + k * rc.cs;
-        IO[c] = make_double2(st_o[idx], st_i[idx]);
+        double o = st_o[idx], i = st_i[idx];
+        if (gained) {
+            const double* Ge = gain.G + e * ns;
+            const double og = fl == kSlotRouted ? 0.0 + Ge[d] : 0.0;
+            double ig = 0.0;
+            for (int32_t q = u0; q < u1; ++q) ig = ig + (0.0 + Ge[gain.up[q]]);
+            o = o + og;
+            i = i + ig;
+        }
+        IO[c] = make_double2(o, i);
         Qm[c] = ent.y < 0 ? lo : (1.0 - f) * lo + f * hi;
     }
 }
@@ -776,11 +794,16 @@ hipError_t launch_gather_io(const double* IO, const MemberWin& mw, const int64_t
 
 hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_rows, int4 ent,
                                 const double* st_o, const double* st_i, double* IO, double* Qm,
-                                int64_t E, const MemberWin& mw, hipStream_t s) {
+                                int64_t E, const MemberWin& mw, hipStream_t s,
+                                const PendingGain& gain) {
     if (ns * E == 0) return hipSuccess;
     if ((E + kMemberRun - 1) / kMemberRun > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(member_inputs, member_grid(ns, E), 256, 0, s, F, mF, ns, n_rows, ent, st_o,
-                       st_i, reinterpret_cast<double2*>(IO), Qm, E, mw);
+    if (gain.G)
+        hipLaunchKernelGGL(member_inputs<true>, member_grid(ns, E), 256, 0, s, F, mF, ns, n_rows,
+                           ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+    else
+        hipLaunchKernelGGL(member_inputs<false>, member_grid(ns, E), 256, 0, s, F, mF, ns, n_rows,
+                           ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
     return hipGetLastError();
 }
 

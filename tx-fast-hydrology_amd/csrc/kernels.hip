@@ -511,6 +511,30 @@ hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t
     return hipGetLastError();
 }
 
+// State hand-over between two plans of one network (mc_net_copy_state): dst[e][d] =
+// src[e][map[d]] (map: the source slot of dst slot d's reach, -1 = no reach -> 0).  Member-major
+// rows, a 2-D grid (slot blocks x members): a block's writes are one contiguous run of a member
+// row and its gathers stay inside the same member's source row (1.5 MB at Texas: L2-resident).
+__global__ __launch_bounds__(256) void permute_slots(const double* __restrict__ src,
+                                                     double* __restrict__ dst,
+                                                     const int32_t* __restrict__ map,
+                                                     int64_t ns_src, int64_t ns_dst) {
+    const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (d >= ns_dst) return;
+    const int64_t e = blockIdx.y;
+    const int32_t k = map[d];
+    dst[e * ns_dst + d] = k >= 0 ? src[e * ns_src + k] : 0.0;
+}
+
+hipError_t launch_permute_slots(const double* src, double* dst, const int32_t* map,
+                                int64_t ns_src, int64_t ns_dst, int64_t E, hipStream_t s) {
+    if (ns_dst <= 0 || E <= 0) return hipSuccess;
+    if (E > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(permute_slots, dim3((unsigned)((ns_dst + 255) / 256), (unsigned)E), 256,
+                       0, s, src, dst, map, ns_src, ns_dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_t* pos,
                                     int64_t n, int64_t nslots, int64_t E, hipStream_t s) {
     hipLaunchKernelGGL(gather_from_slots, grid_for(n * E, 256), 256, 0, s, src, dst, pos, n,

@@ -160,9 +160,18 @@ struct MemberWin {
 // Inputs of a member-dataflow step at the member-window cells: IO = {o, i} of the session
 // state (16 B per cell, one load per slot and tick) and Qm = the step's interpolated lateral
 // inflow of the member (the kernels' formula: (1 - frac) F[e][lo][d] + frac F[e][hi][d]).
+// With gain.G non-NULL the pending analysis increments are applied on the way, exactly as
+// launch_apply_gain would have applied them to the state first (o + (0 + G), i + the one-hop
+// fold of the routed upstreams' 0 + G): the EnKF cycle's apply_gain pass is folded in here.
+struct PendingGain {
+    const double* G = nullptr;       // [E][nslots] increments (NULL: none)
+    const int32_t* up_off = nullptr; // routed upstream slots of each slot, rank order (CSR)
+    const int32_t* up = nullptr;
+};
 hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t nslots, int n_rows,
                                 int4 ent, const double* st_o, const double* st_i, double* IO,
-                                double* Qm, int64_t E, const MemberWin& mw, hipStream_t s);
+                                double* Qm, int64_t E, const MemberWin& mw, hipStream_t s,
+                                const PendingGain& gain = PendingGain());
 // After a member-dataflow step (which leaves each member's new {o, i} in IO): the session state
 // st_o / st_i.  IO keeps the step's outputs until the next run; launch_gather_io reads them in
 // caller order (out[j][e], the outflow or the inflow).
@@ -195,6 +204,8 @@ hipError_t launch_set_slot_coeffs(const uint8_t* flags, double* alpha, double* b
 hipError_t launch_scatter_to_slots(const double* src, double* dst, const int64_t* slot_reach,
                                    int64_t nslots, int64_t E, hipStream_t s);
 // dst[j][e] = src[e][pos[j]]
+hipError_t launch_permute_slots(const double* src, double* dst, const int32_t* map,
+                                int64_t ns_src, int64_t ns_dst, int64_t E, hipStream_t s);
 hipError_t launch_gather_from_slots(const double* src, double* dst, const int64_t* pos,
                                     int64_t n, int64_t nslots, int64_t E, hipStream_t s);
 // F[e][r][d] = fp[r][slot_reach[d]][e]  (forcing table to slot order; 0 for padding slots)

@@ -260,9 +260,10 @@ def _device_dag(sim):
         tickets.append((nets[name], nets[name].fetch_outputs_async(0, T, o[1:], None)))
         tickets.append((nets[name], nets[name].fetch_outputs_async(T - k, T, None, li)))
         series[name], last_i[name] = o, li
+    ph("fetch_enqueue")
     for net, tk in tickets:
         net.fetch_wait(tk)
-    ph("fetch")
+    ph("fetch_wait")
     if any(nets[name].reroutes() != before[name] for name in runs):
         # a horizon whose dataflow waits gave up (the device was shared) was re-routed by its
         # own session at the fetch, but the corrections its downstream sub-basins took from it
