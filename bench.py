@@ -95,6 +95,9 @@ def parse(argv=None, world=None):
     ap.add_argument("--huc8", action="store_true",
                     help="BASELINE configs[0]: one HUC-8 sub-basin (1000 reaches, one outlet, "
                          "deepest path ~100 reaches), deterministic")
+    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow", "ensemble"],
+                    help="execution path (mcroute.h mc_set_mode); 'ensemble': the whole horizon "
+                         "of every member as one dataflow launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-api", action="store_true", help="skip the Muskingum.simulate timing")
@@ -246,6 +249,7 @@ def build_workload(args, rank=0, world=1):
     tile = args.tile or (64 if E > 1 and enkf is None else 16)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E,
                             chain=args.chain)
+    net.set_mode(getattr(args, "mode", "auto"))
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
     net.load_forcing(xp, fp)
@@ -254,6 +258,7 @@ def build_workload(args, rank=0, world=1):
         # launches: the multi-launch ensemble shape), the state handed over on the device
         fnet = engine.RoutingNet(end, indeg, heads, slots=getattr(args, "fslots", 256),
                                  tile=getattr(args, "ftile", 64), members=E)
+        fnet.set_mode(getattr(args, "mode", "auto"))
         fnet.set_coeffs(alpha, beta, chi, gamma)
         fnet.load_forcing(xp, fp)
         enkf.fnet = fnet

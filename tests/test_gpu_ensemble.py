@@ -236,3 +236,62 @@ def test_conus_scale_ensemble_members_bitexact():
                                     np.ascontiguousarray(fpe[:, :, e]), keep_outputs=False)
         assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
         assert np.array_equal(last_o[0, :, e], fo) and np.array_equal(last_i[0, :, e], fi), e
+
+
+@pytest.mark.parametrize("n,E,slots,tile,T,chain", [(3000, 5, 192, 16, 60, 2),
+                                                    (6000, 16, 192, 16, 97, 2),
+                                                    (1200, 64, 128, 32, 25, 2),
+                                                    (2500, 3, 64, 16, 40, 3)])
+def test_ensemble_dataflow_horizon_bitexact(n, E, slots, tile, T, chain):
+    """Ensemble dataflow (mode "ensemble"): the whole horizon of every member in ONE launch whose
+    (workgroup, member) instances take tickets in topological order -- every member bit-identical
+    to its serial oracle run, and to the multi-launch path; a second horizon continues from the
+    state the first left."""
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4, 150, 7 * n + E, E)
+    n = end.size
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    x2 = x[-1] + 300e9 * np.arange(1, 9)
+    res = {}
+    for mode in ("ensemble", "launches"):
+        net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile, members=E,
+                                chain=chain)
+        net.set_mode(mode)
+        net.set_coeffs(*coef)
+        net.set_state(o0, i0)
+        got_o, got_i = net.simulate(x, xp, fpe)
+        path = net.mode()[1]
+        net.run(x2)
+        o2, i2 = net.fetch_outputs()
+        res[mode] = (got_o, got_i, o2, i2, net.get_state(), path)
+        net.close()
+    assert res["ensemble"][5] == "dataflow" and res["launches"][5] == "launches"
+    for a, b in zip(res["ensemble"][:4], res["launches"][:4]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(res["ensemble"][4][0], res["launches"][4][0])
+    assert np.array_equal(res["ensemble"][4][1], res["launches"][4][1])
+    got_o, got_i = res["ensemble"][:2]
+    for e in range(E):
+        want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                            np.ascontiguousarray(fpe[:, :, e]))
+        assert np.array_equal(got_o[:, :, e], want_o), e
+        assert np.array_equal(got_i[:, :, e], want_i), e
+
+
+def test_ensemble_dataflow_give_up_reroutes():
+    """A give-up of the ensemble dataflow (patience < 0) is re-routed with launches at the next
+    synchronising call: still bit-exact."""
+    E, T = 8, 48
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(20000, 6, 600, 5, E)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=192, tile=16, members=E)
+    net.set_mode("ensemble")
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.set_flow_patience(-1)
+    got_o, _ = net.simulate(x, xp, fpe)
+    assert net.reroutes() >= 1 and net.mode()[1] == "launches"
+    for e in (0, E - 1):
+        want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                       np.ascontiguousarray(fpe[:, :, e]))
+        assert np.array_equal(got_o[:, :, e], want_o), e
+    net.close()

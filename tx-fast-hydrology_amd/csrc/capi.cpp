@@ -421,6 +421,66 @@ struct Net {
         return ok;
     }
 
+    // Topological order of the workgroup graph (an edge per cross-cluster input: producer's
+    // workgroup -> consumer's), the ticket order of the ensemble dataflow (WaveArgs::order);
+    // 1 = built, -1 = the graph has a cycle (the ensemble dataflow is not used), 0 = not yet.
+    DBuf<int32_t> topo, qctr;
+    int topo_state = 0;
+    bool topo_ready() {
+        if (topo_state != 0) return topo_state > 0;
+        const int32_t W = plan.nwg;
+        const int RS = row_width();
+        std::vector<std::vector<int32_t>> adj(W);
+        std::vector<int32_t> indeg(W, 0);
+        for (int32_t c = 0; c < W; ++c)
+            for (int32_t e = plan.ext_off[c]; e < plan.ext_off[c + 1]; ++e) {
+                const int64_t src = plan.ext_src[e];
+                const int64_t slot = src < plan.n ? plan.pos[src] : src - plan.n;
+                const int32_t pw = (int32_t)(slot / RS);
+                if (pw == c) continue;
+                adj[pw].push_back(c);
+            }
+        for (auto& v : adj) {
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            for (int32_t c : v) ++indeg[c];
+        }
+        std::vector<int32_t> order;
+        order.reserve(W);
+        for (int32_t w = 0; w < W; ++w)
+            if (indeg[w] == 0) order.push_back(w);
+        for (size_t k = 0; k < order.size(); ++k)
+            for (int32_t c : adj[order[k]])
+                if (--indeg[c] == 0) order.push_back(c);
+        if ((int32_t)order.size() != W) {
+            topo_state = -1;
+            return false;
+        }
+        topo.upload(order.data(), order.size(), stream);
+        topo_state = 1;
+        return true;
+    }
+
+    // Can a T-step horizon of all E members run as ONE ensemble-dataflow launch?  Its
+    // (workgroup, member) instances take tickets in topological order, so they need not be
+    // resident together (mode 3 opts in; mcroute.h mc_set_mode).
+    bool ens_flow_fits(int64_t T, bool dense, size_t& lds) {
+        if (mode != 3 || force_mode == 1 || E < 2 || T < 2) return false;
+        const int S = plan.p.slots, Kc = plan.p.chain;
+        lds = mcr::flow_lds_bytes(S, Kc, (int)T, plan.max_ext_wg);
+        const size_t xgm = plan.ext_src.size() * (size_t)T * 16;
+        bool ok = mcr::flow_shape_ok(S, Kc) && plan.p.tile >= mcr::kFlowMinSlack &&
+                  plan.max_ext_wg <= mcr::kFlowMaxExt && T <= mcr::kFlowMaxT &&
+                  xgm < (size_t(1) << 31) && lds <= 160 * 1024 &&
+                  (int64_t)plan.nwg * E < (1ll << 31) && topo_ready();
+        if (ok) {
+            int bpc = 0;
+            HIPC(mcr::flow_occupancy(S, Kc, dense, lds, &bpc));
+            ok = bpc >= 1;
+        }
+        return ok;
+    }
+
     // Can one step of all E members run as one member-dataflow launch?
     bool members_fit(size_t& lds) {
         if (mode == 1 || force_mode == 1) return false;
@@ -939,6 +999,51 @@ struct Net {
             } else if (E > 1 && mode == 2) {
                 throw Fail(MC_E_STATE, "member dataflow requested but the network does not fit one "
                                        "resident launch");
+            }
+            if (E > 1 && T > 1 && ens_flow_fits(T, dense, flds)) {
+                // ---- the whole horizon of every member as ONE launch (flow.hip, ticket queue):
+                // instance (w, e) walks workgroup w's window for member e; granules per member
+                const size_t words = plan.ext_src.size() * (size_t)T * 4;
+                const size_t all = words * (size_t)E;
+                if (all > xg_words || epoch == 0xffffffffu) {
+                    XG.reserve(std::max<size_t>(all, 4));
+                    HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(all, 4) * 4, stream));
+                    xg_words = std::max(xg_words, all);
+                    epoch = 0;
+                }
+                ++epoch;
+                qctr.reserve(1);
+                HIPC(hipMemsetAsync(qctr.p, 0, sizeof(int32_t), stream));
+                a.XG = XG.p;
+                a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
+                a.mXG = (int64_t)words;
+                a.epoch = epoch;
+                a.status = status.p;
+                a.patience = patience;
+                a.table_cap = (int32_t)T;
+                a.active = all_wg.p;
+                a.queue = qctr.p;
+                a.order = topo.p;
+                a.qE = (int32_t)E;
+                st_o2.reserve(st_o.cap);
+                st_i2.reserve(st_i.cap);
+                a.st_o_out = st_o2.p;
+                a.st_i_out = st_i2.p;
+                if (timing) HIPC(hipEventRecord(events[0], stream));
+                HIPC(mcr::launch_flow(a, plan.nwg * (int)E, plan.p.slots, plan.p.chain, flds,
+                                      dense, stream));
+                if (timing) HIPC(hipEventRecord(events[1], stream));
+                a.queue = nullptr;
+                st_o.swap(st_o2);
+                st_i.swap(st_i2);
+                ++flow_runs;
+                last_flow.valid = true;
+                last_flow.T = T;
+                last_flow.F = Fsrc;
+                last_flow.rows = rows;
+                last_flow.tab = tabh;
+                launched = 1;
+                last_path = 2;
             }
             if (E == 1 && flow_fits(T, dense, flds)) {
                 // ---- one dataflow launch for the whole horizon (flow.hip)
@@ -1662,7 +1767,9 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
+        REQUIRE(mode >= 0 && mode <= 3,
+                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow) or 3 (auto + ensemble "
+                "dataflow horizons)");
         as_net(net)->mode = mode;
     });
 }

@@ -203,13 +203,32 @@ void wavefront_flow(WaveArgs a) {
     const int tid = threadIdx.x;
     const int nthr = SLOTS + kHelperLanes;
     const int64_t t_start = a.trace ? wall_clock64() : 0;
-    const int w = a.active[blockIdx.x];
+    // the routed instance: this workgroup of the plan, or (ensemble horizon) the next ticket's
+    // (workgroup, member) in the queue's topological order
+    int w = 0, mem = 0;
+    if (!MEMB && a.queue) {
+        __shared__ int ticket;
+        if (tid == 0)
+            ticket = __hip_atomic_fetch_add(a.queue, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int t = ticket;
+        w = a.order[t / a.qE];
+        mem = t - (t / a.qE) * a.qE;
+    } else {
+        w = a.active[blockIdx.x];
+    }
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
     const int kb = gminw & ~(kChunk - 1);               // first chunk of this workgroup
     const int wend = gmaxw + T;                         // end of its tick window
     const int e0 = a.ext_off[w];
     const int next = a.ext_off[w + 1] - e0;
-    const auto xg = __builtin_amdgcn_make_buffer_rsrc(a.XG, (short)0, (int)a.xg_bytes, 0x00020000);
+    // member bases (member-major arrays; 0 for the one-member horizon)
+    const double* __restrict__ Fm = a.F + (int64_t)mem * a.mF;
+    double* __restrict__ Om = a.O + (int64_t)mem * a.mO;
+    const int64_t sm = (int64_t)mem * a.mS;
+    const auto xg = __builtin_amdgcn_make_buffer_rsrc(a.XG + (int64_t)mem * a.mXG, (short)0,
+                                                      (int)a.xg_bytes, 0x00020000);
 
     // ---- shared prologue: step table, consumer ticks of external inputs
     if (!MEMB)
@@ -233,7 +252,7 @@ void wavefront_flow(WaveArgs a) {
         auto copy_row = [&](int k) {
             if (MEMB || MCR_EXP_NO_STORES || k < gminw || k >= wend) return;   // wave-uniform
             const char* src = lds + XB + (unsigned)(k & 7) * PL;
-            double* dst = a.O + wbh + (int64_t)(k - gminw) * RS;
+            double* dst = Om + wbh + (int64_t)(k - gminw) * RS;
 #pragma unroll
             for (int c = 2 * hl; c < RS; c += 128)
                 __builtin_nontemporal_store(*reinterpret_cast<const f64x2*>(src + (unsigned)c * 8u),
@@ -288,7 +307,7 @@ void wavefront_flow(WaveArgs a) {
     uint64_t up[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + lid, 0, kb, wend - kb, T);
+        load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + lid, mem, kb, wend - kb, T);
         up[p] = a.up4[S[p].d];
         xbp[(((kb - 1) & 7) * PL) / 8 + p * SLOTS + lid] = S[p].op;
     }
@@ -449,9 +468,9 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
         for (int p = 0; p < K; ++p) {
             chunk_rows(tab, 0, kb, S[p].G, T, rb[p], nr[p]);
-            f0[p] = a.F[(int64_t)clamp_row(rb[p], nrow) * ns + S[p].d];
-            f1[p] = a.F[(int64_t)clamp_row(rb[p] + 1, nrow) * ns + S[p].d];
-            f2[p] = a.F[(int64_t)clamp_row(rb[p] + 2, nrow) * ns + S[p].d];
+            f0[p] = Fm[(int64_t)clamp_row(rb[p], nrow) * ns + S[p].d];
+            f1[p] = Fm[(int64_t)clamp_row(rb[p] + 1, nrow) * ns + S[p].d];
+            f2[p] = Fm[(int64_t)clamp_row(rb[p] + 2, nrow) * ns + S[p].d];
         }
         __builtin_amdgcn_s_waitcnt(0);                      // nothing pending may enter the loop
         __syncthreads();                                    // prologue barrier (helper staged XE)
@@ -483,9 +502,9 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 chunk_rows(tab, 0, kc + kChunk, S[p].G, Tn, rbn[p], nrn[p]);
-                g0[p] = a.F[(int64_t)clamp_row(rbn[p], nrow) * ns + S[p].d];
-                g1[p] = a.F[(int64_t)clamp_row(rbn[p] + 1, nrow) * ns + S[p].d];
-                g2[p] = a.F[(int64_t)clamp_row(rbn[p] + 2, nrow) * ns + S[p].d];
+                g0[p] = Fm[(int64_t)clamp_row(rbn[p], nrow) * ns + S[p].d];
+                g1[p] = Fm[(int64_t)clamp_row(rbn[p] + 1, nrow) * ns + S[p].d];
+                g2[p] = Fm[(int64_t)clamp_row(rbn[p] + 2, nrow) * ns + S[p].d];
             }
             unsigned m[K][kUpInline];
 #pragma unroll
@@ -497,8 +516,8 @@ void wavefront_flow(WaveArgs a) {
                 const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
                 double lo, hi;
                 if (DENSE && slow) {
-                    lo = a.F[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
-                    hi = a.F[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
+                    lo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
+                    hi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
                 } else {
                     lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
                     hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
@@ -579,8 +598,8 @@ void wavefront_flow(WaveArgs a) {
         // session state after the horizon; never-processed reaches hold o = 0
 #pragma unroll
         for (int p = 0; p < K; ++p) {
-            a.st_o_out[S[p].d] = S[p].op;
-            a.st_i_out[S[p].d] = S[p].ip;
+            a.st_o_out[sm + S[p].d] = S[p].op;
+            a.st_i_out[sm + S[p].d] = S[p].ip;
         }
     }
     if (a.trace && tid == 0) {

@@ -104,6 +104,16 @@ struct WaveArgs {
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
+    // ensemble dataflow (flow.hip, E > 1 horizon): every (workgroup, member) instance takes a
+    // ticket from `queue` (zeroed before the launch); ticket t routes workgroup order[t / qE]
+    // for member t % qE.  `order` is a topological order of the workgroup graph (producers
+    // first), so an instance waits only for instances that took earlier tickets: deadlock-free
+    // without co-residency.  mXG: granule words per member.  queue == NULL: the one-member
+    // horizon (the grid is every workgroup, all resident).
+    int32_t* queue;
+    const int32_t* order;
+    int32_t qE;
+    int64_t mXG;
 };
 
 // LDS bytes of the multi-launch kernel for `slots` lanes (chain * slots node slots): the

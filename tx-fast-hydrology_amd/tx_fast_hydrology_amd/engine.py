@@ -358,7 +358,7 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
-    MODES = {"auto": 0, "launches": 1, "dataflow": 2}
+    MODES = {"auto": 0, "launches": 1, "dataflow": 2, "ensemble": 3}
 
     def set_mode(self, mode: str):
         """Execution path: "auto" (default), "launches" or "dataflow" (see mcroute.h)."""
