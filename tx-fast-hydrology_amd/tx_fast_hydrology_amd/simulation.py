@@ -291,15 +291,16 @@ def _device_dag(sim):
             index = indexes[key] = pd.DatetimeIndex(ns.view("datetime64[ns]")).tz_localize("UTC")
         sim.outputs[name] = pd.DataFrame(o, index=index, columns=inputs.columns, copy=False)
     ph("frames")
-    # the corrected input frames, as the reference's += leaves them (same arithmetic)
+    # the corrected input frames, as the reference's += leaves them: the same arithmetic as
+    # _lateral_correction, on the fetched arrays (no Series round trips)
     for name in runs:
         frame = sim.inputs[name]
         for link in corrections[name]:
             up = link.upstream_model
-            series_ = sim.outputs[up.name][up.reach_ids[link.upstream_index]]
-            column = models[name].reach_ids[link.downstream_index]
-            frame.loc[:, column] += _lateral_correction(models[name], link.downstream_index,
-                                                        series_)
+            I = series[up.name][:, link.upstream_index]
+            k = frame.columns.get_loc(models[name].reach_ids[link.downstream_index])
+            corr = _correction_values(models[name], link.downstream_index, I)
+            frame.iloc[:, k] = frame.iloc[:, k].to_numpy() + corr
     ph("corrections")
     sim.dag_phases = ph.ms
     return True
@@ -313,6 +314,15 @@ def _outflow_frame(model, inputs):
     frame.index = pd.to_datetime(frame.index, utc=True)
     frame.columns = inputs.columns
     return frame
+
+
+def _correction_values(model, j, I):
+    """_lateral_correction on a plain array I (the outflow series, start row first): now =
+    I[1:], before = I[:-1] with NaN -> 0 (shift(1).iloc[1:].fillna(0)), same expression."""
+    now = I[1:]
+    before = I[:-1]
+    before = np.where(np.isnan(before), 0.0, before)
+    return model.alpha[j] * now / model.gamma[j] + model.beta[j] * before / model.gamma[j]
 
 
 def _lateral_correction(model, j, series):
