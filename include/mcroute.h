@@ -220,6 +220,8 @@ int mc_fetch_wait(void* net, int64_t ticket);
  * t ^ (t >> 29), t = (bits(rows[r][j]) ^ (j * 0x9E3779B97F4A7C15)) * 0xD6E8FEB86659FD93.  Changing
  * any single element changes it.  Host code (no device needed), a few threads. */
 int mc_host_digest(const double* rows, int64_t nrows, int64_t n, uint64_t* out);
+/* The digests of two rows of n values each (a step's outflows and inflows): out2[0], out2[1]. */
+int mc_host_digest2(const double* a, const double* b, int64_t n, uint64_t* out2);
 /* Copy the full series of the last mc_run, reach-major: out_o[j][t] (either may be NULL). */
 int mc_fetch_series(void* net, double* out_o, double* out_i);
 /* Convenience: mc_load_forcing + mc_run + mc_fetch_outputs(0, T). */

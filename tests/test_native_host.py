@@ -188,3 +188,14 @@ def test_library_needs_no_vendor_blas_or_solver():
     out = subprocess.run(["ldd", _native.lib_path()], capture_output=True, text=True).stdout
     assert "libamdhip64" in out
     assert "rocblas" not in out and "rocsolver" not in out, out
+
+
+def test_host_digest_pair_matches_rows():
+    from api_helpers import digest_rows
+    from tx_fast_hydrology_amd import engine
+    rng = np.random.default_rng(3)
+    a, b = rng.normal(size=70_001), rng.normal(size=70_001)
+    rd = engine.RowDigest()
+    assert rd(a, b) == (int(digest_rows(a)[0]), int(digest_rows(b)[0]))
+    with pytest.raises(ValueError):
+        rd(a[::2], b[::2])

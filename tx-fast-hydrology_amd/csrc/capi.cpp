@@ -1315,10 +1315,17 @@ class DigestPool {
         return pool;
     }
     void run(const double* a, int64_t nrows, int64_t n, uint64_t* out) {
+        std::vector<const double*> rows((size_t)nrows);
+        for (int64_t r = 0; r < nrows; ++r) rows[(size_t)r] = a + r * n;
+        run_rows(rows.data(), nrows, n, out);
+    }
+    // rows given by pointers (the drop-in API checks a step's outflow and inflow rows, which
+    // live in different fetched blocks, in one call)
+    void run_rows(const double* const* rows, int64_t nrows, int64_t n, uint64_t* out) {
         std::lock_guard<std::mutex> call(call_mu_);
         const int parts = (nrows * n < (1 << 15) || workers_.empty())
                               ? 1 : (int)workers_.size() + 1;
-        a_ = a;
+        rows_ = rows;
         nrows_ = nrows;
         n_ = n;
         parts_ = parts;
@@ -1362,7 +1369,7 @@ class DigestPool {
     void block(int p) {
         const int64_t j0 = n_ * p / parts_, j1 = n_ * (p + 1) / parts_;
         for (int64_t r = 0; r < nrows_; ++r) {
-            const uint64_t* row = reinterpret_cast<const uint64_t*>(a_ + r * n_);
+            const uint64_t* row = reinterpret_cast<const uint64_t*>(rows_[r]);
             uint64_t h = 0;
             for (int64_t j = j0; j < j1; ++j) h += mcr::digest_term(row[j], (uint64_t)j);
             partial_[(size_t)p * nrows_ + r] = h;
@@ -1395,7 +1402,7 @@ class DigestPool {
     std::atomic<uint64_t> gen_{0};
     std::atomic<int> pending_{0};
     bool stop_ = false;
-    const double* a_ = nullptr;
+    const double* const* rows_ = nullptr;
     int64_t nrows_ = 0, n_ = 0;
     int parts_ = 1;
     std::vector<uint64_t> partial_;
@@ -1723,6 +1730,18 @@ int mc_host_digest(const double* rows, int64_t nrows, int64_t n, uint64_t* out) 
             return;
         }
         DigestPool::get().run(rows, nrows, n, out);
+    });
+}
+
+int mc_host_digest2(const double* a, const double* b, int64_t n, uint64_t* out2) {
+    return guarded([&] {
+        REQUIRE(n >= 0 && out2 && (n == 0 || (a && b)), "bad digest arguments");
+        if (n == 0) {
+            out2[0] = out2[1] = 0;
+            return;
+        }
+        const double* rows[2] = {a, b};
+        DigestPool::get().run_rows(rows, 2, n, out2);
     });
 }
 

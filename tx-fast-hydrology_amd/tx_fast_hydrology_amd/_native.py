@@ -105,6 +105,7 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_int64)]),
     "mc_fetch_wait": (_i32, [_vp, _i64]),
     "mc_host_digest": (_i32, [_vp, _i64, _i64, _vp]),
+    "mc_host_digest2": (_i32, [_vp, _vp, _i64, _vp]),
     "mc_ens_weights": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "mc_ens_increments": (_i32, [_vp, _i64, _vp, _vp]),
     "mc_ens_unpack_apply": (_i32, [_vp, _i64, _vp]),

@@ -415,6 +415,23 @@ def host_digest(a) -> np.ndarray:
     return out
 
 
+class RowDigest:
+    """Digests of a step's two rows (outflows, inflows) in one library call (mc_host_digest2):
+    the per-yield edit check of Muskingum's fused horizons.  Rows: C-contiguous float64 [n]."""
+
+    def __init__(self):
+        self._fn = nat.lib().mc_host_digest2
+        self._out = np.empty(2, dtype=np.uint64)
+        self._p = self._out.ctypes.data
+
+    def __call__(self, a, b):
+        if not (a.flags.c_contiguous and b.flags.c_contiguous and a.dtype == np.float64 and
+                b.dtype == np.float64 and a.size == b.size):
+            raise ValueError("RowDigest needs two C-contiguous float64 rows of equal size")
+        nat.check(self._fn(a.ctypes.data, b.ctypes.data, a.size, self._p))
+        return int(self._out[0]), int(self._out[1])
+
+
 def probe_tick_floor(slots=192, chain=2, ticks=8192) -> float:
     """Device ns per tick of the bare dataflow tick chain (mcroute.h mc_probe_tick_floor):
     the latency floor bench.py multiplies by the schedule length."""

@@ -600,6 +600,7 @@ class Muskingum:
         block = max(1, _FETCH_BLOCK_VALUES // max(n, 1))
         timedelta = self.timedelta
         rev = self._coef_rev[0]
+        row_digest = engine.RowDigest()
         pending = []          # fetch tickets not yet waited for
         try:
             for c0 in range(0, T, chunk):
@@ -641,8 +642,8 @@ class Muskingum:
                         self.logger.debug(f"Stepped to time {self.datetime}")
                         expected_time = self.datetime
                         yield self
-                        edited = (engine.host_digest(o_next)[0] != digests[0, b0 + k] or
-                                  engine.host_digest(i_next)[0] != digests[1, b0 + k])
+                        h_o, h_i = row_digest(o_next, i_next)
+                        edited = h_o != digests[0, b0 + k] or h_i != digests[1, b0 + k]
                         if (self.o_t_next is not o_next or self.i_t_next is not i_next or edited
                                 or self._coef_rev[0] != rev or not self._callbacks_idle()
                                 or self.datetime != expected_time
