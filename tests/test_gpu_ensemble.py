@@ -281,8 +281,8 @@ def test_ensemble_dataflow_give_up_reroutes():
     """Patience < 0 (give up at the first stale upstream value): a horizon whose wait gave up is
     re-routed with launches at the next synchronising call, else it completes as dataflow (the
     ticket order makes waits rare: producers took earlier tickets) -- bit-exact either way."""
-    E, T = 8, 48
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(20000, 6, 600, 5, E)
+    E, T = 16, 97
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(6000, 4, 150, 7 * 6000 + E, E)
     x = xp[0] + 300e9 * np.arange(1, T + 1)
     net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=192, tile=16, members=E)
     net.set_mode("ensemble")
@@ -291,6 +291,26 @@ def test_ensemble_dataflow_give_up_reroutes():
     net.set_flow_patience(-1)
     got_o, _ = net.simulate(x, xp, fpe)
     assert net.mode()[1] == ("launches" if net.reroutes() else "dataflow")
+    for e in (0, E - 1):
+        want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                       np.ascontiguousarray(fpe[:, :, e]))
+        assert np.array_equal(got_o[:, :, e], want_o), e
+    net.close()
+
+
+def test_ensemble_dataflow_needs_an_acyclic_workgroup_graph():
+    """The ticket order is a topological order of the workgroup graph; a plan whose workgroups
+    feed each other both ways (this network, 192 lanes) routes its ensemble horizons with
+    launches instead -- still bit-exact."""
+    E, T = 8, 48
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(20000, 6, 600, 5, E)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=192, tile=16, members=E)
+    net.set_mode("ensemble")
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    got_o, _ = net.simulate(x, xp, fpe)
+    assert net.mode()[1] == "launches"
     for e in (0, E - 1):
         want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
                                        np.ascontiguousarray(fpe[:, :, e]))
