@@ -20,6 +20,7 @@
 
 #include "analysis.hpp"
 #include "capi_common.hpp"
+#include "digest.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -825,8 +826,7 @@ struct Net {
         settle_state();
         gain_pending = false;            // replaced
         to_slots(o, st_o, E);
-        to_slots(i, st_i, E, &stage2);   // its own staging: one synchronisation for both
-        sync();
+        to_slots(i, st_i, E, &stage2);   // its own staging (stream-ordered reuse, no sync)
     }
 
     // Per-horizon layout: active workgroups of every launch and the output windows (cached
@@ -1149,7 +1149,10 @@ struct Net {
         st.upload(fp, cells, stream);
         HIPC(mcr::launch_forcing_to_slots(st.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
                                           stream, reach_major));
-        sync();
+        // a copy from pageable host memory has read the caller's array when it returns, and the
+        // persistent staging is reused stream-ordered: only the temporary staging must be
+        // drained before it is freed
+        if (&st == &tmp) sync();
     }
     static constexpr size_t kKeepStage = (size_t)1 << 23;   // 64 MiB
     DBuf<double> fstage, stage2;
@@ -1303,110 +1306,6 @@ Net* as_net(void* h) {
     if (!h) throw Fail(MC_E_INVALID, "null session handle");
     return static_cast<Net*>(h);
 }
-
-// Host row digests (mc_host_digest): the device's row_digests sum, formed over column blocks
-// by a small persistent pool.  The drop-in API checks two Texas rows (3 MB) after every yielded
-// step; workers spin briefly between jobs (the next step's check follows within ~0.1 ms), then
-// sleep on a condition variable.
-class DigestPool {
-  public:
-    static DigestPool& get() {
-        static DigestPool pool;
-        return pool;
-    }
-    void run(const double* a, int64_t nrows, int64_t n, uint64_t* out) {
-        std::vector<const double*> rows((size_t)nrows);
-        for (int64_t r = 0; r < nrows; ++r) rows[(size_t)r] = a + r * n;
-        run_rows(rows.data(), nrows, n, out);
-    }
-    // rows given by pointers (the drop-in API checks a step's outflow and inflow rows, which
-    // live in different fetched blocks, in one call)
-    void run_rows(const double* const* rows, int64_t nrows, int64_t n, uint64_t* out) {
-        std::lock_guard<std::mutex> call(call_mu_);
-        const int parts = (nrows * n < (1 << 15) || workers_.empty())
-                              ? 1 : (int)workers_.size() + 1;
-        rows_ = rows;
-        nrows_ = nrows;
-        n_ = n;
-        parts_ = parts;
-        partial_.assign((size_t)parts * (size_t)nrows, 0);
-        if (parts > 1) {
-            pending_.store(parts - 1, std::memory_order_relaxed);
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                gen_.fetch_add(1, std::memory_order_release);
-            }
-            cv_.notify_all();
-        }
-        block(0);
-        while (parts > 1 && pending_.load(std::memory_order_acquire) != 0) {
-        }
-        for (int64_t r = 0; r < nrows; ++r) {
-            uint64_t h = 0;
-            for (int p = 0; p < parts; ++p) h += partial_[(size_t)p * nrows + r];
-            out[r] = h;
-        }
-    }
-    ~DigestPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-            gen_.fetch_add(1, std::memory_order_release);
-        }
-        cv_.notify_all();
-        for (std::thread& t : workers_) t.join();
-    }
-
-  private:
-    DigestPool() {
-        int want = 8;
-        if (const char* e = std::getenv("MCR_DIGEST_THREADS")) want = std::atoi(e);
-        else if (const char* e2 = std::getenv("OMP_NUM_THREADS")) want = std::min(8, std::atoi(e2));
-        const int hw = (int)std::thread::hardware_concurrency();
-        want = std::max(1, std::min(want, hw > 0 ? hw : 1));
-        for (int t = 1; t < want; ++t) workers_.emplace_back([this, t] { work(t); });
-    }
-    void block(int p) {
-        const int64_t j0 = n_ * p / parts_, j1 = n_ * (p + 1) / parts_;
-        for (int64_t r = 0; r < nrows_; ++r) {
-            const uint64_t* row = reinterpret_cast<const uint64_t*>(rows_[r]);
-            uint64_t h = 0;
-            for (int64_t j = j0; j < j1; ++j) h += mcr::digest_term(row[j], (uint64_t)j);
-            partial_[(size_t)p * nrows_ + r] = h;
-        }
-    }
-    void work(int p) {
-        uint64_t seen = 0;
-        for (;;) {
-            uint64_t g = gen_.load(std::memory_order_acquire);
-            if (g == seen) {
-                const auto t0 = std::chrono::steady_clock::now();
-                while ((g = gen_.load(std::memory_order_acquire)) == seen &&
-                       std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(300)) {
-                }
-                if (g == seen) {
-                    std::unique_lock<std::mutex> lk(mu_);
-                    cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
-                    g = gen_.load(std::memory_order_acquire);
-                }
-            }
-            seen = g;
-            if (stop_) return;
-            if (p < parts_) block(p);
-            pending_.fetch_sub(1, std::memory_order_acq_rel);
-        }
-    }
-    std::mutex call_mu_, mu_;
-    std::condition_variable cv_;
-    std::vector<std::thread> workers_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<int> pending_{0};
-    bool stop_ = false;
-    const double* const* rows_ = nullptr;
-    int64_t nrows_ = 0, n_ = 0;
-    int parts_ = 1;
-    std::vector<uint64_t> partial_;
-};
 
 // cache for the stateless mc_ax_bu_f64 mirror: recompiled only when the topology changes
 struct AxBuCache {
@@ -1729,7 +1628,9 @@ int mc_host_digest(const double* rows, int64_t nrows, int64_t n, uint64_t* out) 
             std::fill(out, out + nrows, 0);
             return;
         }
-        DigestPool::get().run(rows, nrows, n, out);
+        std::vector<const double*> ptrs((size_t)nrows);
+        for (int64_t r = 0; r < nrows; ++r) ptrs[(size_t)r] = rows + r * n;
+        mcr::host_digest_rows(ptrs.data(), nrows, n, out);
     });
 }
 
@@ -1741,7 +1642,7 @@ int mc_host_digest2(const double* a, const double* b, int64_t n, uint64_t* out2)
             return;
         }
         const double* rows[2] = {a, b};
-        DigestPool::get().run_rows(rows, 2, n, out2);
+        mcr::host_digest_rows(rows, 2, n, out2);
     });
 }
 

@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void row_digests(const double* __restrict__ ro
     const double* row = rows + (int64_t)blockIdx.x * n;
     uint64_t h = 0;
     for (int64_t j = threadIdx.x; j < n; j += 256)
-        h += digest_term((uint64_t)__double_as_longlong(row[j]), (uint64_t)j);
+        h += digest_term_dev((uint64_t)__double_as_longlong(row[j]), (uint64_t)j);
     part[threadIdx.x] = h;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {

@@ -22,6 +22,8 @@
 
 #include <cstdint>
 
+#include "digest.hpp"
+
 namespace mcr {
 
 // (lanes, node slots per lane) the kernels are instantiated for (plan slots, chain).
@@ -234,15 +236,9 @@ hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase
                                int slots, double* out, int64_t n, int64_t t0, int64_t t1,
                                int64_t E, hipStream_t s);
 // reach-major out[j][t][e] for t in [0, T)
-// Row digest of fetched outputs (edit detection of the drop-in API's fused horizons,
-// mc_fetch_outputs_async / mc_host_digest): the sum mod 2^64 over j of
-//     t = (bits(row[j]) ^ (j * K1)) * K2;  t ^ (t >> 29)
-// The term is a bijection of the element's bits for a fixed j, so changing any one element
-// always changes the digest; the sum is order-free, so the device (one workgroup per row) and
-// the host (threads over column blocks) form the same value.
-constexpr uint64_t kDigestK1 = 0x9E3779B97F4A7C15ull;
-constexpr uint64_t kDigestK2 = 0xD6E8FEB86659FD93ull;
-__host__ __device__ inline uint64_t digest_term(uint64_t bits, uint64_t j) {
+// Row digest of fetched outputs (digest.hpp: definition, constants, the host side): the device
+// form of its term
+__device__ inline uint64_t digest_term_dev(uint64_t bits, uint64_t j) {
     uint64_t t = (bits ^ (j * kDigestK1)) * kDigestK2;
     return t ^ (t >> 29);
 }

@@ -29,7 +29,9 @@ LIB_PATH = os.path.join(LIB_DIR, "libmcroute.so")
 ARCH = os.environ.get("MCROUTE_ARCH", "gfx950")
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-function"]
-LIBS = ["-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"]
+LIBS = ["-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-pthread"]
+# host-only sources (*.cc: no device code) are built by the host C++ compiler
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall"]
 
 
 def _hipcc() -> str:
@@ -41,7 +43,15 @@ def _hipcc() -> str:
 
 def sources():
     return sorted(glob.glob(os.path.join(SRC_DIR, "*.cpp")) +
-                  glob.glob(os.path.join(SRC_DIR, "*.hip")))
+                  glob.glob(os.path.join(SRC_DIR, "*.hip")) +
+                  glob.glob(os.path.join(SRC_DIR, "*.cc")))
+
+
+def _cxx() -> str:
+    for cand in (os.environ.get("CXX"), shutil.which("g++"), shutil.which("c++")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("no host C++ compiler (g++) found")
 
 
 def _headers():
@@ -53,7 +63,7 @@ def source_hash() -> str:
     identity of a build.  Profiles measured on a build carry it (scripts/hbm_traffic.py) and
     bench.py reports a profile only for the build it was measured on."""
     import hashlib
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    h = hashlib.sha256(" ".join(FLAGS + HOST_FLAGS).encode())
     for p in sorted(sources() + _headers()):
         h.update(os.path.basename(p).encode())
         with open(p, "rb") as f:
@@ -94,7 +104,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 os.path.getmtime(obj) >= max(os.path.getmtime(src), t_hdr)):
             return
         tmp = obj + f".{os.getpid()}.tmp"
-        cmd = [hipcc] + FLAGS + ["-I", INCLUDE, "-I", SRC_DIR, "-c", "-o", tmp, src]
+        if src.endswith(".cc"):
+            cmd = [_cxx()] + HOST_FLAGS + ["-I", INCLUDE, "-I", SRC_DIR, "-c", "-o", tmp, src]
+        else:
+            cmd = [hipcc] + FLAGS + ["-I", INCLUDE, "-I", SRC_DIR, "-c", "-o", tmp, src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

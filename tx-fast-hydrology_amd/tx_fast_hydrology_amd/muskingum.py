@@ -601,6 +601,9 @@ class Muskingum:
         timedelta = self.timedelta
         rev = self._coef_rev[0]
         row_digest = engine.RowDigest()
+        # the reference formats its per-step debug message unconditionally; formatting a
+        # Timestamp costs more than the rest of a yielded step, so it is built only when emitted
+        debug = self.logger.isEnabledFor(logging.DEBUG)
         pending = []          # fetch tickets not yet waited for
         try:
             for c0 in range(0, T, chunk):
@@ -638,9 +641,10 @@ class Muskingum:
                             o_next, i_next = o_next.copy(), i_next.copy()
                         self.o_t_prev, self.i_t_prev = self.o_t_next, self.i_t_next
                         self.o_t_next, self.i_t_next = o_next, i_next
-                        self.datetime += timedelta
-                        self.logger.debug(f"Stepped to time {self.datetime}")
-                        expected_time = self.datetime
+                        # (a UTC Timestamp plus a Timedelta: the setter's checks hold)
+                        self._datetime = expected_time = self._datetime + timedelta
+                        if debug:
+                            self.logger.debug(f"Stepped to time {self.datetime}")
                         yield self
                         h_o, h_i = row_digest(o_next, i_next)
                         edited = h_o != digests[0, b0 + k] or h_i != digests[1, b0 + k]
