@@ -13,9 +13,7 @@ if [ "${1:-run}" = build ]; then
   mkdir -p $OUT
   for v in $VARIANTS; do
     name=${v%%:*}; flags=${v#*:}
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
-      -fno-fast-math -Iinclude -I$PKG/csrc ${flags//,/ } -o $OUT/lib_$name.so $PKG/csrc/*.cpp \
-      $PKG/csrc/*.hip -L/opt/rocm/lib -lrocsolver -lrocblas -Wl,-rpath,/opt/rocm/lib &
+    python $PKG/tx_fast_hydrology_amd/_build.py --variant $name ${flags//,/ } > /dev/null &
   done
   wait
   ls -la $OUT

@@ -686,7 +686,9 @@ __device__ __forceinline__ RunCells member_run(const MemberWin& mw, int64_t d, i
 // expression as the tick loop), both at the staging cell of (d, e); padding slots skipped
 // gain.G: pending analysis increments, applied as apply_gain (analysis.hip) would have applied
 // them to st_o / st_i first -- the same operations in the same order, so bit-identical.
-template <bool GAIN>
+// GAIN walks runs of 4 members per thread (RUN): the upstream gathers of the one-hop fold need
+// more threads in flight than the plain copy's runs of kMemberRun
+template <bool GAIN, int RUN>
 __global__ __launch_bounds__(256) void member_inputs(
         const double* __restrict__ F, int64_t mF, int64_t ns, int n_rows, int4 ent,
         const double* __restrict__ st_o, const double* __restrict__ st_i,
@@ -696,8 +698,8 @@ __global__ __launch_bounds__(256) void member_inputs(
     if (d >= ns) return;
     const uint8_t fl = mw.flags[d];
     if (fl == kSlotPad) return;
-    const int64_t e0 = (int64_t)blockIdx.y * kMemberRun;
-    const int ne = (int)(E - e0 < kMemberRun ? E - e0 : kMemberRun);
+    const int64_t e0 = (int64_t)blockIdx.y * RUN;
+    const int ne = (int)(E - e0 < RUN ? E - e0 : RUN);
     const RunCells rc = member_run(mw, d, e0);
     const double f = __hiloint2double(ent.w, ent.z);
     const int64_t rlo = (int64_t)clamp_row(ent.x, n_rows) * ns + d;
@@ -718,6 +720,7 @@ __global__ __launch_bounds__(256) void member_inputs(
             const double* Ge = gain.G + e * ns;
             const double og = fl == kSlotRouted ? 0.0 + Ge[d] : 0.0;
             double ig = 0.0;
+#pragma unroll 4
             for (int32_t q = u0; q < u1; ++q) ig = ig + (0.0 + Ge[gain.up[q]]);
             o = o + og;
             i = i + ig;
@@ -817,12 +820,19 @@ hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_r
                                 const PendingGain& gain) {
     if (ns * E == 0) return hipSuccess;
     if ((E + kMemberRun - 1) / kMemberRun > 65535) return hipErrorInvalidValue;
-    if (gain.G)
-        hipLaunchKernelGGL(member_inputs<true>, member_grid(ns, E), 256, 0, s, F, mF, ns, n_rows,
-                           ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
-    else
-        hipLaunchKernelGGL(member_inputs<false>, member_grid(ns, E), 256, 0, s, F, mF, ns, n_rows,
-                           ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+    constexpr int kGainRun = 4;
+    if (gain.G) {
+        if ((E + kGainRun - 1) / kGainRun > 65535) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((member_inputs<true, kGainRun>),
+                           dim3((unsigned)((ns + 255) / 256),
+                                (unsigned)((E + kGainRun - 1) / kGainRun)),
+                           256, 0, s, F, mF, ns, n_rows, ent, st_o, st_i,
+                           reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+    } else {
+        hipLaunchKernelGGL((member_inputs<false, kMemberRun>), member_grid(ns, E), 256, 0, s, F,
+                           mF, ns, n_rows, ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm,
+                           E, mw, gain);
+    }
     return hipGetLastError();
 }
 

@@ -128,5 +128,40 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB_PATH
 
 
+def build_variant(name: str, extra_flags, verbose: bool = False) -> str:
+    """Diagnostic / A-B build of the whole library with extra compile flags (e.g. an MCR_EXP_*
+    switch) into lib/exp/lib_<name>.so; bench.py / tests load it with MCROUTE_LIB=<path>."""
+    out_dir = os.path.join(LIB_DIR, "exp")
+    obj_dir = os.path.join(out_dir, "obj_" + name)
+    os.makedirs(obj_dir, exist_ok=True)
+    hipcc = _hipcc()
+    extra = list(extra_flags)
+
+    def compile_one(src):
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if src.endswith(".cc"):
+            cmd = [_cxx()] + HOST_FLAGS + extra + ["-I", INCLUDE, "-I", SRC_DIR, "-c", "-o",
+                                                     obj, src]
+        else:
+            cmd = [hipcc] + FLAGS + extra + ["-I", INCLUDE, "-I", SRC_DIR, "-c", "-o", obj,
+                                             src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        return obj
+
+    srcs = sources()
+    with ThreadPoolExecutor(max_workers=min(len(srcs), 6)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    path = os.path.join(out_dir, f"lib_{name}.so")
+    subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", path] +
+                          objs + LIBS)
+    return path
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":
+        # python _build.py --variant NAME [-DFLAG ...]
+        print(build_variant(sys.argv[2], sys.argv[3:], verbose=True))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))
