@@ -149,6 +149,24 @@ def test_huc8_day_golden(golden, monkeypatch):
     assert np.array_equal(sha, g["o_sha"])
 
 
+def test_column_order_check_sees_reach_id_edits(golden, monkeypatch):
+    """The frame-in-reach-order check is cached per column Index; an in-place edit of the
+    model's reach_ids list (two ids swapped) must select the frame's columns again."""
+    use_oracle_device(monkeypatch)
+    g = golden("g1_ynet.npz")
+    m = golden_model(g)
+    df = golden_frame(g, list(m.reach_ids))
+    assert not np.array_equal(df.iloc[:, 0], df.iloc[:, 1])
+    o_ref, _, _ = run(m, df)                     # caches the check for df.columns
+    m.datetime = pd.Timestamp(int(g["start_ns"]), tz="UTC")
+    m.init_states(o_t_next=g["o0"])
+    m.reach_ids[0], m.reach_ids[1] = m.reach_ids[1], m.reach_ids[0]
+    o_sw, _, _ = run(m, df)
+    swapped = pd.DataFrame(df[m.reach_ids].values, index=df.index, columns=df.columns)
+    o_exp, _, _ = run(golden_model(g), swapped)
+    assert np.array_equal(o_sw, o_exp) and not np.array_equal(o_sw, o_ref)
+
+
 def test_dt_change_quirk(golden, monkeypatch):
     use_oracle_device(monkeypatch)
     g = golden("g6_dt_change.npz")

@@ -26,10 +26,6 @@
 
 #pragma clang fp contract(off)
 
-#ifndef MCR_EXP_NO_GAIN_FUSION
-#define MCR_EXP_NO_GAIN_FUSION 0   // A/B: settle the analysis gain with apply_gain, not in staging
-#endif
-
 namespace {
 
 using namespace mcr::capi;
@@ -967,7 +963,6 @@ struct Net {
                 double* IOp = IOb.p;
                 const mcr::MemberWin mw = member_win();
                 mcr::PendingGain pg;
-                if (gain_pending && MCR_EXP_NO_GAIN_FUSION) settle_gain();
                 if (gain_pending) pg = mcr::PendingGain{Gn.p, sup_off.p, sup.p};
                 HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
                                                st_i.p, IOp, Qm.p, E, mw, stream, pg));
