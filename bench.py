@@ -95,7 +95,7 @@ def parse(argv=None, world=None):
     ap.add_argument("--huc8", action="store_true",
                     help="BASELINE configs[0]: one HUC-8 sub-basin (1000 reaches, one outlet, "
                          "deepest path ~100 reaches), deterministic")
-    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow", "ensemble"],
+    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow", "ensemble", "sweep"],
                     help="execution path (mcroute.h mc_set_mode); 'ensemble': the whole horizon "
                          "of every member as one dataflow launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

@@ -239,9 +239,14 @@ int mc_get_timing(void* net, double* kernel_ms, int64_t* launches, double* run_m
 int mc_reset_timing(void* net);
 
 /* Execution path of mc_run / mc_step.  mode 0 (default): one resident dataflow launch for the
- * whole horizon when the network fits the device at once, else launches of `tile` ticks;
- * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit).
- * last_path: 1 or 2 = the path the last run took (0 before any run). */
+ * whole horizon when the network fits the device at once, else launches of `tile` ticks; an
+ * ensemble horizon of an even number >= 32 of members (T >= 2) runs as a member sweep (the members on the lanes of
+ * a member plan of its own, sweep.hpp) when its forcing rows allow (no 8 consecutive steps
+ * touching more than 3 rows or starting 2 rows apart) and the network has such a plan;
+ * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit);
+ * 3: auto + ensemble-dataflow horizons; 4: member sweep for every ensemble horizon (MC_E_STATE
+ * when one cannot run as a sweep).
+ * last_path: 1 launches, 2 dataflow, 3 member sweep (0 before any run). */
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);
 

@@ -44,6 +44,7 @@ def test_ensemble_members_bitexact(n, E, slots, T, chain):
     n = end.size
     x = xp[0] + 300e9 * np.arange(1, T + 1)
     net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=E, chain=chain)
+    net.set_mode("launches")             # (auto takes the member sweep from 32 members)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
     got_o, got_i = net.simulate(x, xp, fpe)
@@ -315,4 +316,91 @@ def test_ensemble_dataflow_needs_an_acyclic_workgroup_graph():
         want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
                                        np.ascontiguousarray(fpe[:, :, e]))
         assert np.array_equal(got_o[:, :, e], want_o), e
+    net.close()
+
+
+@pytest.mark.parametrize("n,E,T,rows,mode", [(3000, 64, 60, 7, "sweep"), (2500, 40, 45, 5, "auto"),
+                                             (1500, 130, 33, 4, "sweep"),
+                                             (4000, 32, 100, 10, "auto")])
+def test_member_sweep_bitexact(n, E, T, rows, mode):
+    """Member sweep (sweep.hip: the members on the lanes of a member plan of its own): every
+    member bit-identical to its serial oracle run -- step outputs and inflows, series, final
+    state -- for a full member group (64), a partial one (40: lanes beyond E idle), three groups
+    (130) and horizons that are not a multiple of the 8-tick chunk; continued over two horizons
+    (the state hand-over through the session layout) and on with the multi-launch path."""
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4, 120, n + E, E, rows=rows)
+    n = end.size
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
+    net.set_mode(mode)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fpe)
+    cut = T // 3
+    net.run(x[:cut])
+    assert net.mode()[1] == "sweep"
+    a_o, a_i = net.fetch_outputs(0, cut)
+    net.run(x[cut:])
+    assert net.mode()[1] == "sweep"
+    b_o, b_i = net.fetch_outputs(0, T - cut)
+    ser_o, ser_i = net.fetch_series()
+    so, si = net.get_state()
+    net.set_mode("launches")            # the session state after a sweep continues elsewhere
+    net.run(x[-3:] + 600e9)
+    c_o, _ = net.fetch_outputs(0, 3)
+    for e in range(E):
+        fe = np.ascontiguousarray(fpe[:, :, e])
+        want_o, want_i, fo, fi = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x,
+                                              xp, fe)
+        assert np.array_equal(a_o[:, :, e], want_o[:cut]), e
+        assert np.array_equal(a_i[:, :, e], want_i[:cut]), e
+        assert np.array_equal(b_o[:, :, e], want_o[cut:]), e
+        assert np.array_equal(b_i[:, :, e], want_i[cut:]), e
+        assert np.array_equal(ser_o[:, :, e], want_o[cut:].T), e
+        assert np.array_equal(ser_i[:, :, e], want_i[cut:].T), e
+        assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
+        w3, _, _, _ = orc.simulate(start, end, indeg, *coef, fo, fi, x[-3:] + 600e9, xp, fe)
+        assert np.array_equal(c_o[:, :, e], w3), e
+    net.close()
+
+
+def test_member_sweep_needs_sparse_forcing_rows():
+    """A step as long as the forcing interval (8 steps touch 9 rows) cannot keep its rows in the
+    sweep's 3-row window: auto routes it with launches, sweep mode refuses it."""
+    E, T = 32, 20
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 9, E, rows=30)
+    x = xp[0] + 3600e9 * np.arange(1, T + 1)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fpe)
+    net.run(x)
+    assert net.mode()[1] == "launches"
+    got_o, _ = net.fetch_outputs(0, T)
+    e = 5
+    want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                   np.ascontiguousarray(fpe[:, :, e]))
+    assert np.array_equal(got_o[:, :, e], want_o)
+    net.set_mode("sweep")
+    with pytest.raises(engine.nat.RoutingError):
+        net.run(x)
+    net.close()
+
+
+def test_member_sweep_needs_an_even_ensemble():
+    """An odd ensemble (the store wave copies two members per lane) routes with launches."""
+    E, T = 33, 20
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 11, E)
+    x = xp[0] + 300e9 * np.arange(1, T + 1)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fpe)
+    net.run(x)
+    assert net.mode()[1] == "launches"
+    got_o, _ = net.fetch_outputs(0, T)
+    e = E - 1
+    want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
+                                   np.ascontiguousarray(fpe[:, :, e]))
+    assert np.array_equal(got_o[:, :, e], want_o)
     net.close()

@@ -23,6 +23,7 @@
 #include "digest.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
+#include "sweep.hpp"
 
 #pragma clang fp contract(off)
 
@@ -186,6 +187,34 @@ struct Net {
 
     // outputs of the last run are the {o, i} pairs of a member-dataflow step (IOb, member windows)
     bool out_io = false;
+
+    // ---- member sweep (sweep.hip): ensemble horizons with the members on the lanes, on a member
+    // plan of its own (kSweepSlots slots per workgroup, chain 1), built on first use
+    std::vector<int64_t> topo_end, topo_deg, topo_heads;
+    struct Sweep {
+        mcr::Plan plan;
+        DBuf<int32_t> G, ext_off, ext_slot, ext_g, mmap, rmap, wg_gmin, wg_gmax;
+        DBuf<uint8_t> flags, up_cnt;
+        DBuf<uint64_t> up4;
+        DBuf<double> coef, So, Si, F, O;
+        DBuf<int64_t> jbase;           // caller reach -> member-plan slot * E (fetches)
+        int64_t jbase_E = 0, f_E = 0, f_rows = 0;
+        uint64_t coef_ver = 0, f_ver = 0;   // versions of the session arrays these came from
+        struct Sch {
+            int64_t T = -1;
+            std::vector<int64_t> off;
+            std::vector<int32_t> list;
+            DBuf<int32_t> active;
+            uint64_t used = 0;
+        };
+        std::vector<std::unique_ptr<Sch>> scheds;
+    };
+    std::unique_ptr<Sweep> sw;
+    int sweep_state = 0;             // 1 built, -1 the network has no member plan the kernel takes
+    uint64_t coef_ver = 1, f_ver = 1;   // bumped by set_coeffs / load_forcing / corrections
+    bool out_sweep = false;          // the outputs of the last run are in sw->O
+    // auto mode takes the sweep from this many members (below it the lanes are mostly idle)
+    static constexpr int64_t kSweepMinMembers = 32;
     // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
     DBuf<int64_t> mwbase;
     int64_t mw_E = 0, mw_cells = 0;
@@ -269,6 +298,9 @@ struct Net {
               int64_t n_head, const mcr::PlanParams& p) {
         const std::string err = mcr::build_plan(n, endnodes, indegree, heads, n_head, p, plan);
         if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
+        topo_end.assign(endnodes, endnodes + n);
+        topo_deg.assign(indegree, indegree + n);
+        topo_heads.assign(heads, heads + n_head);
         if (plan.p.tile % mcr::kChunk != 0)
             throw Fail(MC_E_INVALID, "tile must be a multiple of 16 for the device sweep");
         if (!mcr::wavefront_shape_ok(plan.p.slots, plan.p.chain))
@@ -819,6 +851,7 @@ struct Net {
                                          stream));
         sync();  // `stage` is reused by the next call
         coeffs_set = true;
+        ++coef_ver;
     }
 
     void set_state(const double* o, const double* i) {
@@ -875,6 +908,193 @@ struct Net {
         }
     }
 
+    // ---- member sweep ----------------------------------------------------------------------
+    bool ensure_sweep() {
+        if (sweep_state != 0) return sweep_state > 0;
+        sweep_state = -1;
+        auto S = std::make_unique<Sweep>();
+        mcr::PlanParams pp;
+        pp.slots = mcr::kSweepSlots;
+        pp.tile = mcr::kSweepTile;
+        pp.ext_cap = 4;
+        pp.chain = 1;
+        const std::string err =
+            mcr::build_plan(plan.n, topo_end.data(), topo_deg.data(), topo_heads.data(),
+                            (int64_t)topo_heads.size(), pp, S->plan);
+        const mcr::Plan& P = S->plan;
+        if (!err.empty() || P.max_ext_wg > mcr::kSweepMaxExt ||
+            P.p.tile + mcr::kChunk + 1 + P.max_span > mcr::kSweepTabCap ||
+            P.nslots >= ((int64_t)1 << 31) / 8)
+            return false;
+        const size_t ns = (size_t)P.nslots;
+        S->G.upload(P.G.data(), ns, stream);
+        S->flags.upload(P.flags.data(), ns, stream);
+        S->up_cnt.upload(P.up_cnt.data(), ns, stream);
+        S->up4.upload(P.up4.data(), ns, stream);
+        S->ext_off.upload(P.ext_off.data(), P.ext_off.size(), stream);
+        S->wg_gmin.upload(P.wg_gmin.data(), P.wg_gmin.size(), stream);
+        S->wg_gmax.upload(P.wg_gmax.data(), P.wg_gmax.size(), stream);
+        std::vector<int32_t> xs(std::max<size_t>(P.ext_src.size(), 1), 0);
+        for (size_t x = 0; x < P.ext_src.size(); ++x) {
+            const int64_t src = P.ext_src[x];
+            xs[x] = (int32_t)(src < P.n ? P.pos[src] : src - P.n);
+        }
+        S->ext_slot.upload(xs.data(), xs.size(), stream);
+        S->ext_g.upload(P.ext_g.data(), std::max<size_t>(P.ext_g.size(), 1), stream);
+        std::vector<int32_t> mm((size_t)std::max<int64_t>(plan.nslots, 1), -1);
+        for (int64_t d = 0; d < plan.nslots; ++d)
+            if (plan.slot_reach[d] >= 0) mm[d] = (int32_t)P.pos[plan.slot_reach[d]];
+        S->mmap.upload(mm.data(), mm.size(), stream);
+        std::vector<int32_t> rm(std::max<size_t>(ns, 1), -1);
+        for (size_t d = 0; d < ns; ++d)
+            if (P.slot_reach[d] >= 0) rm[d] = (int32_t)plan.pos[P.slot_reach[d]];
+        S->rmap.upload(rm.data(), rm.size(), stream);
+        S->coef.reserve(4 * ns);
+        sync();
+        sw = std::move(S);
+        sweep_state = 1;
+        return true;
+    }
+
+    // Can this horizon run as a member sweep?  Forcing windows: the steps of any 8-step chunk
+    // touch at most 3 rows and consecutive chunks start at most one row apart (sweep.hip).
+    bool sweep_fits(int64_t T, const double* Fsrc, const std::vector<int4>& tab) {
+        if (mode == 1 || mode == 2 || mode == 3 || force_mode == 1) return false;
+        const bool want = mode == 4 || E >= kSweepMinMembers;
+        // (E even: the store wave copies two members per lane)
+        if (!want || E < 2 || E % 2 || T < 2 || Fsrc != F.p) return false;
+        auto at = [&](int64_t t) { return tab[t < 0 ? 0 : (t >= T ? T - 1 : t)]; };
+        for (int64_t t = -mcr::kChunk; t < T; ++t) {
+            const int4 a0 = at(t), a7 = at(t + mcr::kChunk - 1), a8 = at(t + mcr::kChunk);
+            if (std::max(a7.x, a7.y) - a0.x + 1 > 3 || a8.x - a0.x > 1) return false;
+        }
+        if (!ensure_sweep()) return false;
+        return sw->plan.nslots * E * 8 < ((int64_t)1 << 31) && T < (1 << 28);
+    }
+
+    void run_sweep(int64_t T, int64_t rows) {
+        Sweep& S = *sw;
+        const mcr::Plan& P = S.plan;
+        const int64_t ns = P.nslots, nsm = plan.nslots;
+        if (S.coef_ver != coef_ver) {
+            HIPC(mcr::launch_sweep_coeffs(alpha.p, beta.p, chi.p, gamma.p, S.rmap.p, S.flags.p,
+                                          S.coef.p, ns, stream));
+            S.coef_ver = coef_ver;
+        }
+        if (S.f_ver != f_ver || S.f_E != E || S.f_rows != rows) {
+            // forcing in member-plan order (slots without a reach read 0)
+            const size_t cells = (size_t)(rows * ns * E);
+            S.F.reserve(cells);
+            HIPC(hipMemsetAsync(S.F.p, 0, cells * sizeof(double), stream));
+            HIPC(mcr::launch_to_sweep(F.p, rows * nsm, nsm, rows, S.mmap.p, S.F.p, ns, E, stream));
+            S.f_ver = f_ver;
+            S.f_E = E;
+            S.f_rows = rows;
+        }
+        if (S.jbase_E != E) {
+            std::vector<int64_t> jb((size_t)std::max<int64_t>(plan.n, 1), 0);
+            for (int64_t j = 0; j < plan.n; ++j) jb[j] = P.pos[j] * E;
+            S.jbase.upload(jb.data(), jb.size(), stream);
+            S.jbase_E = E;
+        }
+        S.So.reserve((size_t)(ns * E));
+        S.Si.reserve((size_t)(ns * E));
+        S.O.reserve((size_t)(T * ns * E));
+        HIPC(mcr::launch_sweep_zero_free(S.rmap.p, S.So.p, S.Si.p, ns, E, stream));
+        HIPC(mcr::launch_to_sweep(st_o.p, nsm, nsm, 1, S.mmap.p, S.So.p, ns, E, stream));
+        HIPC(mcr::launch_to_sweep(st_i.p, nsm, nsm, 1, S.mmap.p, S.Si.p, ns, E, stream));
+        // active workgroups of each launch, cached per horizon length
+        Sweep::Sch* sc = nullptr;
+        for (auto& c : S.scheds)
+            if (c->T == T) sc = c.get();
+        if (!sc) {
+            if (S.scheds.size() >= 4) S.scheds.erase(S.scheds.begin());
+            S.scheds.push_back(std::make_unique<Sweep::Sch>());
+            sc = S.scheds.back().get();
+            sc->T = T;
+            mcr::active_schedule(P, T, sc->list, sc->off);
+            sc->active.upload(sc->list.data(), std::max<size_t>(sc->list.size(), 1), stream);
+        }
+        mcr::SweepArgs a{};
+        a.wg_gmin = S.wg_gmin.p;
+        a.wg_gmax = S.wg_gmax.p;
+        a.G = S.G.p;
+        a.flags = S.flags.p;
+        a.up_cnt = S.up_cnt.p;
+        a.up4 = S.up4.p;
+        a.ext_off = S.ext_off.p;
+        a.ext_slot = S.ext_slot.p;
+        a.ext_g = S.ext_g.p;
+        a.coef = S.coef.p;
+        a.So = S.So.p;
+        a.Si = S.Si.p;
+        a.F = S.F.p;
+        a.stab = stab.p;
+        a.O = S.O.p;
+        a.rowB = (uint32_t)(ns * E * 8);
+        a.E = (int32_t)E;
+        a.T = (int32_t)T;
+        a.n_rows = (int32_t)rows;
+        a.tile = P.p.tile;
+        const int64_t nl = (int64_t)sc->off.size() - 1;
+        const int groups = (int)((E + 63) / 64);
+        if (timing) {
+            ensure_events(2 * (size_t)nl + 2);
+            HIPC(hipEventRecord(events[2 * nl], stream));
+        }
+        int64_t launched = 0;
+        trace_launch.clear();
+        trace_wg.clear();
+        if (trace) {
+            trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(sc->off[nl], 1));
+            trace_wg = sc->list;
+        }
+        for (int64_t k = 0; k < nl; ++k) {
+            const int64_t grid = sc->off[k + 1] - sc->off[k];
+            if (grid == 0) continue;
+            a.active = sc->active.p + sc->off[k];
+            a.k0 = (int32_t)(k * P.p.tile);
+            if (trace) {
+                a.trace = trace_buf.p + mcr::kTraceWords * sc->off[k];
+                trace_launch.resize(sc->off[k + 1], k);
+            }
+            if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
+            HIPC(mcr::launch_member_sweep(a, (int)grid, groups, stream));
+            if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
+            ++launched;
+        }
+        HIPC(mcr::launch_from_sweep(S.So.p, ns, S.mmap.p, st_o.p, nsm, E, stream));
+        HIPC(mcr::launch_from_sweep(S.Si.p, ns, S.mmap.p, st_i.p, nsm, E, stream));
+        if (timing) {
+            HIPC(hipEventRecord(events[2 * nl + 1], stream));
+            HIPC(hipEventSynchronize(events[2 * nl + 1]));
+            for (int64_t k = 0; k < launched; ++k) {
+                float ms = 0.f;
+                HIPC(hipEventElapsedTime(&ms, events[2 * k], events[2 * k + 1]));
+                kernel_ms += ms;
+            }
+            float ms = 0.f;
+            HIPC(hipEventElapsedTime(&ms, events[2 * nl], events[2 * nl + 1]));
+            run_ms += ms;
+            launches += launched;
+        }
+        out_sweep = true;
+        last_flow.valid = false;
+        last_path = 3;
+    }
+
+    // the outputs of the last run, as the gather kernels address them
+    struct OutView {
+        const double* O;
+        int64_t mO;
+        const int64_t* jbase;
+        int64_t stride;
+    };
+    OutView out_view() const {
+        if (out_sweep) return {sw->O.p, 1, sw->jbase.p, sw->plan.nslots * E};
+        return {O.p, cur->Otot, cur->jbase.p, (int64_t)row_width()};
+    }
+
     // Run T steps using forcing buffer `Fsrc` with `rows` rows and the host step table.
     void run_tables(int64_t T, const double* Fsrc, int64_t rows, const std::vector<int4>& tabh) {
         REQUIRE(coeffs_set, "mc_set_coeffs must be called before running");
@@ -901,6 +1121,18 @@ struct Net {
             stab_host = tabh;
         }
         last_path = 0;
+        out_io = false;
+        out_sweep = false;
+        if (E > 1 && T > 1 && sweep_fits(T, Fsrc, tabh)) {
+            settle_gain();
+            run_sweep(T, rows);
+            T_out = T;
+            return;
+        }
+        if (mode == 4)
+            throw Fail(MC_E_STATE, "sweep mode requested but this horizon cannot run as a member "
+                                   "sweep (one member, one step, forcing rows too dense for the "
+                                   "step, or no member plan for this network)");
         ensure_schedule(T);
         const int64_t nl = (int64_t)cur->off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
@@ -1139,6 +1371,7 @@ struct Net {
         const int64_t n = plan.n;
         xp.assign(xps, xps + rows);
         n_rows = rows;
+        ++f_ver;
         F.reserve((size_t)(rows * plan.nslots * E));
         if (n == 0) return;
         // caller-order staging: kept between calls when small (sub-basin sessions reload their
@@ -1207,10 +1440,11 @@ struct Net {
             if (out_io)                    // T = 1: t0 = 0, t1 = 1
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, outT.p, n, E,
                                            stream));
-            else
-                HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p,
-                                              in_list.p, c == 1, row_width(), outT.p, n, t0, t1,
-                                              E, stream));
+            else {
+                const OutView ov = out_view();
+                HIPC(mcr::launch_gather_steps(ov.O, ov.mO, ov.jbase, in_off.p, in_list.p, c == 1,
+                                              (int)ov.stride, outT.p, n, t0, t1, E, stream));
+            }
             HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             sync();
@@ -1247,9 +1481,11 @@ struct Net {
             double* buf = c == 0 ? outT.p : outT2.p;
             if (out_io)
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, buf, n, E, stream));
-            else
-                HIPC(mcr::launch_gather_steps(O.p, cur->Otot, cur->jbase.p, in_off.p, in_list.p,
-                                              c == 1, row_width(), buf, n, t0, t1, E, stream));
+            else {
+                const OutView ov = out_view();
+                HIPC(mcr::launch_gather_steps(ov.O, ov.mO, ov.jbase, in_off.p, in_list.p, c == 1,
+                                              (int)ov.stride, buf, n, t0, t1, E, stream));
+            }
             if (dg) {
                 HIPC(mcr::launch_row_digests(buf, k, n * E, dig.p + c * k, stream));
                 HIPC(hipMemcpyAsync(dg, dig.p + c * k, (size_t)k * sizeof(uint64_t),
@@ -1292,10 +1528,11 @@ struct Net {
             if (out_io)                    // T = 1: [j][0][e] is the step layout
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, k == 1, outT.p, n, E,
                                            stream));
-            else
-                HIPC(mcr::launch_gather_series(O.p, cur->Otot, cur->jbase.p, in_off.p,
-                                               in_list.p, k == 1, row_width(), outT.p, n, T_out,
-                                               E, stream));
+            else {
+                const OutView ov = out_view();
+                HIPC(mcr::launch_gather_series(ov.O, ov.mO, ov.jbase, in_off.p, in_list.p, k == 1,
+                                               (int)ov.stride, outT.p, n, T_out, E, stream));
+            }
             HIPC(hipMemcpyAsync(dst, outT.p, bytes, hipMemcpyDeviceToHost, stream));
             sync();
         }
@@ -1552,7 +1789,8 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         REQUIRE(D->E == 1 && S->E == 1, "lateral corrections route single-member sessions");
         REQUIRE(0 <= dst_reach && dst_reach < D->plan.n && 0 <= src_reach && src_reach < S->plan.n,
                 "reach index out of range");
-        REQUIRE(S->T_out > 0 && S->cur && !S->out_io, "the source session has no horizon outputs");
+        REQUIRE(S->T_out > 0 && S->cur && !S->out_io && !S->out_sweep,
+                "the source session has no horizon outputs");
         REQUIRE(D->n_rows == S->T_out,
                 "the destination's forcing rows must be the source horizon's steps (one input "
                 "row per step, as the reference's positional add requires)");
@@ -1570,6 +1808,7 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, S->row_width(),
                                             o_start, alpha, beta, gamma, D->F.p, D->plan.nslots,
                                             D->plan.pos[dst_reach], S->T_out, D->stream));
+        ++D->f_ver;
         HIPC(hipEventRecord(ev, D->stream));
         HIPC(hipStreamWaitEvent(S->stream, ev, 0));
     });
@@ -1687,9 +1926,9 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 3,
-                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow) or 3 (auto + ensemble "
-                "dataflow horizons)");
+        REQUIRE(mode >= 0 && mode <= 4,
+                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow), 3 (auto + ensemble "
+                "dataflow horizons) or 4 (member sweep)");
         as_net(net)->mode = mode;
     });
 }

@@ -52,7 +52,9 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     const int64_t C = params.slots;
     const int32_t B = params.tile;
     if (n < 0) return "n must be >= 0";
-    if (C < 64 || C > 512 || (C % 64) != 0) return "slots must be a multiple of 64 in [64, 512]";
+    // 32: the member sweep's plans (sweep.hpp, chain 1; no lane-per-slot kernel runs them)
+    if (!(C == 32 && params.chain == 1) && (C < 64 || C > 512 || (C % 64) != 0))
+        return "slots must be a multiple of 64 in [64, 512]";
     if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
     if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";
     const int K = params.chain;

@@ -1,0 +1,448 @@
+// Member sweep (sweep.hpp): the ensemble forecast with the members on the lanes.
+//
+// One workgroup = kSweepNW waves = the kSweepSlots node slots of one member-plan workgroup; wave
+// v routes slots v * NPW .. v * NPW + NPW - 1 for 64 members (lane = member, blockIdx.y = member
+// group).  Per node everything that decides control flow or addresses is wave-uniform (the
+// node's step at this tick, its inputs, coefficients and forcing rows), so the tick is scalar
+// control plus f64 arithmetic on 64 members, and every global access is one 512-byte row.
+//
+// Tick k (node d runs step t = k - G[d] when 0 <= t < T):
+//   reads   the inputs' outputs of tick k - 1 from the LDS buffer of parity (k - 1) & 1: a row
+//           per node slot (in-cluster inputs, unit slack), a zero row, and a row per external
+//           input of the workgroup (staged there by its owner wave during tick k - 1);
+//   routes  I = ((0 + x1) + x2) + ...,  o = 0 + (((alpha I + beta I_prev) + chi o_prev) + gamma q),
+//           q = (1 - frac) f[lo] + frac f[hi]   (nutils.py:23-33, 80-83; FMA contraction off);
+//   writes  o to the LDS buffer of parity k & 1 and to O[t][d][.] (non-temporal);
+//   stages  external inputs for tick k + 1, loaded kRing - 1 ticks earlier into a register ring
+//           (every input of another workgroup was produced in an earlier launch: tile slack);
+//   then one workgroup barrier.
+// Forcing rows: a node keeps the 3 rows its steps of the current 8-tick chunk can touch (rows of
+// clamped steps outside [0, T) are those of step 0 / T - 1, so the window is right when the
+// node starts) and prefetches the next one a chunk ahead.  Host-checked: no chunk spans more
+// than 3 rows and consecutive chunks start at most one row apart.
+// Every buffer access has a fixed instruction count (inactive rows use empty buffer records or
+// out-of-range offsets), so the wait counts the compiler places are exact: the tick never waits
+// for its own output stores.
+#include "sweep.hpp"
+
+#include "kernels.hpp"
+#include "plan.hpp"
+
+#pragma clang fp contract(off)
+
+// minimum waves per SIMD the register allocation targets (4: two workgroups per CU at <= 128
+// VGPRs, with some spilling; 1: the compiler's choice, 134 VGPRs = 3 waves per SIMD)
+#ifndef MCR_SWEEP_MIN_WAVES
+#define MCR_SWEEP_MIN_WAVES 1
+#endif
+
+namespace mcr {
+
+namespace {
+
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+
+constexpr unsigned kRow = 512;   // LDS / global row: 64 members x f64
+constexpr int kRing = 4;         // external-input register ring (ticks of prefetch + 1)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_at(uintptr_t p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(p), (short)0, (int)bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return __hiloint2double((int)v.y, (int)v.x);
+}
+template <int AUX>
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, double x) {
+    u32x2_t v;
+    v.x = (unsigned)__double2loint(x);
+    v.y = (unsigned)__double2hiint(x);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, AUX);
+}
+__device__ __forceinline__ double lds_ld(const char* lds, unsigned byte) {
+    return *reinterpret_cast<const double*>(lds + byte);
+}
+__device__ __forceinline__ void lds_st(char* lds, unsigned byte, double x) {
+    *reinterpret_cast<double*>(lds + byte) = x;
+}
+__device__ __forceinline__ int clamp_t(int t, int T) { return t < 0 ? 0 : (t < T ? t : T - 1); }
+
+// NPW node slots per compute wave, NW compute waves, XW external inputs staged per compute wave,
+// plus one store wave.  LDS: the step-table window of the launch, the workgroup's coefficients
+// and G, two parity buffers of rows.
+template <int NPW, int NW, int XW>
+__global__ __launch_bounds__(64 * (NW + 1), MCR_SWEEP_MIN_WAVES)
+void member_sweep(SweepArgs a) {
+    constexpr int RS = NPW * NW;
+    constexpr unsigned TAB = 0;                                   // int4 [kSweepTabCap]
+    constexpr unsigned COEF = TAB + 16u * kSweepTabCap;           // double [RS][4]
+    constexpr unsigned GT = COEF + 32u * RS;                      // int [RS]
+    constexpr unsigned XB = GT + 4u * RS;                         // [2][RS + 1 + NW XW] rows
+    constexpr unsigned BUF = (RS + 1 + NW * XW) * kRow;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int w = a.active[blockIdx.x];
+    const int T = a.T, k0 = a.k0, tile = a.tile, nrow = a.n_rows, E = a.E;
+    const uint32_t rowB = a.rowB;
+    const int e = (int)blockIdx.y * 64 + lane;
+    const unsigned eo = e < E ? (unsigned)e * 8u : 0x80000000u;   // beyond E: out of range
+    const unsigned l8 = (unsigned)lane * 8u;
+    const uintptr_t Fb = reinterpret_cast<uintptr_t>(a.F);
+    const uintptr_t Ob = reinterpret_cast<uintptr_t>(a.O);
+    const bool tr = a.trace != nullptr && blockIdx.y == 0 && threadIdx.x == 0;
+    const int64_t t_start = tr ? wall_clock64() : 0;
+
+    // ---- step-table window: every (clamped) step a node of this workgroup looks up in the
+    // launch, [tw0, tw1]; lookups outside it are clamped into it (non-live slots only)
+    const int gmin = a.wg_gmin[w], gmax = a.wg_gmax[w];
+    const int tw0 = clamp_t(k0 - gmax, T), tw1 = clamp_t(k0 + tile + kChunk - gmin, T);
+    for (int i = threadIdx.x; i <= tw1 - tw0; i += 64 * (NW + 1))
+        reinterpret_cast<int4*>(lds + TAB)[i] = a.stab[tw0 + i];
+
+    if (wv == NW) {
+        // ================= store wave: during tick k it copies the rows of tick k - 1 (stable
+        // until the barrier that ends tick k) to O, two node rows per instruction (16 B = two
+        // members per lane; E is even); it never waits for its stores
+        __syncthreads();                                 // table window, G of every slot
+        const int half = lane >> 5;
+        const unsigned m2 = (unsigned)(lane & 31) * 16u;
+        const int em = (int)blockIdx.y * 64 + 2 * (lane & 31);
+        const bool mok = em < E;                         // member pair inside the ensemble
+        int Gl[RS / 2];
+#pragma unroll
+        for (int m = 0; m < RS / 2; ++m)
+            Gl[m] = *reinterpret_cast<const int*>(lds + GT + 4u * (unsigned)(2 * m + half));
+        const int64_t nsE = (int64_t)(rowB / 8u);        // ns * E
+        auto copy_rows = [&](int k) {                    // outputs of tick k
+            const unsigned buf = XB + (unsigned)(k & 1) * BUF;
+#pragma unroll
+            for (int m = 0; m < RS / 2; ++m) {
+                const int c = 2 * m + half;
+                const int t = k - Gl[m];
+                if ((unsigned)t < (unsigned)T && mok) {
+                    typedef double d2 __attribute__((ext_vector_type(2)));
+                    const d2 v = *reinterpret_cast<const d2*>(lds + buf + (unsigned)c * kRow + m2);
+                    const int64_t d = (int64_t)w * RS + c;
+                    d2* dst = reinterpret_cast<d2*>(Ob + (uintptr_t)(((int64_t)t * nsE +
+                                                                      d * E + em) * 8));
+                    __builtin_nontemporal_store(v, dst);
+                }
+            }
+        };
+        __syncthreads();                                 // prologue of the compute waves
+        for (int k = k0; k < k0 + tile; ++k) {
+            if (k > k0) copy_rows(k - 1);
+            __syncthreads();
+        }
+        copy_rows(k0 + tile - 1);
+        return;
+    }
+
+    // ================= compute waves
+    // uniform table entry of step t (clamped into [0, T) and the window)
+    auto tab_at = [&](int t) -> int4 {
+        int c = clamp_t(t, T);
+        c = c < tw0 ? tw0 : (c > tw1 ? tw1 : c);
+        const int4 v = *reinterpret_cast<const int4*>(lds + TAB + 16u * (unsigned)(c - tw0));
+        return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                         __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+    };
+    int G[NPW], rb[NPW], cnt[NPW];
+    uint64_t up[NPW];
+    unsigned vo[NPW];
+    double op[NPW], ip[NPW], f0[NPW], f1[NPW], f2[NPW];
+    const auto so = rec(a.So, rowB), si = rec(a.Si, rowB);
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) {
+        const int c = wv * NPW + p;
+        const int64_t d = (int64_t)w * RS + c;
+        const uint8_t fl = a.flags[d];
+        const int Gd = a.G[d];
+        const bool live = fl != kSlotPad && k0 - Gd < T && k0 + tile - Gd > 0;
+        G[p] = live ? Gd : (1 << 29);
+        cnt[p] = live ? (int)a.up_cnt[d] : 0;
+        up[p] = a.up4[d];
+        vo[p] = eo + (unsigned)d * (unsigned)E * 8u;
+        if (lane < 4)
+            reinterpret_cast<double*>(lds + COEF)[4 * c + lane] = a.coef[4 * d + lane];
+        if (lane == 0) *reinterpret_cast<int*>(lds + GT + 4u * (unsigned)c) = G[p];
+        op[p] = bld(so, vo[p]);
+        ip[p] = bld(si, vo[p]);
+    }
+    __syncthreads();                 // the table window, G
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) {
+        rb[p] = tab_at(k0 - G[p]).x;
+        const int r0 = rb[p] < nrow ? rb[p] : nrow - 1;
+        const int r1 = rb[p] + 1 < nrow ? rb[p] + 1 : nrow - 1;
+        const int r2 = rb[p] + 2 < nrow ? rb[p] + 2 : nrow - 1;
+        f0[p] = bld(rec_at(Fb + (uintptr_t)r0 * rowB, rowB), vo[p]);
+        f1[p] = bld(rec_at(Fb + (uintptr_t)r1 * rowB, rowB), vo[p]);
+        f2[p] = bld(rec_at(Fb + (uintptr_t)r2 * rowB, rowB), vo[p]);
+    }
+    // input row of input u of node p (zero row when unused)
+    auto in_row = [&](int p, int u) -> unsigned {
+        const unsigned code = u < cnt[p] ? (unsigned)((up[p] >> (16 * u)) & 0xffffu)
+                                         : (unsigned)RS;
+        return (code & kExtBit) ? (unsigned)(RS + 1) + (code & 0x7fffu) : code;
+    };
+
+    // ---- external inputs staged by this wave: x = wv + NW * j (j < XW)
+    const int x0 = a.ext_off[w], nx = a.ext_off[w + 1] - x0;
+    int xg[XW];
+    unsigned xo[XW];
+#pragma unroll
+    for (int j = 0; j < XW; ++j) {
+        const int x = wv + NW * j;
+        const bool ok = x < nx;
+        xg[j] = ok ? a.ext_g[x0 + x] : (1 << 29);       // never a valid step when unused
+        xo[j] = eo + (ok ? (unsigned)a.ext_slot[x0 + x] : 0u) * (unsigned)E * 8u;
+    }
+    // value of external input j for consumer tick k (0 outside the producer's steps)
+    auto ext_load = [&](int j, int k) -> double {
+        const int t = k - xg[j];
+        const bool ok = (unsigned)t < (unsigned)T;
+        return bld(rec_at(Ob + (uintptr_t)(ok ? t : 0) * rowB, ok ? rowB : 0u), xo[j]);
+    };
+    // staged row of external input j
+    auto ext_row = [&](int j) -> unsigned { return (unsigned)(RS + 1 + wv + NW * j) * kRow; };
+
+    // ---- buffer of tick k0 - 1: the outputs of that tick are the state's o; the external
+    // inputs of tick k0; the zero rows
+    const unsigned b_prev = XB + (unsigned)((k0 - 1) & 1) * BUF;
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) lds_st(lds, b_prev + (unsigned)(wv * NPW + p) * kRow + l8, op[p]);
+    if (wv == 0) {
+        lds_st(lds, XB + (unsigned)RS * kRow + l8, 0.0);
+        lds_st(lds, XB + BUF + (unsigned)RS * kRow + l8, 0.0);
+    }
+    double ring[kRing][XW];
+#pragma unroll
+    for (int j = 0; j < XW; ++j) {
+        lds_st(lds, b_prev + ext_row(j) + l8, ext_load(j, k0));
+#pragma unroll
+        for (int r = 1; r < kRing; ++r) ring[r][j] = ext_load(j, k0 + r);   // k0 % kRing == 0
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // nothing pending may enter the tick loop
+    __syncthreads();
+    const int64_t t_loop = tr ? wall_clock64() : 0;
+    const int64_t c_loop = tr ? clock64() : 0;
+
+    for (int kc = k0; kc < k0 + tile; kc += kChunk) {
+        // next chunk's forcing row (only for nodes whose window advances; others read nothing)
+        int rbn[NPW];
+        double g[NPW];
+#pragma unroll
+        for (int p = 0; p < NPW; ++p) {
+            rbn[p] = tab_at(kc + kChunk - G[p]).x;
+            const int r3 = rb[p] + 3 < nrow ? rb[p] + 3 : nrow - 1;
+            g[p] = bld(rec_at(Fb + (uintptr_t)r3 * rowB, rbn[p] != rb[p] ? rowB : 0u), vo[p]);
+        }
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) {
+            const int k = kc + i;
+            const unsigned brd = XB + (unsigned)((i + 1) & 1) * BUF;   // tick k - 1 (kc even)
+            const unsigned bwr = XB + (unsigned)(i & 1) * BUF;
+            // external inputs of tick k + kRing into the slot of tick k (staged at tick k - 1)
+#pragma unroll
+            for (int j = 0; j < XW; ++j) ring[i % kRing][j] = ext_load(j, k + kRing);
+            double v[NPW][4];
+#pragma unroll
+            for (int p = 0; p < NPW; ++p) {
+                v[p][0] = lds_ld(lds, brd + in_row(p, 0) * kRow + l8);
+                v[p][1] = lds_ld(lds, brd + in_row(p, 1) * kRow + l8);
+                if (cnt[p] > 2) {
+                    v[p][2] = lds_ld(lds, brd + in_row(p, 2) * kRow + l8);
+                    v[p][3] = lds_ld(lds, brd + in_row(p, 3) * kRow + l8);
+                } else {
+                    v[p][2] = v[p][3] = 0.0;
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < NPW; ++p) {
+                const int t = k - G[p];
+                if ((unsigned)t < (unsigned)T) {
+                    const int4 en = tab_at(t);
+                    const int lo = en.x - rb[p], hi = en.y - rb[p];
+                    const double flo = lo == 0 ? f0[p] : (lo == 1 ? f1[p] : f2[p]);
+                    const double fhi = hi == 0 ? f0[p] : (hi == 1 ? f1[p] : f2[p]);
+                    const double fr = __hiloint2double(en.w, en.z);
+                    const double q = (1.0 - fr) * flo + fr * fhi;
+                    double I = v[p][0];
+                    I = I + v[p][1];
+                    if (cnt[p] > 2) {
+                        I = I + v[p][2];
+                        I = I + v[p][3];
+                    }
+                    const double* cf =
+                        reinterpret_cast<const double*>(lds + COEF) + 4 * (wv * NPW + p);
+                    const double o = 0.0 + (((cf[0] * I + cf[1] * ip[p]) + cf[2] * op[p]) +
+                                            cf[3] * q);
+                    op[p] = o;
+                    ip[p] = I;
+                    lds_st(lds, bwr + (unsigned)(wv * NPW + p) * kRow + l8, o);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < XW; ++j)
+                lds_st(lds, bwr + ext_row(j) + l8, ring[(i + 1) % kRing][j]);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int p = 0; p < NPW; ++p) {
+            if (rbn[p] != rb[p]) {          // host-checked: one row further
+                f0[p] = f1[p];
+                f1[p] = f2[p];
+                f2[p] = g[p];
+                rb[p] = rbn[p];
+            }
+        }
+    }
+    if (tr) {
+        const int64_t c_end = clock64();
+        int64_t* r = a.trace + kTraceWords * (int64_t)blockIdx.x;
+        r[0] = t_start;
+        r[1] = t_loop;
+        r[2] = wall_clock64();
+        r[3] = (int64_t)__smid();
+        r[4] = c_loop;
+        r[5] = c_end;
+    }
+    // state for the next launch (slots that ran in this one)
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) {
+        const bool live = G[p] != (1 << 29);
+        bst<0>(rec(a.So, live ? rowB : 0u), vo[p], op[p]);
+        bst<0>(rec(a.Si, live ? rowB : 0u), vo[p], ip[p]);
+    }
+}
+
+// ---- layout conversions ----------------------------------------------------------------------
+// one workgroup: 64 main slots x 64 members of one row r, through an LDS tile
+__global__ __launch_bounds__(256) void to_sweep(const double* __restrict__ src, int64_t sstride,
+                                                int64_t nsm, const int32_t* __restrict__ map,
+                                                double* __restrict__ dst, int64_t nss,
+                                                int64_t E) {
+    __shared__ double tile[64][65];
+    const int64_t d0 = (int64_t)blockIdx.x * 64, e0 = (int64_t)blockIdx.y * 64;
+    const int64_t r = blockIdx.z;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {          // member e0 + i: 64 consecutive slots
+        const int64_t e = e0 + i, d = d0 + tx;
+        tile[i][tx] = (e < E && d < nsm) ? src[e * sstride + r * nsm + d] : 0.0;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {          // slot d0 + i: 64 consecutive members
+        const int64_t d = d0 + i, e = e0 + tx;
+        if (d >= nsm || e >= E) continue;
+        const int32_t m = map[d];
+        if (m >= 0) dst[(r * nss + m) * E + e] = tile[tx][i];
+    }
+}
+
+__global__ __launch_bounds__(256) void from_sweep(const double* __restrict__ src, int64_t nss,
+                                                  const int32_t* __restrict__ map,
+                                                  double* __restrict__ dst, int64_t nsm,
+                                                  int64_t E) {
+    __shared__ double tile[64][65];
+    const int64_t d0 = (int64_t)blockIdx.x * 64, e0 = (int64_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {          // slot d0 + i: its members' row
+        const int64_t d = d0 + i, e = e0 + tx;
+        const int32_t m = d < nsm ? map[d] : -1;
+        tile[i][tx] = (m >= 0 && e < E) ? src[(int64_t)m * E + e] : 0.0;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {          // member e0 + i: 64 consecutive slots
+        const int64_t e = e0 + i, d = d0 + tx;
+        if (d >= nsm || e >= E || map[d] < 0) continue;
+        dst[e * nsm + d] = tile[tx][i];
+    }
+}
+
+__global__ void sweep_coeffs(const double* __restrict__ alpha, const double* __restrict__ beta,
+                             const double* __restrict__ chi, const double* __restrict__ gamma,
+                             const int32_t* __restrict__ rmap, const uint8_t* __restrict__ flags,
+                             double* __restrict__ coef, int64_t nss) {
+    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < nss;
+         d += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t m = rmap[d];
+        double c[4] = {0.0, 0.0, 0.0, 0.0};
+        if (m >= 0) {
+            c[0] = alpha[m];
+            c[1] = beta[m];
+            c[2] = chi[m];
+            c[3] = gamma[m];
+        } else if (flags[d] == kSlotSum) {
+            c[0] = 1.0;
+        }
+        for (int k = 0; k < 4; ++k) coef[4 * d + k] = c[k];
+    }
+}
+
+__global__ void sweep_zero_free(const int32_t* __restrict__ rmap, double* __restrict__ So,
+                                double* __restrict__ Si, int64_t nss, int64_t E) {
+    const int64_t total = nss * E;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        if (rmap[x / E] < 0) {
+            So[x] = 0.0;
+            Si[x] = 0.0;
+        }
+    }
+}
+
+inline int grid_for(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+}  // namespace
+
+hipError_t launch_member_sweep(const SweepArgs& a, int grid, int member_groups, hipStream_t s) {
+    if (grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL((member_sweep<kSweepNPW, kSweepNW, kSweepXW>), dim3(grid, member_groups),
+                       dim3(64 * (kSweepNW + 1)), sweep_lds_bytes(), s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_to_sweep(const double* src, int64_t src_stride, int64_t nsm, int64_t R,
+                           const int32_t* map, double* dst, int64_t nss, int64_t E,
+                           hipStream_t s) {
+    if (nsm <= 0 || E <= 0 || R <= 0) return hipSuccess;
+    hipLaunchKernelGGL(to_sweep, dim3((unsigned)((nsm + 63) / 64), (unsigned)((E + 63) / 64),
+                                      (unsigned)R),
+                       dim3(256), 0, s, src, src_stride, nsm, map, dst, nss, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_from_sweep(const double* src, int64_t nss, const int32_t* map, double* dst,
+                             int64_t nsm, int64_t E, hipStream_t s) {
+    if (nsm <= 0 || E <= 0) return hipSuccess;
+    hipLaunchKernelGGL(from_sweep, dim3((unsigned)((nsm + 63) / 64), (unsigned)((E + 63) / 64)),
+                       dim3(256), 0, s, src, nss, map, dst, nsm, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_coeffs(const double* alpha, const double* beta, const double* chi,
+                               const double* gamma, const int32_t* rmap, const uint8_t* flags,
+                               double* coef, int64_t nss, hipStream_t s) {
+    hipLaunchKernelGGL(sweep_coeffs, grid_for(nss, 256), 256, 0, s, alpha, beta, chi, gamma,
+                       rmap, flags, coef, nss);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_zero_free(const int32_t* rmap, double* So, double* Si, int64_t nss,
+                                  int64_t E, hipStream_t s) {
+    hipLaunchKernelGGL(sweep_zero_free, grid_for(nss * E, 256), 256, 0, s, rmap, So, Si, nss, E);
+    return hipGetLastError();
+}
+
+}  // namespace mcr
