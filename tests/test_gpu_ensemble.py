@@ -319,9 +319,9 @@ def test_ensemble_dataflow_needs_an_acyclic_workgroup_graph():
     net.close()
 
 
-@pytest.mark.parametrize("n,E,T,rows,mode", [(3000, 64, 60, 7, "sweep"), (2500, 40, 45, 5, "auto"),
+@pytest.mark.parametrize("n,E,T,rows,mode", [(3000, 64, 60, 7, "sweep"), (2500, 40, 45, 5, "sweep"),
                                              (1500, 130, 33, 4, "sweep"),
-                                             (4000, 32, 100, 10, "auto")])
+                                             (4000, 32, 100, 10, "sweep")])
 def test_member_sweep_bitexact(n, E, T, rows, mode):
     """Member sweep (sweep.hip: the members on the lanes of a member plan of its own): every
     member bit-identical to its serial oracle run -- step outputs and inflows, series, final
@@ -366,7 +366,7 @@ def test_member_sweep_bitexact(n, E, T, rows, mode):
 
 def test_member_sweep_needs_sparse_forcing_rows():
     """A step as long as the forcing interval (8 steps touch 9 rows) cannot keep its rows in the
-    sweep's 3-row window: auto routes it with launches, sweep mode refuses it."""
+    sweep's 3-row window: other modes route it with launches, sweep mode refuses it."""
     E, T = 32, 20
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 9, E, rows=30)
     x = xp[0] + 3600e9 * np.arange(1, T + 1)
@@ -388,7 +388,7 @@ def test_member_sweep_needs_sparse_forcing_rows():
 
 
 def test_member_sweep_needs_an_even_ensemble():
-    """An odd ensemble (the store wave copies two members per lane) routes with launches."""
+    """An odd ensemble (the store wave copies two members per lane) is refused in sweep mode."""
     E, T = 33, 20
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 11, E)
     x = xp[0] + 300e9 * np.arange(1, T + 1)
@@ -396,11 +396,7 @@ def test_member_sweep_needs_an_even_ensemble():
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
     net.load_forcing(xp, fpe)
-    net.run(x)
-    assert net.mode()[1] == "launches"
-    got_o, _ = net.fetch_outputs(0, T)
-    e = E - 1
-    want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
-                                   np.ascontiguousarray(fpe[:, :, e]))
-    assert np.array_equal(got_o[:, :, e], want_o)
+    net.set_mode("sweep")
+    with pytest.raises(engine.nat.RoutingError):
+        net.run(x)
     net.close()

@@ -213,8 +213,9 @@ struct Net {
     int sweep_state = 0;             // 1 built, -1 the network has no member plan the kernel takes
     uint64_t coef_ver = 1, f_ver = 1;   // bumped by set_coeffs / load_forcing / corrections
     bool out_sweep = false;          // the outputs of the last run are in sw->O
-    // auto mode takes the sweep from this many members (below it the lanes are mostly idle)
-    static constexpr int64_t kSweepMinMembers = 32;
+    // auto mode takes the sweep from this many members (below it the lanes are mostly idle);
+    // 0: auto never takes it (opt-in, mode 4) while it is slower than the multi-launch kernel
+    static constexpr int64_t kSweepMinMembers = 0;
     // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
     DBuf<int64_t> mwbase;
     int64_t mw_E = 0, mw_cells = 0;
@@ -914,10 +915,10 @@ struct Net {
         sweep_state = -1;
         auto S = std::make_unique<Sweep>();
         mcr::PlanParams pp;
-        pp.slots = mcr::kSweepSlots;
+        pp.slots = mcr::kSweepNW;          // a plan "lane" is a compute wave of members
         pp.tile = mcr::kSweepTile;
         pp.ext_cap = 4;
-        pp.chain = 1;
+        pp.chain = mcr::kSweepNPW;
         const std::string err =
             mcr::build_plan(plan.n, topo_end.data(), topo_deg.data(), topo_heads.data(),
                             (int64_t)topo_heads.size(), pp, S->plan);
@@ -960,7 +961,7 @@ struct Net {
     // touch at most 3 rows and consecutive chunks start at most one row apart (sweep.hip).
     bool sweep_fits(int64_t T, const double* Fsrc, const std::vector<int4>& tab) {
         if (mode == 1 || mode == 2 || mode == 3 || force_mode == 1) return false;
-        const bool want = mode == 4 || E >= kSweepMinMembers;
+        const bool want = mode == 4 || (kSweepMinMembers > 0 && E >= kSweepMinMembers);
         // (E even: the store wave copies two members per lane)
         if (!want || E < 2 || E % 2 || T < 2 || Fsrc != F.p) return false;
         auto at = [&](int64_t t) { return tab[t < 0 ? 0 : (t >= T ? T - 1 : t)]; };

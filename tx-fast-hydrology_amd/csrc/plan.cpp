@@ -52,8 +52,10 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     const int64_t C = params.slots;
     const int32_t B = params.tile;
     if (n < 0) return "n must be >= 0";
-    // 32: the member sweep's plans (sweep.hpp, chain 1; no lane-per-slot kernel runs them)
-    if (!(C == 32 && params.chain == 1) && (C < 64 || C > 512 || (C % 64) != 0))
+    // fewer than 64 lanes: the member sweep's plans (sweep.hpp: a "lane" is a wave of members,
+    // chain * slots node slots per workgroup); no lane-per-slot kernel runs them
+    const bool member_plan = (C == 4 || C == 8 || C == 16 || C == 32) && C * params.chain <= 64;
+    if (!member_plan && (C < 64 || C > 512 || (C % 64) != 0))
         return "slots must be a multiple of 64 in [64, 512]";
     if (B < 1 || B > 4096) return "tile must be in [1, 4096]";
     if (P.p.ext_cap < 1 || P.p.ext_cap > 0x7fff) return "ext_cap out of range";

@@ -1,8 +1,10 @@
 // Member sweep (sweep.hpp): the ensemble forecast with the members on the lanes.
 //
-// One workgroup = kSweepNW waves = the kSweepSlots node slots of one member-plan workgroup; wave
-// v routes slots v * NPW .. v * NPW + NPW - 1 for 64 members (lane = member, blockIdx.y = member
-// group).  Per node everything that decides control flow or addresses is wave-uniform (the
+// One workgroup = kSweepNW compute waves (+ a store wave) = the kSweepSlots node slots of one
+// member-plan workgroup.  The member plan has kSweepNW "lanes" of kSweepNPW positions (plan.hpp
+// lane chains): wave v routes the chain of plan lane v, positions p = 0 .. NPW - 1 in order
+// within a tick (a chained input is the previous position's output of the same tick, from a
+// register), for 64 members (lane = member, blockIdx.y = member group).  Per node everything that decides control flow or addresses is wave-uniform (the
 // node's step at this tick, its inputs, coefficients and forcing rows), so the tick is scalar
 // control plus f64 arithmetic on 64 members, and every global access is one 512-byte row.
 //
@@ -161,7 +163,7 @@ void member_sweep(SweepArgs a) {
     const auto so = rec(a.So, rowB), si = rec(a.Si, rowB);
 #pragma unroll
     for (int p = 0; p < NPW; ++p) {
-        const int c = wv * NPW + p;
+        const int c = p * NW + wv;       // plan lane = this wave, position p
         const int64_t d = (int64_t)w * RS + c;
         const uint8_t fl = a.flags[d];
         const int Gd = a.G[d];
@@ -188,11 +190,22 @@ void member_sweep(SweepArgs a) {
         f2[p] = bld(rec_at(Fb + (uintptr_t)r2 * rowB, rowB), vo[p]);
     }
     // input row of input u of node p (zero row when unused)
+    // (a chained input -- the previous position's output of the same tick, always the last input
+    // of the fold -- reads the zero row here and is added from a register)
     auto in_row = [&](int p, int u) -> unsigned {
-        const unsigned code = u < cnt[p] ? (unsigned)((up[p] >> (16 * u)) & 0xffffu)
-                                         : (unsigned)RS;
+        unsigned code = u < cnt[p] ? (unsigned)((up[p] >> (16 * u)) & 0xffffu) : (unsigned)RS;
+        if (code == kSelfCode) code = RS;
         return (code & kExtBit) ? (unsigned)(RS + 1) + (code & 0x7fffu) : code;
     };
+    bool chained[NPW];
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) {
+        chained[p] = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            chained[p] = chained[p] ||
+                         (u < cnt[p] && ((up[p] >> (16 * u)) & 0xffffu) == kSelfCode);
+    }
 
     // ---- external inputs staged by this wave: x = wv + NW * j (j < XW)
     const int x0 = a.ext_off[w], nx = a.ext_off[w + 1] - x0;
@@ -218,7 +231,7 @@ void member_sweep(SweepArgs a) {
     // inputs of tick k0; the zero rows
     const unsigned b_prev = XB + (unsigned)((k0 - 1) & 1) * BUF;
 #pragma unroll
-    for (int p = 0; p < NPW; ++p) lds_st(lds, b_prev + (unsigned)(wv * NPW + p) * kRow + l8, op[p]);
+    for (int p = 0; p < NPW; ++p) lds_st(lds, b_prev + (unsigned)(p * NW + wv) * kRow + l8, op[p]);
     if (wv == 0) {
         lds_st(lds, XB + (unsigned)RS * kRow + l8, 0.0);
         lds_st(lds, XB + BUF + (unsigned)RS * kRow + l8, 0.0);
@@ -253,42 +266,41 @@ void member_sweep(SweepArgs a) {
             // external inputs of tick k + kRing into the slot of tick k (staged at tick k - 1)
 #pragma unroll
             for (int j = 0; j < XW; ++j) ring[i % kRing][j] = ext_load(j, k + kRing);
+            // every node's inputs and table entry first, then the updates without branches, so
+            // the NPW dependency chains of the tick interleave (a node that does not run this
+            // tick computes a value nobody reads: its consumers do not run at tick k + 1 either)
             double v[NPW][4];
+            int4 en[NPW];
 #pragma unroll
             for (int p = 0; p < NPW; ++p) {
-                v[p][0] = lds_ld(lds, brd + in_row(p, 0) * kRow + l8);
-                v[p][1] = lds_ld(lds, brd + in_row(p, 1) * kRow + l8);
-                if (cnt[p] > 2) {
-                    v[p][2] = lds_ld(lds, brd + in_row(p, 2) * kRow + l8);
-                    v[p][3] = lds_ld(lds, brd + in_row(p, 3) * kRow + l8);
-                } else {
-                    v[p][2] = v[p][3] = 0.0;
-                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[p][u] = lds_ld(lds, brd + in_row(p, u) * kRow + l8);
+                en[p] = tab_at(k - G[p]);
             }
+            double prev = 0.0;              // output of the previous position (chained input)
 #pragma unroll
             for (int p = 0; p < NPW; ++p) {
-                const int t = k - G[p];
-                if ((unsigned)t < (unsigned)T) {
-                    const int4 en = tab_at(t);
-                    const int lo = en.x - rb[p], hi = en.y - rb[p];
-                    const double flo = lo == 0 ? f0[p] : (lo == 1 ? f1[p] : f2[p]);
-                    const double fhi = hi == 0 ? f0[p] : (hi == 1 ? f1[p] : f2[p]);
-                    const double fr = __hiloint2double(en.w, en.z);
-                    const double q = (1.0 - fr) * flo + fr * fhi;
-                    double I = v[p][0];
-                    I = I + v[p][1];
-                    if (cnt[p] > 2) {
-                        I = I + v[p][2];
-                        I = I + v[p][3];
-                    }
-                    const double* cf =
-                        reinterpret_cast<const double*>(lds + COEF) + 4 * (wv * NPW + p);
-                    const double o = 0.0 + (((cf[0] * I + cf[1] * ip[p]) + cf[2] * op[p]) +
-                                            cf[3] * q);
-                    op[p] = o;
-                    ip[p] = I;
-                    lds_st(lds, bwr + (unsigned)(wv * NPW + p) * kRow + l8, o);
-                }
+                const bool act = (unsigned)(k - G[p]) < (unsigned)T;
+                const int lo = en[p].x - rb[p], hi = en[p].y - rb[p];
+                const double flo = lo == 0 ? f0[p] : (lo == 1 ? f1[p] : f2[p]);
+                const double fhi = hi == 0 ? f0[p] : (hi == 1 ? f1[p] : f2[p]);
+                const double fr = __hiloint2double(en[p].w, en[p].z);
+                const double q = (1.0 - fr) * flo + fr * fhi;
+                // unused inputs read the zero row: adding +0.0 to a sum of published values
+                // (never -0.0) is exact, so the fold over 4 terms is the reference's fold
+                double I = v[p][0];
+                I = I + v[p][1];
+                I = I + v[p][2];
+                I = I + v[p][3];
+                if (p > 0 && chained[p]) I = I + prev;
+                const double* cf =
+                    reinterpret_cast<const double*>(lds + COEF) + 4 * (p * NW + wv);
+                const double o = 0.0 + (((cf[0] * I + cf[1] * ip[p]) + cf[2] * op[p]) +
+                                        cf[3] * q);
+                op[p] = act ? o : op[p];
+                ip[p] = act ? I : ip[p];
+                prev = o;
+                lds_st(lds, bwr + (unsigned)(p * NW + wv) * kRow + l8, o);
             }
 #pragma unroll
             for (int j = 0; j < XW; ++j)

@@ -63,7 +63,7 @@ struct SweepArgs {
 // member plan of the sweep: tile (launch ticks, cross-workgroup slack); step-table entries a
 // launch keeps in LDS (tile + kChunk + 1 + the workgroup's G span must fit)
 #ifndef MCR_SWEEP_TILE
-#define MCR_SWEEP_TILE 64
+#define MCR_SWEEP_TILE 32
 #endif
 constexpr int kSweepTile = MCR_SWEEP_TILE;
 constexpr int kSweepTabCap = 640;
