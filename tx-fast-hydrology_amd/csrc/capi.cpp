@@ -957,17 +957,19 @@ struct Net {
         return true;
     }
 
-    // Can this horizon run as a member sweep?  Forcing windows: the steps of any 8-step chunk
-    // touch at most 3 rows and consecutive chunks start at most one row apart (sweep.hip).
+    // Can this horizon run as a member sweep?
     bool sweep_fits(int64_t T, const double* Fsrc, const std::vector<int4>& tab) {
         if (mode == 1 || mode == 2 || mode == 3 || force_mode == 1) return false;
         const bool want = mode == 4 || (kSweepMinMembers > 0 && E >= kSweepMinMembers);
         // (E even: the store wave copies two members per lane)
         if (!want || E < 2 || E % 2 || T < 2 || Fsrc != F.p) return false;
-        auto at = [&](int64_t t) { return tab[t < 0 ? 0 : (t >= T ? T - 1 : t)]; };
-        for (int64_t t = -mcr::kChunk; t < T; ++t) {
-            const int4 a0 = at(t), a7 = at(t + mcr::kChunk - 1), a8 = at(t + mcr::kChunk);
-            if (std::max(a7.x, a7.y) - a0.x + 1 > 3 || a8.x - a0.x > 1) return false;
+        // row pairs {r, r} or {r, r + 1}; from one step to the next each row advances by at most
+        // one (sweep.hip keeps the pair's rows and the next one in registers)
+        for (int64_t t = 0; t < T; ++t) {
+            if (tab[t].y != tab[t].x && tab[t].y != tab[t].x + 1) return false;
+            if (t > 0 && (tab[t].x - tab[t - 1].x > 1 || tab[t].y - tab[t - 1].y > 1 ||
+                          tab[t].x < tab[t - 1].x))
+                return false;
         }
         if (!ensure_sweep()) return false;
         return sw->plan.nslots * E * 8 < ((int64_t)1 << 31) && T < (1 << 28);
@@ -1000,7 +1002,7 @@ struct Net {
         }
         S.So.reserve((size_t)(ns * E));
         S.Si.reserve((size_t)(ns * E));
-        S.O.reserve((size_t)(T * ns * E));
+        S.O.reserve((size_t)(T * ns * E) + 128);   // (the loader's 16-B reads run past E)
         HIPC(mcr::launch_sweep_zero_free(S.rmap.p, S.So.p, S.Si.p, ns, E, stream));
         HIPC(mcr::launch_to_sweep(st_o.p, nsm, nsm, 1, S.mmap.p, S.So.p, ns, E, stream));
         HIPC(mcr::launch_to_sweep(st_i.p, nsm, nsm, 1, S.mmap.p, S.Si.p, ns, E, stream));

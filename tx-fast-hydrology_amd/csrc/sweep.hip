@@ -9,23 +9,25 @@
 // control plus f64 arithmetic on 64 members, and every global access is one 512-byte row.
 //
 // Tick k (node d runs step t = k - G[d] when 0 <= t < T):
-//   reads   the inputs' outputs of tick k - 1 from the LDS buffer of parity (k - 1) & 1: a row
-//           per node slot (in-cluster inputs, unit slack), a zero row, and a row per external
-//           input of the workgroup (staged there by its owner wave during tick k - 1);
+//   reads   the inputs' outputs of tick k - 1: in-cluster inputs (unit slack) from the LDS buffer
+//           of parity (k - 1) & 1, inputs of other workgroups (produced in earlier launches:
+//           tile slack) from ring slot k % 4, which the loader wave filled by LDS-DMA three
+//           ticks ahead; the table entry of each node's step (row pair, frac);
 //   routes  I = ((0 + x1) + x2) + ...,  o = 0 + (((alpha I + beta I_prev) + chi o_prev) + gamma q),
-//           q = (1 - frac) f[lo] + frac f[hi]   (nutils.py:23-33, 80-83; FMA contraction off);
-//   writes  o to the LDS buffer of parity k & 1 and to O[t][d][.] (non-temporal);
-//   stages  external inputs for tick k + 1, loaded kRing - 1 ticks earlier into a register ring
-//           (every input of another workgroup was produced in an earlier launch: tile slack);
-//   then one workgroup barrier.
-// Forcing rows: a node keeps the 3 rows its steps of the current 8-tick chunk can touch (rows of
-// clamped steps outside [0, T) are those of step 0 / T - 1, so the window is right when the
-// node starts) and prefetches the next one a chunk ahead.  Host-checked: no chunk spans more
-// than 3 rows and consecutive chunks start at most one row apart.
-// Every buffer access has a fixed instruction count (inactive rows use empty buffer records or
-// out-of-range offsets), so the wait counts the compiler places are exact: the tick never waits
-// for its own output stores.
+//           q = (1 - frac) f[lo] + frac f[hi]   (nutils.py:23-33, 80-83; FMA contraction off),
+//           the NPW nodes of a wave in position order (a chained input from a register);
+//   writes  o to the LDS buffer of parity k & 1;
+//   then one workgroup barrier; the store wave copies the rows of tick k to O[t][d][.] during
+//   tick k + 1.
+// Roles keep the wait counts apart: compute waves issue no stores (their only loads are
+// forcing rows), the store wave never waits for its stores, the loader waits only for its own
+// loads.  Forcing: a node keeps f[lo], f[hi] of its current step's row pair and f[hi + 1];
+// when its step moves to the next pair (host-checked: rows advance by at most one per step)
+// they shift and the next row is loaded.  A chunk of 8 ticks in which every node of a wave runs
+// all its ticks is routed without activity selects.
 #include "sweep.hpp"
+
+#include <type_traits>
 
 #include "kernels.hpp"
 #include "plan.hpp"
@@ -45,7 +47,7 @@ namespace {
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 
 constexpr unsigned kRow = 512;   // LDS / global row: 64 members x f64
-constexpr int kRing = 4;         // external-input register ring (ticks of prefetch + 1)
+constexpr int kRing = 4;         // external-input ring slots (ticks; a power of two)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rec(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
@@ -74,18 +76,21 @@ __device__ __forceinline__ void lds_st(char* lds, unsigned byte, double x) {
 }
 __device__ __forceinline__ int clamp_t(int t, int T) { return t < 0 ? 0 : (t < T ? t : T - 1); }
 
-// NPW node slots per compute wave, NW compute waves, XW external inputs staged per compute wave,
-// plus one store wave.  LDS: the step-table window of the launch, the workgroup's coefficients
-// and G, two parity buffers of rows.
-template <int NPW, int NW, int XW>
-__global__ __launch_bounds__(64 * (NW + 1), MCR_SWEEP_MIN_WAVES)
+// NPW node slots per compute wave, NW compute waves, a store wave and a loader wave; XMAX
+// external inputs per workgroup.  LDS: the step-table window of the launch, the workgroup's
+// coefficients and G, two parity buffers of node rows (+ a zero row), and a ring of kRing tick
+// slots of external-input rows.
+template <int NPW, int NW, int XMAX>
+__global__ __launch_bounds__(64 * (NW + 2), MCR_SWEEP_MIN_WAVES)
 void member_sweep(SweepArgs a) {
     constexpr int RS = NPW * NW;
     constexpr unsigned TAB = 0;                                   // int4 [kSweepTabCap]
     constexpr unsigned COEF = TAB + 16u * kSweepTabCap;           // double [RS][4]
     constexpr unsigned GT = COEF + 32u * RS;                      // int [RS]
-    constexpr unsigned XB = GT + 4u * RS;                         // [2][RS + 1 + NW XW] rows
-    constexpr unsigned BUF = (RS + 1 + NW * XW) * kRow;
+    constexpr unsigned XB = GT + 4u * RS;                         // [2][RS + 1] rows
+    constexpr unsigned BUF = (RS + 1) * kRow;
+    constexpr unsigned XE = XB + 2 * BUF;                         // [kRing][XMAX] rows
+    constexpr unsigned XSLOT = XMAX * kRow;
     extern __shared__ __attribute__((aligned(16))) char lds[];
 
     const int lane = threadIdx.x & 63;
@@ -105,9 +110,79 @@ void member_sweep(SweepArgs a) {
     // launch, [tw0, tw1]; lookups outside it are clamped into it (non-live slots only)
     const int gmin = a.wg_gmin[w], gmax = a.wg_gmax[w];
     const int tw0 = clamp_t(k0 - gmax, T), tw1 = clamp_t(k0 + tile + kChunk - gmin, T);
-    for (int i = threadIdx.x; i <= tw1 - tw0; i += 64 * (NW + 1))
-        reinterpret_cast<int4*>(lds + TAB)[i] = a.stab[tw0 + i];
+    // entries {pair = 2 row_lo + (row_hi - row_lo), -, frac}: row_hi - row_lo is 0 or 1
+    // (host-checked), so a step's row pair is one uniform word
+    for (int i = threadIdx.x; i <= tw1 - tw0; i += 64 * (NW + 2)) {
+        const int4 en = a.stab[tw0 + i];
+        reinterpret_cast<int4*>(lds + TAB)[i] = make_int4(2 * en.x + (en.y - en.x), 0, en.z, en.w);
+    }
 
+    if (wv == NW + 1) {
+        // ================= loader wave: the rows of the workgroup's external inputs (outputs of
+        // other workgroups, produced in earlier launches) for consumer tick k go to ring slot
+        // k % kRing by LDS-DMA, kRing - 1 ticks ahead, two rows per instruction (lanes 0-31 row
+        // 2m, 32-63 row 2m + 1; 16 B = two members per lane).  Its wait counts cover only its
+        // own loads, so it uses raw barriers (no drain at a __syncthreads).
+        const int x0 = a.ext_off[w], nx = a.ext_off[w + 1] - x0;
+        const int nin = (nx + 1) >> 1;                   // instructions per tick
+        const int half = lane >> 5;
+        const int em = (int)blockIdx.y * 64 + 2 * (lane & 31);
+        const int64_t nsE = (int64_t)(rowB / 8u);
+        int xg[XMAX / 2];
+        int64_t xs[XMAX / 2];
+#pragma unroll
+        for (int m = 0; m < XMAX / 2; ++m) {
+            const int x = 2 * m + half;
+            const bool ok = x < nx;
+            xg[m] = ok ? a.ext_g[x0 + x] : 0;
+            xs[m] = ok ? (int64_t)a.ext_slot[x0 + x] * E : 0;
+        }
+        auto issue = [&](int k) {                        // the rows of consumer tick k
+            const unsigned slot = XE + (unsigned)(k & (kRing - 1)) * XSLOT;
+#pragma unroll
+            for (int m = 0; m < XMAX / 2; ++m) {
+                if (m < nin) {
+                    const int t = clamp_t(k - xg[m], T);    // (other steps are never read)
+                    const double* src = a.O + ((int64_t)t * nsE + xs[m] + em);
+                    __builtin_amdgcn_global_load_lds(
+                        src, (__attribute__((address_space(3))) void*)(lds + slot + 1024u * m),
+                        16, 0, 0);
+                }
+            }
+        };
+        // wait until at most 2 ticks of loads are in flight (those of ticks k + 1, k + 2 issued
+        // after the rows of tick k)
+        auto wait_two = [&]() {
+            switch (nin) {
+#define MCR_SWEEP_W(n)                                                 \
+    case n:                                                            \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * n) : "memory");   \
+        break;
+                MCR_SWEEP_W(0) MCR_SWEEP_W(1) MCR_SWEEP_W(2) MCR_SWEEP_W(3) MCR_SWEEP_W(4)
+                MCR_SWEEP_W(5) MCR_SWEEP_W(6) MCR_SWEEP_W(7) MCR_SWEEP_W(8) MCR_SWEEP_W(9)
+                MCR_SWEEP_W(10) MCR_SWEEP_W(11) MCR_SWEEP_W(12)
+#undef MCR_SWEEP_W
+                default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        };
+        auto barrier = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        };
+        barrier();                                       // table window, G
+        issue(k0);
+        issue(k0 + 1);
+        issue(k0 + 2);
+        wait_two();                                      // tick k0's rows have landed
+        barrier();                                       // prologue of the compute waves
+        for (int k = k0; k < k0 + tile; ++k) {
+            issue(k + kRing - 1);
+            wait_two();                                  // the rows of tick k + 1
+            barrier();
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
     if (wv == NW) {
         // ================= store wave: during tick k it copies the rows of tick k - 1 (stable
         // until the barrier that ends tick k) to O, two node rows per instruction (16 B = two
@@ -148,19 +223,27 @@ void member_sweep(SweepArgs a) {
     }
 
     // ================= compute waves
-    // uniform table entry of step t (clamped into [0, T) and the window)
-    auto tab_at = [&](int t) -> int4 {
+    // table entry of step t (clamped into [0, T) and the window): the row pair (uniform) and
+    // frac (a broadcast VGPR operand)
+    auto tab_raw = [&](int t) -> int4 {
         int c = clamp_t(t, T);
         c = c < tw0 ? tw0 : (c > tw1 ? tw1 : c);
-        const int4 v = *reinterpret_cast<const int4*>(lds + TAB + 16u * (unsigned)(c - tw0));
-        return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
-                         __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+        return *reinterpret_cast<const int4*>(lds + TAB + 16u * (unsigned)(c - tw0));
     };
-    int G[NPW], rb[NPW], cnt[NPW];
+    int G[NPW], cnt[NPW];
     uint64_t up[NPW];
     unsigned vo[NPW];
-    double op[NPW], ip[NPW], f0[NPW], f1[NPW], f2[NPW];
+    double op[NPW], ip[NPW];
+    // forcing: the rows of the pair of the node's current step, fA = f[lo], fB = f[hi]
+    // (cur = the pair's table word), and the next row fN = f[hi + 1].  Host-checked: from one
+    // step to the next, lo and hi advance by at most one row, so a new pair is made of these.
+    double fA[NPW], fB[NPW], fN[NPW];
+    int cur[NPW];
     const auto so = rec(a.So, rowB), si = rec(a.Si, rowB);
+    auto frow = [&](int r, unsigned off) -> double {
+        r = r < 0 ? 0 : (r < nrow ? r : nrow - 1);
+        return bld(rec_at(Fb + (uintptr_t)r * rowB, rowB), off);
+    };
 #pragma unroll
     for (int p = 0; p < NPW; ++p) {
         const int c = p * NW + wv;       // plan lane = this wave, position p
@@ -181,21 +264,19 @@ void member_sweep(SweepArgs a) {
     __syncthreads();                 // the table window, G
 #pragma unroll
     for (int p = 0; p < NPW; ++p) {
-        rb[p] = tab_at(k0 - G[p]).x;
-        const int r0 = rb[p] < nrow ? rb[p] : nrow - 1;
-        const int r1 = rb[p] + 1 < nrow ? rb[p] + 1 : nrow - 1;
-        const int r2 = rb[p] + 2 < nrow ? rb[p] + 2 : nrow - 1;
-        f0[p] = bld(rec_at(Fb + (uintptr_t)r0 * rowB, rowB), vo[p]);
-        f1[p] = bld(rec_at(Fb + (uintptr_t)r1 * rowB, rowB), vo[p]);
-        f2[p] = bld(rec_at(Fb + (uintptr_t)r2 * rowB, rowB), vo[p]);
+        cur[p] = __builtin_amdgcn_readfirstlane(tab_raw(k0 - G[p]).x);
+        const int lo = cur[p] >> 1, hi = lo + (cur[p] & 1);
+        fA[p] = frow(lo, vo[p]);
+        fB[p] = frow(hi, vo[p]);
+        fN[p] = frow(hi + 1, vo[p]);
     }
-    // input row of input u of node p (zero row when unused)
-    // (a chained input -- the previous position's output of the same tick, always the last input
-    // of the fold -- reads the zero row here and is added from a register)
-    auto in_row = [&](int p, int u) -> unsigned {
+    // LDS address of input u of node p at a tick reading parity buffer `brd` and ring slot
+    // `xsl` (a chained input -- the previous position's output of the same tick, always the last
+    // input of the fold -- and an unused one read the zero row)
+    auto in_addr = [&](int p, int u, unsigned brd, unsigned xsl) -> unsigned {
         unsigned code = u < cnt[p] ? (unsigned)((up[p] >> (16 * u)) & 0xffffu) : (unsigned)RS;
         if (code == kSelfCode) code = RS;
-        return (code & kExtBit) ? (unsigned)(RS + 1) + (code & 0x7fffu) : code;
+        return (code & kExtBit) ? xsl + (code & 0x7fffu) * kRow : brd + code * kRow;
     };
     bool chained[NPW];
 #pragma unroll
@@ -207,28 +288,7 @@ void member_sweep(SweepArgs a) {
                          (u < cnt[p] && ((up[p] >> (16 * u)) & 0xffffu) == kSelfCode);
     }
 
-    // ---- external inputs staged by this wave: x = wv + NW * j (j < XW)
-    const int x0 = a.ext_off[w], nx = a.ext_off[w + 1] - x0;
-    int xg[XW];
-    unsigned xo[XW];
-#pragma unroll
-    for (int j = 0; j < XW; ++j) {
-        const int x = wv + NW * j;
-        const bool ok = x < nx;
-        xg[j] = ok ? a.ext_g[x0 + x] : (1 << 29);       // never a valid step when unused
-        xo[j] = eo + (ok ? (unsigned)a.ext_slot[x0 + x] : 0u) * (unsigned)E * 8u;
-    }
-    // value of external input j for consumer tick k (0 outside the producer's steps)
-    auto ext_load = [&](int j, int k) -> double {
-        const int t = k - xg[j];
-        const bool ok = (unsigned)t < (unsigned)T;
-        return bld(rec_at(Ob + (uintptr_t)(ok ? t : 0) * rowB, ok ? rowB : 0u), xo[j]);
-    };
-    // staged row of external input j
-    auto ext_row = [&](int j) -> unsigned { return (unsigned)(RS + 1 + wv + NW * j) * kRow; };
-
-    // ---- buffer of tick k0 - 1: the outputs of that tick are the state's o; the external
-    // inputs of tick k0; the zero rows
+    // ---- buffer of tick k0 - 1: the outputs of that tick are the state's o; the zero rows
     const unsigned b_prev = XB + (unsigned)((k0 - 1) & 1) * BUF;
 #pragma unroll
     for (int p = 0; p < NPW; ++p) lds_st(lds, b_prev + (unsigned)(p * NW + wv) * kRow + l8, op[p]);
@@ -236,86 +296,87 @@ void member_sweep(SweepArgs a) {
         lds_st(lds, XB + (unsigned)RS * kRow + l8, 0.0);
         lds_st(lds, XB + BUF + (unsigned)RS * kRow + l8, 0.0);
     }
-    double ring[kRing][XW];
-#pragma unroll
-    for (int j = 0; j < XW; ++j) {
-        lds_st(lds, b_prev + ext_row(j) + l8, ext_load(j, k0));
-#pragma unroll
-        for (int r = 1; r < kRing; ++r) ring[r][j] = ext_load(j, k0 + r);   // k0 % kRing == 0
-    }
     __builtin_amdgcn_s_waitcnt(0);   // nothing pending may enter the tick loop
     __syncthreads();
     const int64_t t_loop = tr ? wall_clock64() : 0;
     const int64_t c_loop = tr ? clock64() : 0;
 
     for (int kc = k0; kc < k0 + tile; kc += kChunk) {
-        // next chunk's forcing row (only for nodes whose window advances; others read nothing)
-        int rbn[NPW];
-        double g[NPW];
+        // a chunk in which every node of this wave runs all its ticks needs no activity selects
+        bool steady = true;
 #pragma unroll
-        for (int p = 0; p < NPW; ++p) {
-            rbn[p] = tab_at(kc + kChunk - G[p]).x;
-            const int r3 = rb[p] + 3 < nrow ? rb[p] + 3 : nrow - 1;
-            g[p] = bld(rec_at(Fb + (uintptr_t)r3 * rowB, rbn[p] != rb[p] ? rowB : 0u), vo[p]);
-        }
+        for (int p = 0; p < NPW; ++p)
+            steady = steady && kc - G[p] >= 0 && kc + kChunk - 1 - G[p] < T;
+        auto chunk = [&](auto steady_tag) {
+            constexpr bool S = decltype(steady_tag)::value;
+#pragma unroll 2
+            for (int i = 0; i < kChunk; ++i) {
+                const int k = kc + i;
+                const unsigned brd = XB + (unsigned)((i + 1) & 1) * BUF;   // tick k - 1
+                const unsigned bwr = XB + (unsigned)(i & 1) * BUF;
+                const unsigned xsl = XE + (unsigned)(i % kRing) * XSLOT;   // kc % kRing == 0
+                // every node's inputs and table entry first, then the updates without branches,
+                // so the NPW dependency chains of the tick interleave (a node that does not run
+                // this tick computes a value nobody reads: its consumers do not run at k + 1)
+                double v[NPW][4], fr[NPW];
+                int pr[NPW];
+                bool chg = false;
 #pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-            const int k = kc + i;
-            const unsigned brd = XB + (unsigned)((i + 1) & 1) * BUF;   // tick k - 1 (kc even)
-            const unsigned bwr = XB + (unsigned)(i & 1) * BUF;
-            // external inputs of tick k + kRing into the slot of tick k (staged at tick k - 1)
+                for (int p = 0; p < NPW; ++p) {
 #pragma unroll
-            for (int j = 0; j < XW; ++j) ring[i % kRing][j] = ext_load(j, k + kRing);
-            // every node's inputs and table entry first, then the updates without branches, so
-            // the NPW dependency chains of the tick interleave (a node that does not run this
-            // tick computes a value nobody reads: its consumers do not run at tick k + 1 either)
-            double v[NPW][4];
-            int4 en[NPW];
+                    for (int u = 0; u < 4; ++u) v[p][u] = lds_ld(lds, in_addr(p, u, brd, xsl) + l8);
+                    const int4 tv = tab_raw(k - G[p]);
+                    pr[p] = __builtin_amdgcn_readfirstlane(tv.x);
+                    fr[p] = __hiloint2double(tv.w, tv.z);
+                    chg = chg || pr[p] != cur[p];
+                }
+                if (chg) {                  // a node's step moved to another row pair (rare)
 #pragma unroll
-            for (int p = 0; p < NPW; ++p) {
+                    for (int p = 0; p < NPW; ++p) {
+                        if (pr[p] != cur[p]) {
+                            const int lo = cur[p] >> 1, hi = lo + (cur[p] & 1);
+                            const int lo2 = pr[p] >> 1, hi2 = lo2 + (pr[p] & 1);
+                            const double a0 = fA[p], b0 = fB[p], n0 = fN[p];
+                            fA[p] = lo2 == lo ? a0 : (lo2 == hi ? b0 : n0);
+                            fB[p] = hi2 == hi ? b0 : (hi2 == lo ? a0 : n0);
+                            if (hi2 != hi) fN[p] = frow(hi2 + 1, vo[p]);
+                            cur[p] = pr[p];
+                        }
+                    }
+                }
+                double prev = 0.0;          // output of the previous position (chained input)
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[p][u] = lds_ld(lds, brd + in_row(p, u) * kRow + l8);
-                en[p] = tab_at(k - G[p]);
+                for (int p = 0; p < NPW; ++p) {
+                    const double q = (1.0 - fr[p]) * fA[p] + fr[p] * fB[p];
+                    // unused inputs read the zero row: adding +0.0 to a sum of published values
+                    // (never -0.0) is exact, so the fold over 4 terms is the reference's fold
+                    double I = v[p][0];
+                    I = I + v[p][1];
+                    I = I + v[p][2];
+                    I = I + v[p][3];
+                    if (p > 0 && chained[p]) I = I + prev;
+                    const double* cf =
+                        reinterpret_cast<const double*>(lds + COEF) + 4 * (p * NW + wv);
+                    const double o = 0.0 + (((cf[0] * I + cf[1] * ip[p]) + cf[2] * op[p]) +
+                                            cf[3] * q);
+                    if constexpr (S) {
+                        op[p] = o;
+                        ip[p] = I;
+                    } else {
+                        const bool act = (unsigned)(k - G[p]) < (unsigned)T;
+                        op[p] = act ? o : op[p];
+                        ip[p] = act ? I : ip[p];
+                    }
+                    prev = o;
+                    lds_st(lds, bwr + (unsigned)(p * NW + wv) * kRow + l8, o);
+                }
+                __syncthreads();
             }
-            double prev = 0.0;              // output of the previous position (chained input)
-#pragma unroll
-            for (int p = 0; p < NPW; ++p) {
-                const bool act = (unsigned)(k - G[p]) < (unsigned)T;
-                const int lo = en[p].x - rb[p], hi = en[p].y - rb[p];
-                const double flo = lo == 0 ? f0[p] : (lo == 1 ? f1[p] : f2[p]);
-                const double fhi = hi == 0 ? f0[p] : (hi == 1 ? f1[p] : f2[p]);
-                const double fr = __hiloint2double(en[p].w, en[p].z);
-                const double q = (1.0 - fr) * flo + fr * fhi;
-                // unused inputs read the zero row: adding +0.0 to a sum of published values
-                // (never -0.0) is exact, so the fold over 4 terms is the reference's fold
-                double I = v[p][0];
-                I = I + v[p][1];
-                I = I + v[p][2];
-                I = I + v[p][3];
-                if (p > 0 && chained[p]) I = I + prev;
-                const double* cf =
-                    reinterpret_cast<const double*>(lds + COEF) + 4 * (p * NW + wv);
-                const double o = 0.0 + (((cf[0] * I + cf[1] * ip[p]) + cf[2] * op[p]) +
-                                        cf[3] * q);
-                op[p] = act ? o : op[p];
-                ip[p] = act ? I : ip[p];
-                prev = o;
-                lds_st(lds, bwr + (unsigned)(p * NW + wv) * kRow + l8, o);
-            }
-#pragma unroll
-            for (int j = 0; j < XW; ++j)
-                lds_st(lds, bwr + ext_row(j) + l8, ring[(i + 1) % kRing][j]);
-            __syncthreads();
-        }
-#pragma unroll
-        for (int p = 0; p < NPW; ++p) {
-            if (rbn[p] != rb[p]) {          // host-checked: one row further
-                f0[p] = f1[p];
-                f1[p] = f2[p];
-                f2[p] = g[p];
-                rb[p] = rbn[p];
-            }
-        }
+        };
+        if (steady)
+            chunk(std::true_type{});
+        else
+            chunk(std::false_type{});
     }
     if (tr) {
         const int64_t c_end = clock64();
@@ -420,8 +481,9 @@ inline int grid_for(int64_t work, int block) {
 
 hipError_t launch_member_sweep(const SweepArgs& a, int grid, int member_groups, hipStream_t s) {
     if (grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL((member_sweep<kSweepNPW, kSweepNW, kSweepXW>), dim3(grid, member_groups),
-                       dim3(64 * (kSweepNW + 1)), sweep_lds_bytes(), s, a);
+    hipLaunchKernelGGL((member_sweep<kSweepNPW, kSweepNW, kSweepMaxExt>),
+                       dim3(grid, member_groups), dim3(64 * (kSweepNW + 2)), sweep_lds_bytes(), s,
+                       a);
     return hipGetLastError();
 }
 

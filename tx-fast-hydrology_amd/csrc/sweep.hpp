@@ -28,9 +28,8 @@ namespace mcr {
 constexpr int kSweepNPW = 4;
 constexpr int kSweepNW = 8;
 constexpr int kSweepSlots = kSweepNPW * kSweepNW;
-// external inputs (inputs from other workgroups) staged per wave and per workgroup
-constexpr int kSweepXW = 3;
-constexpr int kSweepMaxExt = kSweepNW * kSweepXW;
+// external inputs (inputs from other workgroups) per workgroup (even: two rows per LDS-DMA)
+constexpr int kSweepMaxExt = 24;
 
 struct SweepArgs {
     const int32_t* active;     // workgroups of this launch
@@ -68,7 +67,8 @@ struct SweepArgs {
 constexpr int kSweepTile = MCR_SWEEP_TILE;
 constexpr int kSweepTabCap = 640;
 inline size_t sweep_lds_bytes() {
-    return 16u * kSweepTabCap + 36u * kSweepSlots + 2u * (kSweepSlots + 1 + kSweepMaxExt) * 512u;
+    return 16u * kSweepTabCap + 36u * kSweepSlots + 2u * (kSweepSlots + 1) * 512u +
+           4u * kSweepMaxExt * 512u;
 }
 
 hipError_t launch_member_sweep(const SweepArgs& a, int grid, int member_groups, hipStream_t s);
