@@ -498,7 +498,7 @@ def main():
     launches = max(tm["launches"], 1)
     launch_ms = tm["kernel_ms"] / launches
     path = net.mode()[1]
-    kernel = "wavefront_flow" if path == "dataflow" else "wavefront_det"
+    kernel = {"dataflow": "wavefront_flow", "sweep": "member_sweep"}.get(path, "wavefront_det")
     if wl.enkf is not None and len(nets) > 1:
         # member steps on the member-dataflow kernel, the forecast on the multi-launch kernel
         kernel = "wavefront_flow (member steps) + wavefront_det (forecast)"
@@ -527,6 +527,20 @@ def main():
             "floor": "mc_probe_tick_floor: the bare tick chain of this kernel shape (LDS inputs, "
                      "chained updates, LDS outputs, barrier; 2 workgroups per CU, no memory "
                      "traffic), measured now on this device"}
+    elif wl.enkf is None and E > 1:
+        # an ensemble horizon is throughput-bound: its critical path (the schedule's ticks at the
+        # bare tick latency) is a small fraction of it, and the bound it is measured against is
+        # the HBM roofline of the bytes it must move (compulsory, below)
+        ticks = info["gmax"] + args.T
+        ns_tick = engine.probe_tick_floor(192, 2, 8192)
+        floor_ms = ticks * ns_tick * 1e-6
+        roofline["bound"] = "hbm"
+        roofline["latency"] = {
+            "schedule_ticks": ticks, "floor_ns_per_tick": round(ns_tick, 2),
+            "floor_ms": round(floor_ms, 4), "frac": round(floor_ms / (launch_ms *
+                                                                       launches_per_step), 4),
+            "floor": "critical path: schedule ticks x the bare tick latency of the 192-lane "
+                     "dataflow tick (mc_probe_tick_floor), a lower bound for any ensemble path"}
     else:
         roofline["latency"] = None
     roofline["compulsory"] = {

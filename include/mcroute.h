@@ -176,6 +176,25 @@ int mc_ens_weights(void* net, int64_t nranks, int64_t m, const double* HXall_dev
 int mc_ens_increments(void* net, int64_t nranks, const double* Xs_dev, double* Gs_dev);
 int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv_dev);
 
+/* The member-sharded analysis for callers without torch.distributed: a
+ * communicator of nranks processes, one GPU each, over RCCL (xGMI), which the library loads at
+ * first use (librccl.so.1; a process that already holds one -- e.g. PyTorch's -- shares it).
+ *   mc_comm_unique_id: rank 0 makes the 128-byte id and hands it to the other ranks (any
+ *                      channel: MPI, a file, a socket);
+ *   mc_comm_init:      every rank, with the same id (collective: blocks until all ranks join);
+ *   mc_ens_analysis_dist: one analysis of this rank's E members (y_local [m][E]; gauges and R
+ *                      identical on every rank): the stages above with the all-gathers and
+ *                      all-to-alls on the session's stream, the member -> slice all-to-all on a
+ *                      side stream while the Et x Et weights are formed.  Bit-identical to the
+ *                      staged Python driver (ensemble.distributed_analysis) and, with one rank,
+ *                      to mc_enkf_analysis.
+ * MC_E_STATE when no RCCL library can be loaded. */
+int mc_comm_unique_id(uint8_t* id128);
+int mc_comm_init(int32_t nranks, int32_t rank, const uint8_t* id128, void** comm);
+int mc_comm_destroy(void* comm);
+int mc_ens_analysis_dist(void* net, void* comm, int64_t m, const int64_t* gauges,
+                         const double* y_local, const double* R);
+
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
                   const double* gamma);
 /* State (o_t_next, i_t_next) of the model, caller order. */

@@ -191,6 +191,36 @@ def test_staged_driver_single_rank_equals_enkf_analysis():
     assert np.array_equal(oa, ob) and np.array_equal(ia, ib)
 
 
+def test_comm_analysis_single_rank_equals_enkf_analysis():
+    """The C ABI's own communicator (mc_comm_* over RCCL, no torch.distributed): one rank runs
+    the whole program -- all-gathers, both all-to-alls (copies with one rank), the weights under
+    the member -> slice all-to-all on the side stream -- and reproduces RoutingNet.enkf_analysis
+    exactly (two ranks cannot share the one GPU of a test box under RCCL)."""
+    end = synthetic.river_network(5000, 4, 150, np.random.default_rng(18))
+    n = end.size
+    E, m = 16, 30
+    rng = np.random.default_rng(19)
+    X = rng.uniform(0.5, 5, n)[:, None] * rng.lognormal(0, 0.3, (n, E))
+    I0 = rng.uniform(0, 5, (n, E))
+    s = np.sort(rng.choice(n, m, replace=False))
+    R = 2e-2 * np.eye(m)
+    Y = X[s] + rng.normal(0, 0.1, (m, E))
+    a, _, _ = _net(end, members=E)
+    a.set_state(X, I0)
+    a.enkf_analysis(s, Y, R)
+    b, _, _ = _net(end, members=E)
+    b.set_state(X, I0)
+    comm = engine.Communicator(1, 0, engine.Communicator.unique_id())
+    for _ in range(2):                         # scratch reuse across analyses
+        b.ens_analysis_dist(comm, s, Y, R)
+        if _ == 0:
+            a.enkf_analysis(s, Y, R)
+    oa, ia = a.get_state()
+    ob, ib = b.get_state()
+    assert np.array_equal(oa, ob) and np.array_equal(ia, ib)
+    comm.close()
+
+
 # (16, 40), (48, 12): the one-workgroup SPD solve; (96, 150), (200, 260): E > 64, the
 # factorisation and the two triangular solves of the large-ensemble path
 @pytest.mark.parametrize("E,m", [(16, 40), (48, 12), (96, 150), (200, 260)])

@@ -2,6 +2,9 @@
 #include "mcroute.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <atomic>
@@ -16,6 +19,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "analysis.hpp"
@@ -1542,6 +1546,73 @@ struct Net {
     }
 };
 
+// ---- C-level communicator: RCCL loaded at first use (no link-time dependency) ---------------
+struct Rccl {
+    bool tried = false;
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclAllToAll) all_to_all = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+};
+Rccl& rccl() {
+    static Rccl R;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!R.tried) {
+        R.tried = true;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            R.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (R.h) break;
+        }
+        if (R.h) {
+            auto sym = [&](auto& f, const char* n) {
+                f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(R.h, n));
+            };
+            sym(R.get_id, "ncclGetUniqueId");
+            sym(R.init, "ncclCommInitRank");
+            sym(R.destroy, "ncclCommDestroy");
+            sym(R.all_gather, "ncclAllGather");
+            sym(R.all_to_all, "ncclAllToAll");
+            sym(R.group_start, "ncclGroupStart");
+            sym(R.group_end, "ncclGroupEnd");
+            sym(R.err, "ncclGetErrorString");
+        }
+    }
+    if (!R.h || !R.get_id || !R.init || !R.destroy || !R.all_gather || !R.all_to_all ||
+        !R.group_start || !R.group_end || !R.err)
+        throw Fail(MC_E_STATE, "RCCL (librccl.so.1) could not be loaded");
+    return R;
+}
+#define NCCLC(call)                                                                    \
+    do {                                                                               \
+        const ncclResult_t r_ = (call);                                                \
+        if (r_ != ncclSuccess) throw Fail(MC_E_HIP, std::string("RCCL: ") + rccl().err(r_)); \
+    } while (0)
+
+struct Comm {
+    ncclComm_t c = nullptr;
+    int nranks = 1, rank = 0;
+    hipStream_t side = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    DBuf<double> HX, D, HXall, Dall, send, Xs, Gs, Grecv;
+    ~Comm() {
+        if (side) (void)hipStreamSynchronize(side);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (side) (void)hipStreamDestroy(side);
+        if (c) (void)rccl().destroy(c);
+    }
+};
+Comm* as_comm(void* h) {
+    if (!h) throw Fail(MC_E_INVALID, "null communicator handle");
+    return static_cast<Comm*>(h);
+}
+
 Net* as_net(void* h) {
     if (!h) throw Fail(MC_E_INVALID, "null session handle");
     return static_cast<Net*>(h);
@@ -1720,6 +1791,76 @@ int mc_ens_increments(void* net, int64_t nranks, const double* Xs, double* Gs) {
 
 int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv) {
     return guarded([&] { as_net(net)->ens_unpack_apply(nranks, Grecv); });
+}
+
+int mc_comm_unique_id(uint8_t* id128) {
+    return guarded([&] {
+        REQUIRE(id128, "id must not be NULL");
+        static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+        ncclUniqueId id;
+        NCCLC(rccl().get_id(&id));
+        std::memcpy(id128, &id, sizeof(id));
+    });
+}
+
+int mc_comm_init(int32_t nranks, int32_t rank, const uint8_t* id128, void** comm) {
+    return guarded([&] {
+        REQUIRE(comm && id128, "null argument");
+        REQUIRE(nranks >= 1 && 0 <= rank && rank < nranks, "rank out of range");
+        *comm = nullptr;
+        auto C = std::make_unique<Comm>();
+        C->nranks = nranks;
+        C->rank = rank;
+        ncclUniqueId id;
+        std::memcpy(&id, id128, sizeof(id));
+        NCCLC(rccl().init(&C->c, nranks, id, rank));
+        HIPC(hipStreamCreateWithFlags(&C->side, hipStreamNonBlocking));
+        for (hipEvent_t& e : C->ev) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        *comm = C.release();
+    });
+}
+
+int mc_comm_destroy(void* comm) {
+    return guarded([&] { delete static_cast<Comm*>(comm); });
+}
+
+int mc_ens_analysis_dist(void* net, void* comm, int64_t m, const int64_t* gauges,
+                         const double* y_local, const double* R) {
+    return guarded([&] {
+        Net& N = *as_net(net);
+        Comm& C = *as_comm(comm);
+        REQUIRE(m >= 1 && gauges && y_local && R, "bad analysis arguments");
+        if (N.plan.n == 0) return;
+        const int64_t P = C.nranks, E = N.E, S = N.slice_size(P), Et = E * P;
+        REQUIRE(Et >= 2, "the ensemble analysis needs at least 2 members");
+        const hipStream_t st = N.stream;
+        Rccl& R_ = rccl();
+        C.HX.reserve((size_t)(E * m));
+        C.D.reserve((size_t)(E * m));
+        C.send.reserve((size_t)(P * E * S));
+        C.HXall.reserve((size_t)(Et * m));
+        C.Dall.reserve((size_t)(Et * m));
+        C.Xs.reserve((size_t)(P * E * S));
+        C.Gs.reserve((size_t)(Et * S));
+        C.Grecv.reserve((size_t)(Et * S));
+        N.ens_gauges(m, gauges, y_local, C.HX.p, C.D.p);
+        N.ens_pack(P, C.send.p);
+        // (one rank: the collectives are copies; the program is the same)
+        NCCLC(R_.group_start());
+        NCCLC(R_.all_gather(C.HX.p, C.HXall.p, (size_t)(E * m), ncclDouble, C.c, st));
+        NCCLC(R_.all_gather(C.D.p, C.Dall.p, (size_t)(E * m), ncclDouble, C.c, st));
+        NCCLC(R_.group_end());
+        // the member -> slice all-to-all travels on the side stream while the weights form
+        HIPC(hipEventRecord(C.ev[0], st));
+        HIPC(hipStreamWaitEvent(C.side, C.ev[0], 0));
+        NCCLC(R_.all_to_all(C.send.p, C.Xs.p, (size_t)(E * S), ncclDouble, C.c, C.side));
+        HIPC(hipEventRecord(C.ev[1], C.side));
+        N.ens_weights(P, m, C.HXall.p, C.Dall.p, R);
+        HIPC(hipStreamWaitEvent(st, C.ev[1], 0));
+        N.ens_increments(P, C.Xs.p, C.Gs.p);
+        NCCLC(R_.all_to_all(C.Gs.p, C.Grecv.p, (size_t)(E * S), ncclDouble, C.c, st));
+        N.ens_unpack_apply(P, C.Grecv.p);
+    });
 }
 
 int mc_enkf_gain(void* net, int64_t m, const int64_t* gauges, const double* R, double* K_out) {

@@ -24,9 +24,12 @@
 namespace mcr {
 
 // node slots per wave and waves per workgroup; the member plan has NPW * NW slots per
-// workgroup (plan slots = 32, chain 1)
+// workgroup (plan: kSweepNW lanes x kSweepNPW positions)
+#ifndef MCR_SWEEP_NW
+#define MCR_SWEEP_NW 8
+#endif
 constexpr int kSweepNPW = 4;
-constexpr int kSweepNW = 8;
+constexpr int kSweepNW = MCR_SWEEP_NW;
 constexpr int kSweepSlots = kSweepNPW * kSweepNW;
 // external inputs (inputs from other workgroups) per workgroup (even: two rows per LDS-DMA)
 constexpr int kSweepMaxExt = 24;

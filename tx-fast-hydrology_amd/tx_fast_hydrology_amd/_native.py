@@ -109,6 +109,10 @@ SIGNATURES = {
     "mc_ens_weights": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "mc_ens_increments": (_i32, [_vp, _i64, _vp, _vp]),
     "mc_ens_unpack_apply": (_i32, [_vp, _i64, _vp]),
+    "mc_comm_unique_id": (_i32, [_vp]),
+    "mc_comm_init": (_i32, [ctypes.c_int32, ctypes.c_int32, _vp, _pp]),
+    "mc_comm_destroy": (_i32, [_vp]),
+    "mc_ens_analysis_dist": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "mc_set_mode": (_i32, [_vp, ctypes.c_int]),
     "mc_set_flow_patience": (_i32, [_vp, _i64]),
     "mc_net_lateral_correction": (_i32, [_vp, _i64, _vp, _i64, ctypes.c_double, ctypes.c_double,

@@ -90,6 +90,40 @@ class Plan:
             pass
 
 
+class Communicator:
+    """Member-sharding communicator of the C ABI (mcroute.h mc_comm_*): nranks processes, one GPU
+    each, over RCCL, without torch.distributed.  Rank 0 makes the id (``unique_id()``) and hands
+    it to the others by any channel; every rank then constructs ``Communicator(nranks, rank,
+    id)`` (collective).  ``RoutingNet.ens_analysis_dist(comm, ...)`` runs one analysis."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        nat.check(nat.lib().mc_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+        return bytes(buf)
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        if len(uid) != 128:
+            raise ValueError("the communicator id is 128 bytes (Communicator.unique_id())")
+        self.nranks, self.rank = int(nranks), int(rank)
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        nat.check(nat.lib().mc_comm_init(self.nranks, self.rank,
+                                         ctypes.cast(buf, ctypes.c_void_p), ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.lib().mc_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
 class RoutingNet:
     """Device-resident routing session for one network (one HIP device, one stream).
 
@@ -222,6 +256,17 @@ class RoutingNet:
             raise ValueError("y must be [m, E] and R [m, m]")
         nat.check(nat.lib().mc_enkf_analysis(self._h, m, ptr(gs), ptr(yy), ptr(RR)))
 
+    def ens_analysis_dist(self, comm: "Communicator", gauges, y_local, R) -> None:
+        """One member-sharded analysis of this rank's E members over `comm` (RCCL;
+        mcroute.h mc_ens_analysis_dist): gauges [m] and R [m, m] identical on every rank,
+        y_local [m, E] this rank's perturbed observations."""
+        g = i64(gauges)
+        y = f64(y_local)
+        Rm = f64(R)
+        m = g.size
+        if y.shape != (m, self.E) or Rm.shape != (m, m):
+            raise ValueError("y_local must be [m, E] and R [m, m]")
+        nat.check(nat.lib().mc_ens_analysis_dist(self._h, comm._h, m, ptr(g), ptr(y), ptr(Rm)))
     def enkf_gain(self, gauges, R):
         """Kalman gain of the current ensemble, K = P H^T (H P H^T + R)^-1, as [n, m]."""
         gs, RR = i64(gauges), f64(R)
