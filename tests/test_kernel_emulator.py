@@ -83,3 +83,26 @@ def test_emulator_river_network_and_golden_edges(golden, chain):
                        np.array([0.0]), a[6][None, :])
         assert np.array_equal(O[:, 0], g[f"{name}_o"]), name
         assert np.array_equal(I[:, 0], g[f"{name}_i"]), name
+
+
+@pytest.mark.parametrize("slots,chain,tile", [(8, 4, 16), (8, 4, 32), (4, 4, 16), (32, 1, 32)])
+def test_emulator_member_plans(slots, chain, tile):
+    """The member sweep's plans (sweep.hpp: a "lane" is a wave of members, so a workgroup has
+    8 or 4 lanes of 4 positions, or 32 lanes of one): the same launch / tick protocol on them
+    reproduces the oracle (chained positions within a tick, cross-workgroup inputs from earlier
+    launches, partial sums)."""
+    rng = np.random.default_rng(slots * 100 + tile)
+    end = synthetic.random_forest(2500, 6, rng, p_chain=0.9)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=3)
+    start, indeg, coef, i0 = _case(end, K, X, 300.0, o0)
+    xp, fp = synthetic.forcing(n, rows=5, seed=4)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 45)
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile, chain=chain,
+                       ext_cap=4)
+    assert plan.info["slots"] == slots and plan.info["chain"] == chain
+    O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
+    assert np.array_equal(O.T, want_o)
+    assert np.array_equal(I.T, want_i)
