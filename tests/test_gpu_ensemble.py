@@ -364,12 +364,30 @@ def test_member_sweep_bitexact(n, E, T, rows, mode):
     net.close()
 
 
-def test_member_sweep_needs_sparse_forcing_rows():
-    """A step as long as the forcing interval (8 steps touch 9 rows) cannot keep its rows in the
-    sweep's 3-row window: other modes route it with launches, sweep mode refuses it."""
+@pytest.mark.parametrize("dt_s,sweeps", [(3600.0, True), (7200.0, False)])
+def test_member_sweep_forcing_row_steps(dt_s, sweeps):
+    """A step as long as the forcing interval advances one row per step: the sweep's row-pair
+    registers follow it (bit-exact).  A longer step skips rows: other modes route it with
+    launches, sweep mode refuses it."""
     E, T = 32, 20
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 9, E, rows=30)
-    x = xp[0] + 3600e9 * np.arange(1, T + 1)
+    end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 9, E, rows=50)
+    x = xp[0] + dt_s * 1e9 * np.arange(1, T + 1)
+    if sweeps:
+        net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
+        net.set_mode("sweep")
+        net.set_coeffs(*coef)
+        net.set_state(o0, i0)
+        net.load_forcing(xp, fpe)
+        net.run(x)
+        assert net.mode()[1] == "sweep"
+        got_o, got_i = net.fetch_outputs(0, T)
+        for e in (0, 17, E - 1):
+            want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e],
+                                                x, xp, np.ascontiguousarray(fpe[:, :, e]))
+            assert np.array_equal(got_o[:, :, e], want_o), e
+            assert np.array_equal(got_i[:, :, e], want_i), e
+        net.close()
+        return
     net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)

@@ -23,11 +23,9 @@
 // forcing rows), the store wave never waits for its stores, the loader waits only for its own
 // loads.  Forcing: a node keeps f[lo], f[hi] of its current step's row pair and f[hi + 1];
 // when its step moves to the next pair (host-checked: rows advance by at most one per step)
-// they shift and the next row is loaded.  A chunk of 8 ticks in which every node of a wave runs
-// all its ticks is routed without activity selects.
+// they shift and the next row is loaded.
 #include "sweep.hpp"
 
-#include <type_traits>
 
 #include "kernels.hpp"
 #include "plan.hpp"
@@ -84,13 +82,15 @@ template <int NPW, int NW, int XMAX>
 __global__ __launch_bounds__(64 * (NW + 2), MCR_SWEEP_MIN_WAVES)
 void member_sweep(SweepArgs a) {
     constexpr int RS = NPW * NW;
-    constexpr unsigned TAB = 0;                                   // int4 [kSweepTabCap]
-    constexpr unsigned COEF = TAB + 16u * kSweepTabCap;           // double [RS][4]
-    constexpr unsigned GT = COEF + 32u * RS;                      // int [RS]
-    constexpr unsigned XB = GT + 4u * RS;                         // [2][RS + 1] rows
-    constexpr unsigned BUF = (RS + 1) * kRow;
+    // the parity buffers first, so that their offsets fit a DS instruction's immediate
+    constexpr unsigned XB = 0;                                    // [2][RS + 1 + XMAX] rows
+    constexpr unsigned BUF = (RS + 1 + XMAX) * kRow;
     constexpr unsigned XE = XB + 2 * BUF;                         // [kRing][XMAX] rows
     constexpr unsigned XSLOT = XMAX * kRow;
+    constexpr unsigned TAB = XE + kRing * XSLOT;                  // int4 [kSweepTabCap]
+    constexpr unsigned COEF = TAB + 16u * kSweepTabCap;           // double [RS][4]
+    constexpr unsigned GT = COEF + 32u * RS;                      // int [RS]
+    static_assert(2 * BUF <= 65536, "parity buffers must be addressable by DS immediates");
     extern __shared__ __attribute__((aligned(16))) char lds[];
 
     const int lane = threadIdx.x & 63;
@@ -169,15 +169,29 @@ void member_sweep(SweepArgs a) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
         };
+        // ring slot of consumer tick j -> the ext rows of parity buffer (j - 1) & 1, which the
+        // consumers of tick j read (two rows per 16-B lane access)
+        auto stage = [&](int j) {
+            const unsigned src = XE + (unsigned)(j & (kRing - 1)) * XSLOT;
+            const unsigned dst = XB + (unsigned)((j - 1) & 1) * BUF + (unsigned)(RS + 1) * kRow;
+            const unsigned l16 = (unsigned)lane * 16u;
+            for (int m = 0; m < nin; ++m) {
+                typedef double d2 __attribute__((ext_vector_type(2)));
+                const d2 v = *reinterpret_cast<const d2*>(lds + src + 1024u * m + l16);
+                *reinterpret_cast<d2*>(lds + dst + 1024u * m + l16) = v;
+            }
+        };
         barrier();                                       // table window, G
         issue(k0);
         issue(k0 + 1);
         issue(k0 + 2);
         wait_two();                                      // tick k0's rows have landed
+        stage(k0);
         barrier();                                       // prologue of the compute waves
         for (int k = k0; k < k0 + tile; ++k) {
             issue(k + kRing - 1);
             wait_two();                                  // the rows of tick k + 1
+            stage(k + 1);
             barrier();
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -270,14 +284,22 @@ void member_sweep(SweepArgs a) {
         fB[p] = frow(hi, vo[p]);
         fN[p] = frow(hi + 1, vo[p]);
     }
-    // LDS address of input u of node p at a tick reading parity buffer `brd` and ring slot
-    // `xsl` (a chained input -- the previous position's output of the same tick, always the last
-    // input of the fold -- and an unused one read the zero row)
-    auto in_addr = [&](int p, int u, unsigned brd, unsigned xsl) -> unsigned {
-        unsigned code = u < cnt[p] ? (unsigned)((up[p] >> (16 * u)) & 0xffffu) : (unsigned)RS;
-        if (code == kSelfCode) code = RS;
-        return (code & kExtBit) ? xsl + (code & 0x7fffu) * kRow : brd + code * kRow;
-    };
+    // LDS byte offset (lane included) of input u of node p inside a parity buffer: its node
+    // row, an external input's row, or the zero row (unused inputs, and a chained input -- the
+    // previous position's output of the same tick, always the last input of the fold, added
+    // from a register)
+    unsigned va[NPW][4];
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            unsigned code =
+                u < cnt[p] ? (unsigned)((up[p] >> (16 * u)) & 0xffffu) : (unsigned)RS;
+            if (code == kSelfCode) code = RS;
+            const unsigned row = (code & kExtBit) ? (unsigned)(RS + 1) + (code & 0x7fffu) : code;
+            va[p][u] = row * kRow + l8;
+        }
+    }
     bool chained[NPW];
 #pragma unroll
     for (int p = 0; p < NPW; ++p) {
@@ -302,19 +324,12 @@ void member_sweep(SweepArgs a) {
     const int64_t c_loop = tr ? clock64() : 0;
 
     for (int kc = k0; kc < k0 + tile; kc += kChunk) {
-        // a chunk in which every node of this wave runs all its ticks needs no activity selects
-        bool steady = true;
-#pragma unroll
-        for (int p = 0; p < NPW; ++p)
-            steady = steady && kc - G[p] >= 0 && kc + kChunk - 1 - G[p] < T;
-        auto chunk = [&](auto steady_tag) {
-            constexpr bool S = decltype(steady_tag)::value;
+        {
 #pragma unroll 2
             for (int i = 0; i < kChunk; ++i) {
                 const int k = kc + i;
                 const unsigned brd = XB + (unsigned)((i + 1) & 1) * BUF;   // tick k - 1
                 const unsigned bwr = XB + (unsigned)(i & 1) * BUF;
-                const unsigned xsl = XE + (unsigned)(i % kRing) * XSLOT;   // kc % kRing == 0
                 // every node's inputs and table entry first, then the updates without branches,
                 // so the NPW dependency chains of the tick interleave (a node that does not run
                 // this tick computes a value nobody reads: its consumers do not run at k + 1)
@@ -324,7 +339,7 @@ void member_sweep(SweepArgs a) {
 #pragma unroll
                 for (int p = 0; p < NPW; ++p) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) v[p][u] = lds_ld(lds, in_addr(p, u, brd, xsl) + l8);
+                    for (int u = 0; u < 4; ++u) v[p][u] = lds_ld(lds, brd + va[p][u]);
                     const int4 tv = tab_raw(k - G[p]);
                     pr[p] = __builtin_amdgcn_readfirstlane(tv.x);
                     fr[p] = __hiloint2double(tv.w, tv.z);
@@ -359,24 +374,15 @@ void member_sweep(SweepArgs a) {
                         reinterpret_cast<const double*>(lds + COEF) + 4 * (p * NW + wv);
                     const double o = 0.0 + (((cf[0] * I + cf[1] * ip[p]) + cf[2] * op[p]) +
                                             cf[3] * q);
-                    if constexpr (S) {
-                        op[p] = o;
-                        ip[p] = I;
-                    } else {
-                        const bool act = (unsigned)(k - G[p]) < (unsigned)T;
-                        op[p] = act ? o : op[p];
-                        ip[p] = act ? I : ip[p];
-                    }
+                    const bool act = (unsigned)(k - G[p]) < (unsigned)T;
+                    op[p] = act ? o : op[p];
+                    ip[p] = act ? I : ip[p];
                     prev = o;
                     lds_st(lds, bwr + (unsigned)(p * NW + wv) * kRow + l8, o);
                 }
                 __syncthreads();
             }
-        };
-        if (steady)
-            chunk(std::true_type{});
-        else
-            chunk(std::false_type{});
+        }
     }
     if (tr) {
         const int64_t c_end = clock64();

@@ -68,9 +68,9 @@ struct SweepArgs {
 #define MCR_SWEEP_TILE 32
 #endif
 constexpr int kSweepTile = MCR_SWEEP_TILE;
-constexpr int kSweepTabCap = 640;
+constexpr int kSweepTabCap = 352;
 inline size_t sweep_lds_bytes() {
-    return 16u * kSweepTabCap + 36u * kSweepSlots + 2u * (kSweepSlots + 1) * 512u +
+    return 16u * kSweepTabCap + 36u * kSweepSlots + 2u * (kSweepSlots + 1 + kSweepMaxExt) * 512u +
            4u * kSweepMaxExt * 512u;
 }
 
