@@ -730,6 +730,235 @@ __global__ __launch_bounds__(256) void member_inputs(
     }
 }
 
+// Member staging of the skewed windows through LDS (E >= kSkewMembers): one wave per group of
+// kStageSlots consecutive slots (one 256-B IO segment of a window row).  The per-lane form above
+// writes cell (d, e) at row G[d] + e, so a wave's store touches a different window line in
+// almost every lane (~3.7 TB/s at EnKF256); here the wave reads the member-major side a whole
+// 128-B line per 16 lanes (4 members per load), keeps the staged {o, i, q} of the last
+// kStageRing members in an LDS ring, and writes the window rows whose members are all staged,
+// 4 rows x 16 slots per store: both sides move whole lines.  A group whose G spread exceeds what
+// the ring can hold (spread > kStageRing - kStageChunk) stores directly, as the per-lane form.
+// Same operations per (d, e) as member_inputs, so bit-identical.
+#ifndef MCR_STAGE_RING
+#define MCR_STAGE_RING 1
+#endif
+constexpr int kStageSlots = 16;
+constexpr int kStageRing = 32;
+#ifndef MCR_STAGE_CHUNK
+#define MCR_STAGE_CHUNK 16
+#endif
+constexpr int kStageChunk = MCR_STAGE_CHUNK;     // members staged per round (4 per load)
+constexpr int kStageLoads = kStageChunk / 4;
+template <bool GAIN>
+__global__ __launch_bounds__(256) void member_inputs_ring(
+        const double* __restrict__ F, int64_t mF, int64_t ns, int n_rows, int4 ent,
+        const double* __restrict__ st_o, const double* __restrict__ st_i,
+        double2* __restrict__ IO, double* __restrict__ Qm, int64_t E, MemberWin mw,
+        PendingGain gain) {
+    __shared__ double ring[4][3][kStageRing * kStageSlots];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int s = lane & (kStageSlots - 1), sub = lane >> 4;
+    const int64_t d0 = ((int64_t)blockIdx.x * 4 + wv) * kStageSlots;
+    if (d0 >= ns) return;                                  // wave-uniform
+    const int64_t d = d0 + s;
+    const uint8_t fl = mw.flags[d];
+    const bool real = fl != kSlotPad;
+    const int64_t w = d0 / mw.rs;
+    const int gs = real ? mw.G[d] - mw.gmin[w] : 0;       // window row of member 0
+    int glo = real ? gs : 0x7fffffff, ghi = real ? gs : -1;
+#pragma unroll
+    for (int o = kStageSlots / 2; o >= 1; o >>= 1) {
+        glo = min(glo, __shfl_xor(glo, o, kStageSlots));
+        ghi = max(ghi, __shfl_xor(ghi, o, kStageSlots));
+    }
+    if (ghi < 0) return;                                   // padding only (wave-uniform)
+    const int64_t rs = mw.rs;
+    const int64_t cell0 = mw.wbase[w] + (d - w * rs);
+    const double f = __hiloint2double(ent.w, ent.z);
+    const int64_t rlo = (int64_t)clamp_row(ent.x, n_rows) * ns + d;
+    const int64_t rhi = (int64_t)clamp_row(ent.y < 0 ? ent.x : ent.y, n_rows) * ns + d;
+    const bool gained = GAIN && (fl == kSlotRouted || fl == kSlotUnrouted);
+    const int32_t u0 = GAIN ? gain.up_off[d] : 0, u1 = GAIN ? gain.up_off[d + 1] : 0;
+    // the first kUpInline upstream slots in registers: their increments are loaded together
+    // (independent loads) and folded in rank order; longer lists continue in a loop
+    int32_t upr[kUpInline];
+#pragma unroll
+    for (int k = 0; k < kUpInline; ++k) upr[k] = GAIN && u0 + k < u1 ? gain.up[u0 + k] : (int32_t)d;
+    auto value = [&](int64_t e, double& o, double& i, double& q) {
+        const int64_t idx = e * ns + d;
+        const double* Fe = F + e * mF;
+        const double lo = Fe[rlo];
+        const double hi = Fe[rhi];
+        o = st_o[idx];
+        i = st_i[idx];
+        if (gained) {
+            const double* Ge = gain.G + e * ns;
+            double gu[kUpInline];
+#pragma unroll
+            for (int k = 0; k < kUpInline; ++k) gu[k] = Ge[upr[k]];   // unconditional (dummy d)
+            const double og = fl == kSlotRouted ? 0.0 + Ge[d] : 0.0;
+            double ig = 0.0;
+#pragma unroll
+            for (int k = 0; k < kUpInline; ++k) ig = u0 + k < u1 ? ig + (0.0 + gu[k]) : ig;
+            for (int32_t u = u0 + kUpInline; u < u1; ++u) ig = ig + (0.0 + Ge[gain.up[u]]);
+            o = o + og;
+            i = i + ig;
+        }
+        q = ent.y < 0 ? lo : (1.0 - f) * lo + f * hi;
+    };
+    if (ghi - glo > kStageRing - kStageChunk) {            // wide group (wave-uniform)
+        if (real)
+            for (int64_t e0 = 0; e0 < E; e0 += kStageChunk) {
+                double o[kStageLoads], i[kStageLoads], q[kStageLoads];
+#pragma unroll
+                for (int h = 0; h < kStageLoads; ++h)
+                    if (e0 + 4 * h + sub < E) value(e0 + 4 * h + sub, o[h], i[h], q[h]);
+#pragma unroll
+                for (int h = 0; h < kStageLoads; ++h) {
+                    const int64_t e = e0 + 4 * h + sub;
+                    if (e < E) {
+                        const int64_t c = cell0 + ((int64_t)gs + e) * rs;
+                        IO[c] = make_double2(o[h], i[h]);
+                        Qm[c] = q[h];
+                    }
+                }
+            }
+        return;
+    }
+    double* Ro = ring[wv][0];
+    double* Ri = ring[wv][1];
+    double* Rq = ring[wv][2];
+    const int rend = ghi + (int)E;                         // rows glo .. rend - 1
+    int next = glo;                                        // first row not yet stored
+    for (int e0 = 0; e0 < (int)E; e0 += kStageChunk) {
+        double o[kStageLoads], i[kStageLoads], q[kStageLoads];
+#pragma unroll
+        for (int h = 0; h < kStageLoads; ++h) {
+            const int e = e0 + 4 * h + sub;
+            if (real && e < (int)E) value(e, o[h], i[h], q[h]);
+        }
+#pragma unroll
+        for (int h = 0; h < kStageLoads; ++h) {
+            const int e = e0 + 4 * h + sub;
+            if (real && e < (int)E) {
+                const int k = (e & (kStageRing - 1)) * kStageSlots + s;
+                Ro[k] = o[h];
+                Ri[k] = i[h];
+                Rq[k] = q[h];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // rows whose members are all staged: row r takes member r - gs <= r - glo
+        const int staged = min(e0 + kStageChunk, (int)E);
+        const int rstop = staged >= (int)E ? rend : glo + staged;
+        if (next < rstop) {
+            for (int r0 = next; r0 < rstop; r0 += 4) {
+                const int r = r0 + sub;
+                const int e = r - gs;
+                if (real && r < rstop && e >= 0 && e < (int)E) {
+                    const int k = (e & (kStageRing - 1)) * kStageSlots + s;
+                    const int64_t c = cell0 + (int64_t)r * rs;
+                    IO[c] = make_double2(Ro[k], Ri[k]);
+                    Qm[c] = Rq[k];
+                }
+            }
+            next = rstop;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// The reverse of member_inputs_ring for member_unpack: a wave per group of kStageSlots slots
+// reads the group's window rows in order (4 rows x 16 slots per load: whole lines), parks the
+// cells in an LDS ring by member, and writes each member's {o, i} once every slot's cell of it
+// has been read (member e is complete after row ghi + e), 4 members x 16 slots per store.
+template <int UNUSED = 0>
+__global__ __launch_bounds__(256) void member_unpack_ring(
+        const double2* __restrict__ IO, double* __restrict__ st_o, double* __restrict__ st_i,
+        int64_t ns, int64_t E, MemberWin mw) {
+    __shared__ double ring[4][2][kStageRing * kStageSlots];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int s = lane & (kStageSlots - 1), sub = lane >> 4;
+    const int64_t d0 = ((int64_t)blockIdx.x * 4 + wv) * kStageSlots;
+    if (d0 >= ns) return;                                  // wave-uniform
+    const int64_t d = d0 + s;
+    const bool real = mw.flags[d] != kSlotPad;
+    const int64_t w = d0 / mw.rs;
+    const int gs = real ? mw.G[d] - mw.gmin[w] : 0;
+    int glo = real ? gs : 0x7fffffff, ghi = real ? gs : -1;
+#pragma unroll
+    for (int o = kStageSlots / 2; o >= 1; o >>= 1) {
+        glo = min(glo, __shfl_xor(glo, o, kStageSlots));
+        ghi = max(ghi, __shfl_xor(ghi, o, kStageSlots));
+    }
+    if (ghi < 0) return;
+    const int64_t rs = mw.rs;
+    const int64_t cell0 = mw.wbase[w] + (d - w * rs);
+    if (ghi - glo > kStageRing - kStageChunk) {            // wide group: direct, per lane
+        if (real)
+            for (int64_t e0 = 0; e0 < E; e0 += kStageChunk) {
+                double2 v[kStageLoads];
+#pragma unroll
+                for (int h = 0; h < kStageLoads; ++h) {
+                    const int64_t e = e0 + 4 * h + sub;
+                    if (e < E) v[h] = IO[cell0 + ((int64_t)gs + e) * rs];
+                }
+#pragma unroll
+                for (int h = 0; h < kStageLoads; ++h) {
+                    const int64_t e = e0 + 4 * h + sub;
+                    if (e < E) {
+                        st_o[e * ns + d] = v[h].x;
+                        st_i[e * ns + d] = v[h].y;
+                    }
+                }
+            }
+        return;
+    }
+    double* Ro = ring[wv][0];
+    double* Ri = ring[wv][1];
+    const int rend = ghi + (int)E;
+    int done = 0;                                          // members [0, done) written
+    for (int r0 = glo; r0 < rend; r0 += kStageChunk) {
+        double2 v[kStageLoads];
+#pragma unroll
+        for (int h = 0; h < kStageLoads; ++h) {
+            const int r = r0 + 4 * h + sub, e = r - gs;
+            if (real && r < rend && e >= 0 && e < (int)E) v[h] = IO[cell0 + (int64_t)r * rs];
+        }
+#pragma unroll
+        for (int h = 0; h < kStageLoads; ++h) {
+            const int r = r0 + 4 * h + sub, e = r - gs;
+            if (real && r < rend && e >= 0 && e < (int)E) {
+                const int k = (e & (kStageRing - 1)) * kStageSlots + s;
+                Ro[k] = v[h].x;
+                Ri[k] = v[h].y;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int upto = min(min(r0 + kStageChunk, rend) - ghi, (int)E);
+        if (done < upto) {
+            for (int e0 = done; e0 < upto; e0 += 4) {
+                const int e = e0 + sub;
+                if (real && e < upto) {
+                    const int k = (e & (kStageRing - 1)) * kStageSlots + s;
+                    st_o[(int64_t)e * ns + d] = Ro[k];
+                    st_i[(int64_t)e * ns + d] = Ri[k];
+                }
+            }
+            done = upto;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 }  // namespace
 
 hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds, int* blocks_per_cu) {
@@ -801,6 +1030,11 @@ static dim3 member_grid(int64_t ns, int64_t E) {
 hipError_t launch_member_unpack(const double* IO, const MemberWin& mw, double* st_o,
                                 double* st_i, int64_t ns, int64_t E, hipStream_t s) {
     if (ns * E == 0) return hipSuccess;
+    if (mw.skew && MCR_STAGE_RING && mw.rs % kStageSlots == 0 && ns % kStageSlots == 0) {
+        hipLaunchKernelGGL(member_unpack_ring<>, dim3((unsigned)((ns / kStageSlots + 3) / 4)), 256,
+                           0, s, reinterpret_cast<const double2*>(IO), st_o, st_i, ns, E, mw);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(member_unpack, member_grid(ns, E), 256, 0, s,
                        reinterpret_cast<const double2*>(IO), st_o, st_i, ns, E, mw);
     return hipGetLastError();
@@ -820,6 +1054,16 @@ hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_r
                                 const PendingGain& gain) {
     if (ns * E == 0) return hipSuccess;
     if ((E + kMemberRun - 1) / kMemberRun > 65535) return hipErrorInvalidValue;
+    if (mw.skew && MCR_STAGE_RING && mw.rs % kStageSlots == 0 && ns % kStageSlots == 0) {
+        const dim3 grid((unsigned)((ns / kStageSlots + 3) / 4));
+        if (gain.G)
+            hipLaunchKernelGGL((member_inputs_ring<true>), grid, 256, 0, s, F, mF, ns, n_rows,
+                               ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+        else
+            hipLaunchKernelGGL((member_inputs_ring<false>), grid, 256, 0, s, F, mF, ns, n_rows,
+                               ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+        return hipGetLastError();
+    }
     constexpr int kGainRun = 4;
     if (gain.G) {
         if ((E + kGainRun - 1) / kGainRun > 65535) return hipErrorInvalidValue;

@@ -56,9 +56,15 @@ using dev::read_inputs;
 // DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
+#ifndef MCR_DET_WAVES
+#define MCR_DET_WAVES 2
+#endif
+#ifndef MCR_DET_BATCHQ
+#define MCR_DET_BATCHQ 1
+#endif
 template <int SLOTS, int K, bool DENSE>
 __global__ __launch_bounds__(SLOTS)
-__attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
+__attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : MCR_DET_WAVES, K >= 4 ? 1 : MCR_DET_WAVES)))
 void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int RS = K * SLOTS;
@@ -158,7 +164,7 @@ void wavefront_det(WaveArgs a) {
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
-    constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
+    constexpr bool kBatchQ = MCR_DET_BATCHQ && K <= 2;                    // lateral inflows per chunk (registers)
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         // this chunk's forcing rows -> the slots' LDS rows (private: no barrier needed)
