@@ -28,7 +28,10 @@ Prints ONE JSON line on rank 0 with
     move: outflows written, forcing / coefficients / state read, state written) and `dram`
     (rocprofv3 PMC bytes of THIS build, profiles/*_hbm_traffic*.json, source-hash checked);
   * `cpu_baseline`: the oracle's C transliteration of the reference loop (oracle/, test
-    infrastructure used only here) timed on this host, rank 0 at N = 1 only;
+    infrastructure used only here) timed on this host's cores, on rank 0 at any N (after the
+    timed region);
+  * `emulated_shards` (--enkf --emulate-shards N at N = 1): the configs[3] horizon as N member
+    shards on the one GPU, each shard's device time, and the projected N-GPU speed-up;
   * `api_ms_per_horizon` (det, N = 1): the drop-in `Muskingum.simulate` over the same horizon,
     host fetch of every step's outflows and inflows included.
 """
@@ -95,13 +98,24 @@ def parse(argv=None, world=None):
     ap.add_argument("--huc8", action="store_true",
                     help="BASELINE configs[0]: one HUC-8 sub-basin (1000 reaches, one outlet, "
                          "deepest path ~100 reaches), deterministic")
-    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow", "ensemble", "sweep"],
-                    help="execution path (mcroute.h mc_set_mode); 'ensemble': the whole horizon "
-                         "of every member as one dataflow launch")
+    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow"],
+                    help="execution path (mcroute.h mc_set_mode)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-api", action="store_true", help="skip the Muskingum.simulate timing")
     ap.add_argument("--timing-runs", type=int, default=3)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI, one GPU per "
+                         "rank; gloo: host-staged collectives, lets several ranks share one GPU "
+                         "in the tests)")
+    ap.add_argument("--emulate-shards", type=int, default=0,
+                    help="--enkf at N = 1: also run the configs[3] horizon as this many member "
+                         "shards on the one GPU (ensemble.emulated_analysis, the stage program "
+                         "of the N-rank run) and report each shard's device time per horizon "
+                         "and the projected N-GPU speed-up")
+    ap.add_argument("--xgmi-gbs", type=float, default=50.0,
+                    help="--emulate-shards: modelled per-peer, per-direction xGMI rate (GB/s) "
+                         "for the collectives the emulation does as device copies")
     args = ap.parse_args(argv)
     if world is None:
         world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,6 +187,10 @@ def measured_traffic(info, n, T, E=1):
         except (OSError, ValueError):
             continue
         if rec.get("workload") != want:
+            continue
+        if "launches_per_horizon" not in rec:
+            # written before hbm_traffic.py selected the bench horizons only (round 4's det
+            # profile averaged the drop-in API's launches in): never quoted
             continue
         if rec.get("source_hash") != h:
             stale = stale or os.path.relpath(f, ROOT)
@@ -407,6 +425,106 @@ def api_timing(wl, runs=2):
     return 1e3 * min(times)
 
 
+def emulated_shards(args, t1_ms):
+    """configs[3] as N member shards on ONE GPU: shard r is exactly rank r of the N-rank run (its
+    workload from build_workload(args, r, N): members r*E/N .., its own observation draws), the
+    member steps and forecast of each shard on one stream, the analyses through
+    ensemble.emulated_analysis (every mc_ens_* stage with nranks = N, the collectives as device
+    copies).  Reports each shard's device time per horizon (HIP events on that stream, the
+    collectives' copies excluded), the bytes each rank would move in the collectives, their time
+    at a modelled xGMI rate, and the projected N-GPU speed-up T(1 GPU) / T(rank)."""
+    import torch
+
+    from tx_fast_hydrology_amd import ensemble
+    N = args.emulate_shards
+    if args.members % N:
+        raise SystemExit("--emulate-shards must divide --members")
+    built = [build_workload(args, r, N) for r in range(N)]
+    nets = [b[0] for b in built]
+    wls = [b[1] for b in built]
+    ek0 = wls[0].enkf
+    x = wls[0].x
+    stream = torch.cuda.Stream()
+    sessions = nets + [w.enkf.fnet for w in wls if getattr(w.enkf, "fnet", None) is not None]
+    for s_ in sessions:
+        s_.set_stream(stream.cuda_stream)
+    ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
+    spans = []                                          # (shard, part, start, end)
+
+    def rec(r, part, fn):
+        a, b = ev(), ev()
+        a.record(stream)
+        fn()
+        b.record(stream)
+        spans.append((r, part, a, b))
+
+    def horizon(stage_ms):
+        for k in range(ek0.n_an):
+            for r in range(N):
+                rec(r, "member_steps", lambda r=r: nets[r].run(x[k:k + 1]))
+            with torch.cuda.stream(stream):
+                ensemble.emulated_analysis(nets, ek0.gauges,
+                                           [wls[r].enkf.Y[k] for r in range(N)], ek0.R,
+                                           stage_ms=stage_ms)
+        for r in range(N):
+            f = wls[r].enkf.fnet
+
+            def fc(r=r, f=f):
+                f.copy_state_from(nets[r])
+                f.run(x[ek0.n_an:])
+                nets[r].copy_state_from(f)
+            rec(r, "forecast", fc)
+
+    with torch.cuda.stream(stream):
+        horizon({})                                     # warm-up (plans, buffers)
+        stream.synchronize()
+        spans.clear()
+        reps = max(1, min(args.steps, 3))
+        stage_ms = {}
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            horizon(stage_ms)
+        stream.synchronize()
+        wall_ms = (time.perf_counter() - t0) * 1e3 / reps
+    per = [dict() for _ in range(N)]
+    for r, part, a, b in spans:
+        per[r][part] = per[r].get(part, 0.0) + a.elapsed_time(b) / reps
+    for name, vals in stage_ms.items():
+        if name.startswith("exchange"):
+            continue
+        for r in range(N):
+            per[r]["analysis: " + name] = per[r].get("analysis: " + name, 0.0) + vals[r] / reps
+    exch_copy_ms = sum(stage_ms.get("exchange (device copies)", [0.0])) / reps
+    shard_ms = [sum(p.values()) for p in per]
+    # bytes one rank sends per analysis (mc_ens_* layout): all-gather of HX and D (E x m each),
+    # the member -> slice all-to-all and the increments back (E x S each per peer)
+    E, m = wls[0].E, ek0.m
+    S = nets[0].slice_size(N)
+    ag = 2 * E * m * 8 * (N - 1)                        # each rank's blocks to N - 1 peers
+    a2a = 2 * E * S * 8 * (N - 1)                       # E x S doubles to each peer, twice
+    peers = min(N - 1, 7)                               # xGMI: one link per peer (7 per GPU)
+    lat_us = 25.0                                       # per collective (RCCL small-message)
+    model_ms = ek0.n_an * ((ag + a2a) / (peers * args.xgmi_gbs * 1e9) * 1e3 +
+                           3 * lat_us * 1e-3)
+    t_rank = max(shard_ms) + model_ms
+    for s_ in sessions:
+        s_.close()
+    return {"shards": N, "members_per_shard": E, "t1_ms_per_horizon": round(t1_ms, 3),
+            "shard_device_ms_per_horizon": [round(v, 3) for v in shard_ms],
+            "shard_breakdown_ms": {k: [round(p.get(k, 0.0), 3) for p in per]
+                                   for k in sorted(per[0])},
+            "emulation_wall_ms_per_horizon": round(wall_ms, 3),
+            "exchange_device_copies_ms_per_horizon": round(exch_copy_ms, 3),
+            "collective_bytes_per_rank_per_analysis": {"all_gather": ag, "all_to_all": a2a},
+            "collective_model": {"xgmi_gbs_per_peer": args.xgmi_gbs, "peers": peers,
+                                 "latency_us_per_collective": lat_us,
+                                 "ms_per_horizon": round(model_ms, 3),
+                                 "note": "not measured (one GPU): bytes / (peers x rate) + 3 "
+                                         "collective latencies per analysis, no overlap"},
+            "projected_rank_ms_per_horizon": round(t_rank, 3),
+            "projected_speedup": round(t1_ms / t_rank, 3)}
+
+
 def main():
     args = parse()
     what, world = launch_plan(args.gpus, os.environ)
@@ -421,8 +539,10 @@ def main():
         import datetime as _dt
 
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", timeout=_dt.timedelta(seconds=600))
+        # gloo (tests): several ranks may share one GPU
+        ndev = max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local if args.backend == "nccl" else local % ndev)
+        dist.init_process_group(args.backend, timeout=_dt.timedelta(seconds=600))
     else:
         torch.cuda.set_device(0)
 
@@ -438,7 +558,8 @@ def main():
     def max_over_ranks(v):
         if dist is None:
             return v
-        tt = torch.tensor([v], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([v], dtype=torch.float64,
+                          device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
 
@@ -498,7 +619,7 @@ def main():
     launches = max(tm["launches"], 1)
     launch_ms = tm["kernel_ms"] / launches
     path = net.mode()[1]
-    kernel = {"dataflow": "wavefront_flow", "sweep": "member_sweep"}.get(path, "wavefront_det")
+    kernel = "wavefront_flow" if path == "dataflow" else "wavefront_det"
     if wl.enkf is not None and len(nets) > 1:
         # member steps on the member-dataflow kernel, the forecast on the multi-launch kernel
         kernel = "wavefront_flow (member steps) + wavefront_det (forecast)"
@@ -563,10 +684,21 @@ def main():
     else:
         roofline["dram"] = {"source": None, "note": note}
 
-    # ---- CPU baseline (serial transliteration of the reference loop, rank 0 at N=1) --------
+    # ---- CPU baseline (transliteration of the reference loop, rank 0 at any N) --------------
+    # north_star: "timed on the node's own host cores in the same run"; at N > 1 the other ranks
+    # wait for rank 0 at the next barrier
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         cpu = cpu_baseline(args, wl, orc, E, x)
+    if world > 1:
+        barrier()
+
+    # ---- configs[3] as emulated member shards on this one GPU ---------------------------------
+    shards = None
+    if world == 1 and wl.enkf is not None and args.emulate_shards > 1:
+        for nt in nets:
+            nt.close()
+        shards = emulated_shards(args, elapsed / args.steps * 1e3)
 
     # ---- the drop-in API over the same horizon (det, N = 1) ---------------------------------
     api_ms = None
@@ -634,6 +766,8 @@ def main():
                                 "iterated (host outflows and inflows of each step)")
         if det_rep is not None:
             line["det_replicas"] = det_rep
+        if shards is not None:
+            line["emulated_shards"] = shards
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

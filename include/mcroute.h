@@ -259,12 +259,8 @@ int mc_reset_timing(void* net);
 
 /* Execution path of mc_run / mc_step.  mode 0 (default): one resident dataflow launch for the
  * whole horizon when the network fits the device at once, else launches of `tile` ticks;
- * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit);
- * 3: auto + ensemble-dataflow horizons; 4: member sweep for every ensemble horizon (the members
- * on the lanes of a member plan of its own, sweep.hpp; MC_E_STATE when a horizon cannot run as
- * one: one member or one step, an odd ensemble, forcing rows too dense for the step -- 8
- * consecutive steps touching more than 3 rows or starting 2 rows apart -- or no member plan).
- * last_path: 1 launches, 2 dataflow, 3 member sweep (0 before any run). */
+ * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit).
+ * last_path: 1 launches, 2 dataflow (0 before any run). */
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);
 

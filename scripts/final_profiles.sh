@@ -14,7 +14,7 @@ BENCH_ARGS="--conus" bash scripts/gpu_pmc.sh ${TAG}_conus FETCH_SIZE WRITE_SIZE 
 stats() {   # name, bench args
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$O/prof_$name" \
-      -o run -- python3 "$PWD/bench.py" --no-cpu --timing-runs 1 "$@" > $O/prof_$name.log 2>&1
+      -o run -- python3 "$PWD/bench.py" --no-cpu --no-api --timing-runs 1 "$@" > $O/prof_$name.log 2>&1
   local rc=$?
   echo "stats $name rc=$rc"
   [ $rc -ne 0 ] && { tail -5 $O/prof_$name.log; exit $rc; }

@@ -111,11 +111,7 @@ def main():
         gmin, gmax = wg_windows(plan)
         summarize_flow(rec, khz, gmin, gmax, len(wl.x))
     else:
-        # the member sweep launches tiles of its own plan (sweep.hpp kSweepTile; variant builds:
-        # SWEEP_TILE)
-        tile = (int(os.environ.get("SWEEP_TILE", "32")) if net.mode()[1] == "sweep"
-                else net.info["tile"])
-        summarize(rec, khz, tile, quiet)
+        summarize(rec, khz, net.info["tile"], quiet)
 
 
 if __name__ == "__main__":

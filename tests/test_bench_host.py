@@ -88,13 +88,18 @@ def test_measured_traffic_matches_the_exact_workload_and_build(tmp_path, monkeyp
     prof = tmp_path / "profiles"
     prof.mkdir()
     det = {"workload": {"slots": 192, "tile": 16, "n": 190000, "T": 288},
-           "traffic_bytes_per_launch": 7.0e8, "source_hash": h}
+           "traffic_bytes_per_launch": 7.0e8, "source_hash": h, "launches_per_horizon": 1}
     ens = {"workload": {"slots": 256, "tile": 64, "n": 190000, "T": 288, "E": 64},
-           "traffic_bytes_per_launch": 2.1e9, "source_hash": h}
+           "traffic_bytes_per_launch": 2.1e9, "source_hash": h, "launches_per_horizon": 23}
     old = {"workload": {"slots": 384, "tile": 32, "n": 190000, "T": 288},
-           "traffic_bytes_per_launch": 6.9e8, "source_hash": h}
+           "traffic_bytes_per_launch": 6.9e8, "source_hash": h, "launches_per_horizon": 1}
     stale = {"workload": {"slots": 192, "tile": 16, "n": 190000, "T": 288},
-             "traffic_bytes_per_launch": 9.9e8, "source_hash": "0" * 16}
+             "traffic_bytes_per_launch": 9.9e8, "source_hash": "0" * 16,
+             "launches_per_horizon": 1}
+    # a profile of this build written before the bench-horizon selection: never quoted
+    mixed = {"workload": {"slots": 192, "tile": 16, "n": 190000, "T": 288},
+             "traffic_bytes_per_launch": 4.9e8, "source_hash": h}
+    (prof / "r01e_hbm_traffic.json").write_text(json.dumps(mixed))
     (prof / "r01a_hbm_traffic.json").write_text(json.dumps(old))
     (prof / "r01b_hbm_traffic.json").write_text(json.dumps(det))
     (prof / "r01b_hbm_traffic_ens64.json").write_text(json.dumps(ens))

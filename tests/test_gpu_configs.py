@@ -51,17 +51,15 @@ def test_config0_huc8_bench_plan():
     net.close()
 
 
-@pytest.mark.parametrize("mode", ["sweep", "launches"])
-def test_config2_texas_ens64_bench_plan(mode):
-    """The bench's ens64 horizon on both ensemble paths: the member sweep (sweep.hip) and the
-    multi-launch kernel on the 256-lane / 64-tick plan (auto)."""
-    args = bench.parse(["--members", "64", "--mode", mode], world=1)
+def test_config2_texas_ens64_bench_plan():
+    """The bench's ens64 horizon: the multi-launch kernel on the 256-lane / 64-tick plan."""
+    args = bench.parse(["--members", "64"], world=1)
     net, wl = bench.build_workload(args)
     assert net.info["slots"] == 256 and net.info["tile"] == 64 and wl.E == 64
     n, T = wl.n, wl.x.size
     assert (n, T) == (190_000, 288)
     net.run(wl.x)
-    assert net.mode()[1] == mode
+    assert net.mode()[1] == "launches"
     so, si = net.get_state()
     fo, fi = orc.simulate_members(wl.start, wl.end, wl.indeg, *_coef(wl), wl.o0, wl.i0, wl.x,
                                   wl.xp, wl.fp, threads=THREADS)

@@ -99,17 +99,20 @@ def test_enkf_extreme_shapes_vs_numpy(E, m):
         np.testing.assert_allclose(i[:, e] - I0[:, e], ig, rtol=0, atol=1e-8 * scale)
 
 
+def _same(a, b):
+    """bit-equal arrays, NaN where the other has NaN (float64 cells)"""
+    return np.array_equal(a, b, equal_nan=True)
+
+
 @pytest.mark.parametrize("mode", ["launches", "auto"])
-def test_non_finite_inputs_documented_behaviour(mode):
-    """Non-finite inputs are outside the bit-exact contract (mcroute.h header): the kernels
-    evaluate a clamped forcing step as (1 - 0) f + 0 f and give unrouted reaches zero
-    coefficients, so where the reference (nutils.py:24-27 row copy, :68 fresh zeros) yields
-    +-Inf or keeps o = 0, the device yields NaN.  Pinned here: every cell the reference computes
-    finite is bit-identical on the device except the outflows of unrouted reaches with
-    non-finite inputs (NaN instead of 0); every cell the reference computes non-finite is
-    non-finite on the device (NaN where the reference has +-Inf)."""
-    # 0 -> 1 <-> 2 (cycle: 1 and 2 are never processed), 6 -> 1, 3, 4 -> 5 (outlet), 7 -> 3
-    end = np.array([1, 2, 1, 5, 5, 5, 1, 3], dtype=np.int64)
+def test_non_finite_inputs_match_reference(mode):
+    """Non-finite inputs route exactly as the reference routes them: a step outside the forcing
+    index copies the clamped row (nutils.py:24-27, so +-Inf stays +-Inf instead of (1 - 0) f +
+    0 f = NaN), and a never-processed reach keeps o = 0 (nutils.py:68) whatever its state and
+    forcing hold.  Every cell equals the oracle's, +-Inf and NaN included."""
+    # 0 -> 1 <-> 2 (cycle: 1 and 2 are never processed), 6 -> 1, 3, 4 -> 5 (outlet), 7 -> 3,
+    # 8..13 -> 5: eight upstreams, so 5's inflow fold runs through partial-sum nodes
+    end = np.array([1, 2, 1, 5, 5, 5, 1, 3] + [5] * 6, dtype=np.int64)
     n = end.size
     start = np.arange(n, dtype=np.int64)
     indeg = orc.compute_indegree(start, end)
@@ -124,8 +127,12 @@ def test_non_finite_inputs_documented_behaviour(mode):
     fp = np.full((4, n), 0.5)
     fp[1, 1] = np.nan                                # unrouted reach forcing
     fp[3, 7] = np.inf                                # last row: clamped steps copy it
+    fp[0, 4] = -np.inf                               # first row, interpolated from step 1
+    fp[1, 9] = np.inf                                # into the partial sums of reach 5
+    fp[2, 12] = -np.inf                              # ... and later Inf - Inf = NaN
     x = xp[0] + 300e9 * np.arange(1, 61)             # 60 steps: the last 24 beyond xp[-1]
-    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    want_o, want_i, want_so, want_si = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    assert np.isinf(want_o[-1, 7]) and (want_o[:, 1] == 0).all()
     net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16)
     net.set_mode(mode)
     net.set_coeffs(*coef)
@@ -133,15 +140,16 @@ def test_non_finite_inputs_documented_behaviour(mode):
     net.load_forcing(xp, fp)
     net.run(x)
     got_o, got_i = net.fetch_outputs()
-    unrouted = np.zeros(n, bool)
-    unrouted[[1, 2]] = True
-    for got, want, is_o in ((got_o, want_o, True), (got_i, want_i, False)):
-        fin = np.isfinite(want)
-        cell_ok = got == want
-        if is_o:            # documented: unrouted outflows may be NaN where the reference has 0
-            cell_ok |= unrouted[None, :] & np.isnan(got) & (want == 0)
-        assert cell_ok[fin].all()
-        assert (~np.isfinite(got[~fin])).all()
-    assert np.isinf(want_o[-1, 7]) and np.isnan(got_o[-1, 7])     # the clamped Inf row
-    assert (want_o[:, 1] == 0).all() and np.isnan(got_o[-1, 1])    # unrouted, NaN forcing
+    assert _same(got_o, want_o) and _same(got_i, want_i)
+    so, si = net.get_state()
+    assert _same(so, want_so) and _same(si, want_si)
+    # the reach-major fetch, and one step at a time (mc_step: the forcing row is q itself)
+    O, I = net.fetch_series()
+    assert _same(O, want_o.T) and _same(I, want_i.T)
+    net.set_state(o0, i0)
+    q = np.array([0.5, np.nan, 0.5, np.inf, 0.5, -np.inf, 0.5, np.inf] + [0.25] * 6)
+    q[11] = np.inf
+    i1, o1 = net.step(q)
+    wi, wo = orc.ax_bu(heads, end, *coef, i0, o0, q, indeg)
+    assert _same(o1, wo) and _same(i1, wi)
     net.close()

@@ -44,7 +44,7 @@ def test_ensemble_members_bitexact(n, E, slots, T, chain):
     n = end.size
     x = xp[0] + 300e9 * np.arange(1, T + 1)
     net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=E, chain=chain)
-    net.set_mode("launches")             # (auto takes the member sweep from 32 members)
+    net.set_mode("launches")
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
     got_o, got_i = net.simulate(x, xp, fpe)
@@ -237,184 +237,3 @@ def test_conus_scale_ensemble_members_bitexact():
                                     np.ascontiguousarray(fpe[:, :, e]), keep_outputs=False)
         assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
         assert np.array_equal(last_o[0, :, e], fo) and np.array_equal(last_i[0, :, e], fi), e
-
-
-@pytest.mark.parametrize("n,E,slots,tile,T,chain", [(3000, 5, 192, 16, 60, 2),
-                                                    (6000, 16, 192, 16, 97, 2),
-                                                    (1200, 64, 128, 32, 25, 2),
-                                                    (2500, 3, 64, 16, 40, 3)])
-def test_ensemble_dataflow_horizon_bitexact(n, E, slots, tile, T, chain):
-    """Ensemble dataflow (mode "ensemble"): the whole horizon of every member in ONE launch whose
-    (workgroup, member) instances take tickets in topological order -- every member bit-identical
-    to its serial oracle run, and to the multi-launch path; a second horizon continues from the
-    state the first left."""
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4, 150, 7 * n + E, E)
-    n = end.size
-    x = xp[0] + 300e9 * np.arange(1, T + 1)
-    x2 = x[-1] + 300e9 * np.arange(1, 9)
-    res = {}
-    for mode in ("ensemble", "launches"):
-        net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile, members=E,
-                                chain=chain)
-        net.set_mode(mode)
-        net.set_coeffs(*coef)
-        net.set_state(o0, i0)
-        got_o, got_i = net.simulate(x, xp, fpe)
-        path = net.mode()[1]
-        net.run(x2)
-        o2, i2 = net.fetch_outputs()
-        res[mode] = (got_o, got_i, o2, i2, net.get_state(), path)
-        net.close()
-    assert res["ensemble"][5] == "dataflow" and res["launches"][5] == "launches"
-    for a, b in zip(res["ensemble"][:4], res["launches"][:4]):
-        assert np.array_equal(a, b)
-    assert np.array_equal(res["ensemble"][4][0], res["launches"][4][0])
-    assert np.array_equal(res["ensemble"][4][1], res["launches"][4][1])
-    got_o, got_i = res["ensemble"][:2]
-    for e in range(E):
-        want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
-                                            np.ascontiguousarray(fpe[:, :, e]))
-        assert np.array_equal(got_o[:, :, e], want_o), e
-        assert np.array_equal(got_i[:, :, e], want_i), e
-
-
-def test_ensemble_dataflow_give_up_reroutes():
-    """Patience < 0 (give up at the first stale upstream value): a horizon whose wait gave up is
-    re-routed with launches at the next synchronising call, else it completes as dataflow (the
-    ticket order makes waits rare: producers took earlier tickets) -- bit-exact either way."""
-    E, T = 16, 97
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(6000, 4, 150, 7 * 6000 + E, E)
-    x = xp[0] + 300e9 * np.arange(1, T + 1)
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=192, tile=16, members=E)
-    net.set_mode("ensemble")
-    net.set_coeffs(*coef)
-    net.set_state(o0, i0)
-    net.set_flow_patience(-1)
-    got_o, _ = net.simulate(x, xp, fpe)
-    assert net.mode()[1] == ("launches" if net.reroutes() else "dataflow")
-    for e in (0, E - 1):
-        want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
-                                       np.ascontiguousarray(fpe[:, :, e]))
-        assert np.array_equal(got_o[:, :, e], want_o), e
-    net.close()
-
-
-def test_ensemble_dataflow_needs_an_acyclic_workgroup_graph():
-    """The ticket order is a topological order of the workgroup graph; a plan whose workgroups
-    feed each other both ways (this network, 192 lanes) routes its ensemble horizons with
-    launches instead -- still bit-exact."""
-    E, T = 8, 48
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(20000, 6, 600, 5, E)
-    x = xp[0] + 300e9 * np.arange(1, T + 1)
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=192, tile=16, members=E)
-    net.set_mode("ensemble")
-    net.set_coeffs(*coef)
-    net.set_state(o0, i0)
-    got_o, _ = net.simulate(x, xp, fpe)
-    assert net.mode()[1] == "launches"
-    for e in (0, E - 1):
-        want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
-                                       np.ascontiguousarray(fpe[:, :, e]))
-        assert np.array_equal(got_o[:, :, e], want_o), e
-    net.close()
-
-
-@pytest.mark.parametrize("n,E,T,rows,mode", [(3000, 64, 60, 7, "sweep"), (2500, 40, 45, 5, "sweep"),
-                                             (1500, 130, 33, 4, "sweep"),
-                                             (4000, 32, 100, 10, "sweep")])
-def test_member_sweep_bitexact(n, E, T, rows, mode):
-    """Member sweep (sweep.hip: the members on the lanes of a member plan of its own): every
-    member bit-identical to its serial oracle run -- step outputs and inflows, series, final
-    state -- for a full member group (64), a partial one (40: lanes beyond E idle), three groups
-    (130) and horizons that are not a multiple of the 8-tick chunk; continued over two horizons
-    (the state hand-over through the session layout) and on with the multi-launch path."""
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4, 120, n + E, E, rows=rows)
-    n = end.size
-    x = xp[0] + 300e9 * np.arange(1, T + 1)
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
-    net.set_mode(mode)
-    net.set_coeffs(*coef)
-    net.set_state(o0, i0)
-    net.load_forcing(xp, fpe)
-    cut = T // 3
-    net.run(x[:cut])
-    assert net.mode()[1] == "sweep"
-    a_o, a_i = net.fetch_outputs(0, cut)
-    net.run(x[cut:])
-    assert net.mode()[1] == "sweep"
-    b_o, b_i = net.fetch_outputs(0, T - cut)
-    ser_o, ser_i = net.fetch_series()
-    so, si = net.get_state()
-    net.set_mode("launches")            # the session state after a sweep continues elsewhere
-    net.run(x[-3:] + 600e9)
-    c_o, _ = net.fetch_outputs(0, 3)
-    for e in range(E):
-        fe = np.ascontiguousarray(fpe[:, :, e])
-        want_o, want_i, fo, fi = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x,
-                                              xp, fe)
-        assert np.array_equal(a_o[:, :, e], want_o[:cut]), e
-        assert np.array_equal(a_i[:, :, e], want_i[:cut]), e
-        assert np.array_equal(b_o[:, :, e], want_o[cut:]), e
-        assert np.array_equal(b_i[:, :, e], want_i[cut:]), e
-        assert np.array_equal(ser_o[:, :, e], want_o[cut:].T), e
-        assert np.array_equal(ser_i[:, :, e], want_i[cut:].T), e
-        assert np.array_equal(so[:, e], fo) and np.array_equal(si[:, e], fi), e
-        w3, _, _, _ = orc.simulate(start, end, indeg, *coef, fo, fi, x[-3:] + 600e9, xp, fe)
-        assert np.array_equal(c_o[:, :, e], w3), e
-    net.close()
-
-
-@pytest.mark.parametrize("dt_s,sweeps", [(3600.0, True), (7200.0, False)])
-def test_member_sweep_forcing_row_steps(dt_s, sweeps):
-    """A step as long as the forcing interval advances one row per step: the sweep's row-pair
-    registers follow it (bit-exact).  A longer step skips rows: other modes route it with
-    launches, sweep mode refuses it."""
-    E, T = 32, 20
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 9, E, rows=50)
-    x = xp[0] + dt_s * 1e9 * np.arange(1, T + 1)
-    if sweeps:
-        net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
-        net.set_mode("sweep")
-        net.set_coeffs(*coef)
-        net.set_state(o0, i0)
-        net.load_forcing(xp, fpe)
-        net.run(x)
-        assert net.mode()[1] == "sweep"
-        got_o, got_i = net.fetch_outputs(0, T)
-        for e in (0, 17, E - 1):
-            want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e],
-                                                x, xp, np.ascontiguousarray(fpe[:, :, e]))
-            assert np.array_equal(got_o[:, :, e], want_o), e
-            assert np.array_equal(got_i[:, :, e], want_i), e
-        net.close()
-        return
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
-    net.set_coeffs(*coef)
-    net.set_state(o0, i0)
-    net.load_forcing(xp, fpe)
-    net.run(x)
-    assert net.mode()[1] == "launches"
-    got_o, _ = net.fetch_outputs(0, T)
-    e = 5
-    want_o, _, _, _ = orc.simulate(start, end, indeg, *coef, o0[:, e], i0[:, e], x, xp,
-                                   np.ascontiguousarray(fpe[:, :, e]))
-    assert np.array_equal(got_o[:, :, e], want_o)
-    net.set_mode("sweep")
-    with pytest.raises(engine.nat.RoutingError):
-        net.run(x)
-    net.close()
-
-
-def test_member_sweep_needs_an_even_ensemble():
-    """An odd ensemble (the store wave copies two members per lane) is refused in sweep mode."""
-    E, T = 33, 20
-    end, start, indeg, coef, xp, fpe, o0, i0 = _case(1500, 3, 60, 11, E)
-    x = xp[0] + 300e9 * np.arange(1, T + 1)
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], members=E)
-    net.set_coeffs(*coef)
-    net.set_state(o0, i0)
-    net.load_forcing(xp, fpe)
-    net.set_mode("sweep")
-    with pytest.raises(engine.nat.RoutingError):
-        net.run(x)
-    net.close()

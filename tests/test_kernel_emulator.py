@@ -87,10 +87,9 @@ def test_emulator_river_network_and_golden_edges(golden, chain):
 
 @pytest.mark.parametrize("slots,chain,tile", [(8, 4, 16), (8, 4, 32), (4, 4, 16), (32, 1, 32)])
 def test_emulator_member_plans(slots, chain, tile):
-    """The member sweep's plans (sweep.hpp: a "lane" is a wave of members, so a workgroup has
-    8 or 4 lanes of 4 positions, or 32 lanes of one): the same launch / tick protocol on them
-    reproduces the oracle (chained positions within a tick, cross-workgroup inputs from earlier
-    launches, partial sums)."""
+    """Narrow plans (8 or 4 lanes of 4 positions, or 32 lanes of one): the same launch / tick
+    protocol on them reproduces the oracle (chained positions within a tick, cross-workgroup
+    inputs from earlier launches, partial sums)."""
     rng = np.random.default_rng(slots * 100 + tile)
     end = synthetic.random_forest(2500, 6, rng, p_chain=0.9)
     n = end.size

@@ -27,7 +27,6 @@
 #include "digest.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
-#include "sweep.hpp"
 
 #pragma clang fp contract(off)
 
@@ -192,34 +191,6 @@ struct Net {
     // outputs of the last run are the {o, i} pairs of a member-dataflow step (IOb, member windows)
     bool out_io = false;
 
-    // ---- member sweep (sweep.hip): ensemble horizons with the members on the lanes, on a member
-    // plan of its own (kSweepSlots slots per workgroup, chain 1), built on first use
-    std::vector<int64_t> topo_end, topo_deg, topo_heads;
-    struct Sweep {
-        mcr::Plan plan;
-        DBuf<int32_t> G, ext_off, ext_slot, ext_g, mmap, rmap, wg_gmin, wg_gmax;
-        DBuf<uint8_t> flags, up_cnt;
-        DBuf<uint64_t> up4;
-        DBuf<double> coef, So, Si, F, O;
-        DBuf<int64_t> jbase;           // caller reach -> member-plan slot * E (fetches)
-        int64_t jbase_E = 0, f_E = 0, f_rows = 0;
-        uint64_t coef_ver = 0, f_ver = 0;   // versions of the session arrays these came from
-        struct Sch {
-            int64_t T = -1;
-            std::vector<int64_t> off;
-            std::vector<int32_t> list;
-            DBuf<int32_t> active;
-            uint64_t used = 0;
-        };
-        std::vector<std::unique_ptr<Sch>> scheds;
-    };
-    std::unique_ptr<Sweep> sw;
-    int sweep_state = 0;             // 1 built, -1 the network has no member plan the kernel takes
-    uint64_t coef_ver = 1, f_ver = 1;   // bumped by set_coeffs / load_forcing / corrections
-    bool out_sweep = false;          // the outputs of the last run are in sw->O
-    // auto mode takes the sweep from this many members (below it the lanes are mostly idle);
-    // 0: auto never takes it (opt-in, mode 4) while it is slower than the multi-launch kernel
-    static constexpr int64_t kSweepMinMembers = 0;
     // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
     DBuf<int64_t> mwbase;
     int64_t mw_E = 0, mw_cells = 0;
@@ -303,11 +274,8 @@ struct Net {
               int64_t n_head, const mcr::PlanParams& p) {
         const std::string err = mcr::build_plan(n, endnodes, indegree, heads, n_head, p, plan);
         if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
-        topo_end.assign(endnodes, endnodes + n);
-        topo_deg.assign(indegree, indegree + n);
-        topo_heads.assign(heads, heads + n_head);
         if (plan.p.tile % mcr::kChunk != 0)
-            throw Fail(MC_E_INVALID, "tile must be a multiple of 16 for the device sweep");
+            throw Fail(MC_E_INVALID, "tile must be a multiple of 8 (the kernels' tick chunk)");
         if (!mcr::wavefront_shape_ok(plan.p.slots, plan.p.chain))
             throw Fail(MC_E_INVALID, "no device kernel for this (slots, chain): chain 1 takes "
                                      "slots 64, chain 2 slots 64..512 (multiples of 64 up to "
@@ -459,67 +427,6 @@ struct Net {
         return ok;
     }
 
-    // Topological order of the workgroup graph (an edge per cross-cluster input: producer's
-    // workgroup -> consumer's), the ticket order of the ensemble dataflow (WaveArgs::order);
-    // 1 = built, -1 = the graph has a cycle (the ensemble dataflow is not used), 0 = not yet.
-    DBuf<int32_t> topo, qctr;
-    int topo_state = 0;
-    bool topo_ready() {
-        if (topo_state != 0) return topo_state > 0;
-        const int32_t W = plan.nwg;
-        const int RS = row_width();
-        std::vector<std::vector<int32_t>> adj(W);
-        std::vector<int32_t> indeg(W, 0);
-        for (int32_t c = 0; c < W; ++c)
-            for (int32_t e = plan.ext_off[c]; e < plan.ext_off[c + 1]; ++e) {
-                const int64_t src = plan.ext_src[e];
-                const int64_t slot = src < plan.n ? plan.pos[src] : src - plan.n;
-                const int32_t pw = (int32_t)(slot / RS);
-                if (pw == c) continue;
-                adj[pw].push_back(c);
-            }
-        for (auto& v : adj) {
-            std::sort(v.begin(), v.end());
-            v.erase(std::unique(v.begin(), v.end()), v.end());
-            for (int32_t c : v) ++indeg[c];
-        }
-        std::vector<int32_t> order;
-        order.reserve(W);
-        for (int32_t w = 0; w < W; ++w)
-            if (indeg[w] == 0) order.push_back(w);
-        for (size_t k = 0; k < order.size(); ++k)
-            for (int32_t c : adj[order[k]])
-                if (--indeg[c] == 0) order.push_back(c);
-        if ((int32_t)order.size() != W) {
-            topo_state = -1;
-            return false;
-        }
-        topo.upload(order.data(), order.size(), stream);
-        topo_state = 1;
-        return true;
-    }
-
-    // Can a T-step horizon of all E members run as ONE ensemble-dataflow launch?  Its
-    // (workgroup, member) instances take tickets in topological order, so they need not be
-    // resident together (mode 3 opts in; mcroute.h mc_set_mode).
-    bool ens_flow_fits(int64_t T, bool dense, size_t& lds) {
-        if (mode != 3 || force_mode == 1 || E < 2 || T < 2) return false;
-        const int S = plan.p.slots, Kc = plan.p.chain;
-        lds = mcr::flow_lds_bytes(S, Kc, (int)T, plan.max_ext_wg);
-        const size_t xgm = plan.ext_src.size() * (size_t)T * 16;
-        bool ok = mcr::flow_shape_ok(S, Kc) && plan.p.tile >= mcr::kFlowMinSlack &&
-                  plan.max_ext_wg <= mcr::kFlowMaxExt && T <= mcr::kFlowMaxT &&
-                  xgm < (size_t(1) << 31) && lds <= 160 * 1024 &&
-                  (int64_t)plan.nwg * E < (1ll << 31) && topo_ready();
-        if (ok) {
-            int bpc = 0;
-            HIPC(mcr::flow_occupancy(S, Kc, dense, lds, &bpc));
-            ok = bpc >= 1;
-        }
-        return ok;
-    }
-
-    // Can one step of all E members run as one member-dataflow launch?
     bool members_fit(size_t& lds) {
         if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
@@ -856,7 +763,6 @@ struct Net {
                                          stream));
         sync();  // `stage` is reused by the next call
         coeffs_set = true;
-        ++coef_ver;
     }
 
     void set_state(const double* o, const double* i) {
@@ -895,8 +801,8 @@ struct Net {
             hit->wbase.upload(wb.data(), wb.size(), stream);
             hit->Otot = total;
             hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
-            HIPC(mcr::launch_window_index(pos.p, G.p, wg_gmin.p, hit->wbase.p, row_width(),
-                                          plan.n, hit->jbase.p, stream));
+            HIPC(mcr::launch_window_index(pos.p, G.p, flags.p, wg_gmin.p, hit->wbase.p,
+                                          row_width(), plan.n, hit->jbase.p, stream));
             sync();
         }
         hit->used = ++use_clock;
@@ -913,183 +819,6 @@ struct Net {
         }
     }
 
-    // ---- member sweep ----------------------------------------------------------------------
-    bool ensure_sweep() {
-        if (sweep_state != 0) return sweep_state > 0;
-        sweep_state = -1;
-        auto S = std::make_unique<Sweep>();
-        mcr::PlanParams pp;
-        pp.slots = mcr::kSweepNW;          // a plan "lane" is a compute wave of members
-        pp.tile = mcr::kSweepTile;
-        pp.ext_cap = 4;
-        pp.chain = mcr::kSweepNPW;
-        const std::string err =
-            mcr::build_plan(plan.n, topo_end.data(), topo_deg.data(), topo_heads.data(),
-                            (int64_t)topo_heads.size(), pp, S->plan);
-        const mcr::Plan& P = S->plan;
-        if (!err.empty() || P.max_ext_wg > mcr::kSweepMaxExt ||
-            P.p.tile + mcr::kChunk + 1 + P.max_span > mcr::kSweepTabCap ||
-            P.nslots >= ((int64_t)1 << 31) / 8)
-            return false;
-        const size_t ns = (size_t)P.nslots;
-        S->G.upload(P.G.data(), ns, stream);
-        S->flags.upload(P.flags.data(), ns, stream);
-        S->up_cnt.upload(P.up_cnt.data(), ns, stream);
-        S->up4.upload(P.up4.data(), ns, stream);
-        S->ext_off.upload(P.ext_off.data(), P.ext_off.size(), stream);
-        S->wg_gmin.upload(P.wg_gmin.data(), P.wg_gmin.size(), stream);
-        S->wg_gmax.upload(P.wg_gmax.data(), P.wg_gmax.size(), stream);
-        std::vector<int32_t> xs(std::max<size_t>(P.ext_src.size(), 1), 0);
-        for (size_t x = 0; x < P.ext_src.size(); ++x) {
-            const int64_t src = P.ext_src[x];
-            xs[x] = (int32_t)(src < P.n ? P.pos[src] : src - P.n);
-        }
-        S->ext_slot.upload(xs.data(), xs.size(), stream);
-        S->ext_g.upload(P.ext_g.data(), std::max<size_t>(P.ext_g.size(), 1), stream);
-        std::vector<int32_t> mm((size_t)std::max<int64_t>(plan.nslots, 1), -1);
-        for (int64_t d = 0; d < plan.nslots; ++d)
-            if (plan.slot_reach[d] >= 0) mm[d] = (int32_t)P.pos[plan.slot_reach[d]];
-        S->mmap.upload(mm.data(), mm.size(), stream);
-        std::vector<int32_t> rm(std::max<size_t>(ns, 1), -1);
-        for (size_t d = 0; d < ns; ++d)
-            if (P.slot_reach[d] >= 0) rm[d] = (int32_t)plan.pos[P.slot_reach[d]];
-        S->rmap.upload(rm.data(), rm.size(), stream);
-        S->coef.reserve(4 * ns);
-        sync();
-        sw = std::move(S);
-        sweep_state = 1;
-        return true;
-    }
-
-    // Can this horizon run as a member sweep?
-    bool sweep_fits(int64_t T, const double* Fsrc, const std::vector<int4>& tab) {
-        if (mode == 1 || mode == 2 || mode == 3 || force_mode == 1) return false;
-        const bool want = mode == 4 || (kSweepMinMembers > 0 && E >= kSweepMinMembers);
-        // (E even: the store wave copies two members per lane)
-        if (!want || E < 2 || E % 2 || T < 2 || Fsrc != F.p) return false;
-        // row pairs {r, r} or {r, r + 1}; from one step to the next each row advances by at most
-        // one (sweep.hip keeps the pair's rows and the next one in registers)
-        for (int64_t t = 0; t < T; ++t) {
-            if (tab[t].y != tab[t].x && tab[t].y != tab[t].x + 1) return false;
-            if (t > 0 && (tab[t].x - tab[t - 1].x > 1 || tab[t].y - tab[t - 1].y > 1 ||
-                          tab[t].x < tab[t - 1].x))
-                return false;
-        }
-        if (!ensure_sweep()) return false;
-        return sw->plan.nslots * E * 8 < ((int64_t)1 << 31) && T < (1 << 28);
-    }
-
-    void run_sweep(int64_t T, int64_t rows) {
-        Sweep& S = *sw;
-        const mcr::Plan& P = S.plan;
-        const int64_t ns = P.nslots, nsm = plan.nslots;
-        if (S.coef_ver != coef_ver) {
-            HIPC(mcr::launch_sweep_coeffs(alpha.p, beta.p, chi.p, gamma.p, S.rmap.p, S.flags.p,
-                                          S.coef.p, ns, stream));
-            S.coef_ver = coef_ver;
-        }
-        if (S.f_ver != f_ver || S.f_E != E || S.f_rows != rows) {
-            // forcing in member-plan order (slots without a reach read 0)
-            const size_t cells = (size_t)(rows * ns * E);
-            S.F.reserve(cells);
-            HIPC(hipMemsetAsync(S.F.p, 0, cells * sizeof(double), stream));
-            HIPC(mcr::launch_to_sweep(F.p, rows * nsm, nsm, rows, S.mmap.p, S.F.p, ns, E, stream));
-            S.f_ver = f_ver;
-            S.f_E = E;
-            S.f_rows = rows;
-        }
-        if (S.jbase_E != E) {
-            std::vector<int64_t> jb((size_t)std::max<int64_t>(plan.n, 1), 0);
-            for (int64_t j = 0; j < plan.n; ++j) jb[j] = P.pos[j] * E;
-            S.jbase.upload(jb.data(), jb.size(), stream);
-            S.jbase_E = E;
-        }
-        S.So.reserve((size_t)(ns * E));
-        S.Si.reserve((size_t)(ns * E));
-        S.O.reserve((size_t)(T * ns * E) + 128);   // (the loader's 16-B reads run past E)
-        HIPC(mcr::launch_sweep_zero_free(S.rmap.p, S.So.p, S.Si.p, ns, E, stream));
-        HIPC(mcr::launch_to_sweep(st_o.p, nsm, nsm, 1, S.mmap.p, S.So.p, ns, E, stream));
-        HIPC(mcr::launch_to_sweep(st_i.p, nsm, nsm, 1, S.mmap.p, S.Si.p, ns, E, stream));
-        // active workgroups of each launch, cached per horizon length
-        Sweep::Sch* sc = nullptr;
-        for (auto& c : S.scheds)
-            if (c->T == T) sc = c.get();
-        if (!sc) {
-            if (S.scheds.size() >= 4) S.scheds.erase(S.scheds.begin());
-            S.scheds.push_back(std::make_unique<Sweep::Sch>());
-            sc = S.scheds.back().get();
-            sc->T = T;
-            mcr::active_schedule(P, T, sc->list, sc->off);
-            sc->active.upload(sc->list.data(), std::max<size_t>(sc->list.size(), 1), stream);
-        }
-        mcr::SweepArgs a{};
-        a.wg_gmin = S.wg_gmin.p;
-        a.wg_gmax = S.wg_gmax.p;
-        a.G = S.G.p;
-        a.flags = S.flags.p;
-        a.up_cnt = S.up_cnt.p;
-        a.up4 = S.up4.p;
-        a.ext_off = S.ext_off.p;
-        a.ext_slot = S.ext_slot.p;
-        a.ext_g = S.ext_g.p;
-        a.coef = S.coef.p;
-        a.So = S.So.p;
-        a.Si = S.Si.p;
-        a.F = S.F.p;
-        a.stab = stab.p;
-        a.O = S.O.p;
-        a.rowB = (uint32_t)(ns * E * 8);
-        a.E = (int32_t)E;
-        a.T = (int32_t)T;
-        a.n_rows = (int32_t)rows;
-        a.tile = P.p.tile;
-        const int64_t nl = (int64_t)sc->off.size() - 1;
-        const int groups = (int)((E + 63) / 64);
-        if (timing) {
-            ensure_events(2 * (size_t)nl + 2);
-            HIPC(hipEventRecord(events[2 * nl], stream));
-        }
-        int64_t launched = 0;
-        trace_launch.clear();
-        trace_wg.clear();
-        if (trace) {
-            trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(sc->off[nl], 1));
-            trace_wg = sc->list;
-        }
-        for (int64_t k = 0; k < nl; ++k) {
-            const int64_t grid = sc->off[k + 1] - sc->off[k];
-            if (grid == 0) continue;
-            a.active = sc->active.p + sc->off[k];
-            a.k0 = (int32_t)(k * P.p.tile);
-            if (trace) {
-                a.trace = trace_buf.p + mcr::kTraceWords * sc->off[k];
-                trace_launch.resize(sc->off[k + 1], k);
-            }
-            if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-            HIPC(mcr::launch_member_sweep(a, (int)grid, groups, stream));
-            if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
-            ++launched;
-        }
-        HIPC(mcr::launch_from_sweep(S.So.p, ns, S.mmap.p, st_o.p, nsm, E, stream));
-        HIPC(mcr::launch_from_sweep(S.Si.p, ns, S.mmap.p, st_i.p, nsm, E, stream));
-        if (timing) {
-            HIPC(hipEventRecord(events[2 * nl + 1], stream));
-            HIPC(hipEventSynchronize(events[2 * nl + 1]));
-            for (int64_t k = 0; k < launched; ++k) {
-                float ms = 0.f;
-                HIPC(hipEventElapsedTime(&ms, events[2 * k], events[2 * k + 1]));
-                kernel_ms += ms;
-            }
-            float ms = 0.f;
-            HIPC(hipEventElapsedTime(&ms, events[2 * nl], events[2 * nl + 1]));
-            run_ms += ms;
-            launches += launched;
-        }
-        out_sweep = true;
-        last_flow.valid = false;
-        last_path = 3;
-    }
-
     // the outputs of the last run, as the gather kernels address them
     struct OutView {
         const double* O;
@@ -1098,7 +827,6 @@ struct Net {
         int64_t stride;
     };
     OutView out_view() const {
-        if (out_sweep) return {sw->O.p, 1, sw->jbase.p, sw->plan.nslots * E};
         return {O.p, cur->Otot, cur->jbase.p, (int64_t)row_width()};
     }
 
@@ -1129,17 +857,6 @@ struct Net {
         }
         last_path = 0;
         out_io = false;
-        out_sweep = false;
-        if (E > 1 && T > 1 && sweep_fits(T, Fsrc, tabh)) {
-            settle_gain();
-            run_sweep(T, rows);
-            T_out = T;
-            return;
-        }
-        if (mode == 4)
-            throw Fail(MC_E_STATE, "sweep mode requested but this horizon cannot run as a member "
-                                   "sweep (one member, one step, forcing rows too dense for the "
-                                   "step, or no member plan for this network)");
         ensure_schedule(T);
         const int64_t nl = (int64_t)cur->off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
@@ -1239,51 +956,6 @@ struct Net {
                 throw Fail(MC_E_STATE, "member dataflow requested but the network does not fit one "
                                        "resident launch");
             }
-            if (E > 1 && T > 1 && ens_flow_fits(T, dense, flds)) {
-                // ---- the whole horizon of every member as ONE launch (flow.hip, ticket queue):
-                // instance (w, e) walks workgroup w's window for member e; granules per member
-                const size_t words = plan.ext_src.size() * (size_t)T * 4;
-                const size_t all = words * (size_t)E;
-                if (all > xg_words || epoch == 0xffffffffu) {
-                    XG.reserve(std::max<size_t>(all, 4));
-                    HIPC(hipMemsetAsync(XG.p, 0, std::max<size_t>(all, 4) * 4, stream));
-                    xg_words = std::max(xg_words, all);
-                    epoch = 0;
-                }
-                ++epoch;
-                qctr.reserve(1);
-                HIPC(hipMemsetAsync(qctr.p, 0, sizeof(int32_t), stream));
-                a.XG = XG.p;
-                a.xg_bytes = (uint32_t)std::max<size_t>(words * 4, 16);
-                a.mXG = (int64_t)words;
-                a.epoch = epoch;
-                a.status = status.p;
-                a.patience = patience;
-                a.table_cap = (int32_t)T;
-                a.active = all_wg.p;
-                a.queue = qctr.p;
-                a.order = topo.p;
-                a.qE = (int32_t)E;
-                st_o2.reserve(st_o.cap);
-                st_i2.reserve(st_i.cap);
-                a.st_o_out = st_o2.p;
-                a.st_i_out = st_i2.p;
-                if (timing) HIPC(hipEventRecord(events[0], stream));
-                HIPC(mcr::launch_flow(a, plan.nwg * (int)E, plan.p.slots, plan.p.chain, flds,
-                                      dense, stream));
-                if (timing) HIPC(hipEventRecord(events[1], stream));
-                a.queue = nullptr;
-                st_o.swap(st_o2);
-                st_i.swap(st_i2);
-                ++flow_runs;
-                last_flow.valid = true;
-                last_flow.T = T;
-                last_flow.F = Fsrc;
-                last_flow.rows = rows;
-                last_flow.tab = tabh;
-                launched = 1;
-                last_path = 2;
-            }
             if (E == 1 && flow_fits(T, dense, flds)) {
                 // ---- one dataflow launch for the whole horizon (flow.hip)
                 const size_t words = plan.ext_src.size() * (size_t)T * 4;
@@ -1378,7 +1050,6 @@ struct Net {
         const int64_t n = plan.n;
         xp.assign(xps, xps + rows);
         n_rows = rows;
-        ++f_ver;
         F.reserve((size_t)(rows * plan.nslots * E));
         if (n == 0) return;
         // caller-order staging: kept between calls when small (sub-basin sessions reload their
@@ -1933,7 +1604,7 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         REQUIRE(D->E == 1 && S->E == 1, "lateral corrections route single-member sessions");
         REQUIRE(0 <= dst_reach && dst_reach < D->plan.n && 0 <= src_reach && src_reach < S->plan.n,
                 "reach index out of range");
-        REQUIRE(S->T_out > 0 && S->cur && !S->out_io && !S->out_sweep,
+        REQUIRE(S->T_out > 0 && S->cur && !S->out_io,
                 "the source session has no horizon outputs");
         REQUIRE(D->n_rows == S->T_out,
                 "the destination's forcing rows must be the source horizon's steps (one input "
@@ -1952,7 +1623,6 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, S->row_width(),
                                             o_start, alpha, beta, gamma, D->F.p, D->plan.nslots,
                                             D->plan.pos[dst_reach], S->T_out, D->stream));
-        ++D->f_ver;
         HIPC(hipEventRecord(ev, D->stream));
         HIPC(hipStreamWaitEvent(S->stream, ev, 0));
     });
@@ -2070,9 +1740,8 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 4,
-                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow), 3 (auto + ensemble "
-                "dataflow horizons) or 4 (member sweep)");
+        REQUIRE(mode >= 0 && mode <= 2,
+                "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
         as_net(net)->mode = mode;
     });
 }

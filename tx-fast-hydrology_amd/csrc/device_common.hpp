@@ -41,7 +41,10 @@ __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
 struct Slot {
     int64_t d;            // node slot
     int G;                // tick of step 0 (huge when the slot has no work in this launch)
-    bool routed, psum, xsrc;
+    int Ga;               // G for the state update: huge for partial sums, whose state stays 0
+                          // (their update 0 + (((1 I + 0 Ip) + 0 Op) + 0 q) is then exactly I,
+                          // also for non-finite I: 0 Ip with Ip = +-Inf would be NaN)
+    bool routed, psum, unr, xsrc;   // unr: never processed by the reference walk (o = 0)
     double al, be, ch, ga, op, ip;
     int cnt;
     unsigned ubase[kUpInline];  // LDS byte base of each input
@@ -62,6 +65,8 @@ __device__ __forceinline__ void load_slot(Slot& s, const WaveArgs& a, int64_t d,
     s.G = live ? Gr : (1 << 29);                        // never active when not live
     s.routed = fl == kSlotRouted;
     s.psum = fl == kSlotSum;
+    s.Ga = s.psum ? (1 << 29) : s.G;
+    s.unr = fl == kSlotUnrouted;
     // state after the last step this slot ran in an earlier launch (or the initial state)
     s.op = a.st_o[mem * a.mS + d];
     s.ip = a.st_i[mem * a.mS + d];

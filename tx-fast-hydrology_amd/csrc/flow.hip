@@ -23,28 +23,6 @@
 
 #pragma clang fp contract(off)
 
-#ifndef MCR_EXP_NO_STORES
-#define MCR_EXP_NO_STORES 0
-#endif
-#ifndef MCR_EXP_NO_Q
-#define MCR_EXP_NO_Q 0
-#endif
-#ifndef MCR_EXP_CHUNK_BARRIER
-#define MCR_EXP_CHUNK_BARRIER 0  // diagnostic (wrong results): one barrier per chunk, not per tick
-#endif
-#ifndef MCR_EXP_BARRIER_CLOCK
-#define MCR_EXP_BARRIER_CLOCK 0  // diagnostic: the trace's CU-id word holds tick-barrier cycles
-#endif
-#ifndef MCR_EXP_NO_ZERO_ADD
-#define MCR_EXP_NO_ZERO_ADD 0    // diagnostic: drop the reference's leading 0 + of the update
-#endif
-#ifndef MCR_EXP_NO_ACT
-#define MCR_EXP_NO_ACT 0         // diagnostic (wrong results): every slot active at every tick
-#endif
-#ifndef MCR_EXP_NO_HELPER
-#define MCR_EXP_NO_HELPER 0      // diagnostic: the helper wave only joins the barriers
-#endif
-
 namespace mcr {
 
 namespace {
@@ -203,32 +181,16 @@ void wavefront_flow(WaveArgs a) {
     const int tid = threadIdx.x;
     const int nthr = SLOTS + kHelperLanes;
     const int64_t t_start = a.trace ? wall_clock64() : 0;
-    // the routed instance: this workgroup of the plan, or (ensemble horizon) the next ticket's
-    // (workgroup, member) in the queue's topological order
-    int w = 0, mem = 0;
-    if (!MEMB && a.queue) {
-        __shared__ int ticket;
-        if (tid == 0)
-            ticket = __hip_atomic_fetch_add(a.queue, 1, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int t = ticket;
-        w = a.order[t / a.qE];
-        mem = t - (t / a.qE) * a.qE;
-    } else {
-        w = a.active[blockIdx.x];
-    }
+    const int w = a.active[blockIdx.x];
     const int gminw = a.wg_gmin[w], gmaxw = a.wg_gmax[w];
     const int kb = gminw & ~(kChunk - 1);               // first chunk of this workgroup
     const int wend = gmaxw + T;                         // end of its tick window
     const int e0 = a.ext_off[w];
     const int next = a.ext_off[w + 1] - e0;
-    // member bases (member-major arrays; 0 for the one-member horizon)
-    const double* __restrict__ Fm = a.F + (int64_t)mem * a.mF;
-    double* __restrict__ Om = a.O + (int64_t)mem * a.mO;
-    const int64_t sm = (int64_t)mem * a.mS;
-    const auto xg = __builtin_amdgcn_make_buffer_rsrc(a.XG + (int64_t)mem * a.mXG, (short)0,
-                                                      (int)a.xg_bytes, 0x00020000);
+    const double* __restrict__ Fm = a.F;
+    double* __restrict__ Om = a.O;
+    const auto xg = __builtin_amdgcn_make_buffer_rsrc(a.XG, (short)0, (int)a.xg_bytes,
+                                                      0x00020000);
 
     // ---- shared prologue: step table, consumer ticks of external inputs
     if (!MEMB)
@@ -250,7 +212,7 @@ void wavefront_flow(WaveArgs a) {
         const int hl = tid & 63;
         const int64_t wbh = a.wbase[w];
         auto copy_row = [&](int k) {
-            if (MEMB || MCR_EXP_NO_STORES || k < gminw || k >= wend) return;   // wave-uniform
+            if (MEMB || k < gminw || k >= wend) return;   // wave-uniform
             const char* src = lds + XB + (unsigned)(k & 7) * PL;
             double* dst = Om + wbh + (int64_t)(k - gminw) * RS;
 #pragma unroll
@@ -264,34 +226,34 @@ void wavefront_flow(WaveArgs a) {
         __syncthreads();                     // prologue barrier (matches the compute waves)
         for (int kc = kb; kc < wend; kc += kChunk) {
             const int kn = kc + kChunk;
-            const bool pre = kn < wend && nb > 0 && !MCR_EXP_NO_HELPER;
+            const bool pre = kn < wend && nb > 0;
             const unsigned slot = (unsigned)((kn >> 3) & 1);
             // both batches issued at the chunk start and consumed after ticks 4 and 5 (the
             // sc1 loads cross the XCDs: consuming at tick 3 stalled the group, -1.6% measured)
             u32x4 g[kBatch], g1[kBatch];
             if (pre) h.issue(0, kn, g);
             if (pre && nb > 1) h.issue(1, kn, g1);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 0
+            __syncthreads();   // tick 0
             copy_row(kc);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 1
+            __syncthreads();   // tick 1
             copy_row(kc + 1);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 2
+            __syncthreads();   // tick 2
             copy_row(kc + 2);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 3
+            __syncthreads();   // tick 3
             copy_row(kc + 3);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 4
+            __syncthreads();   // tick 4
             if (pre) {
                 const int bad = h.consume(0, kn, slot, g);
                 if (__any(bad >= 0)) h.settle(0, kn, slot, bad);
             }
             copy_row(kc + 4);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 5
+            __syncthreads();   // tick 5
             if (pre && nb > 1) {
                 const int bad = h.consume(1, kn, slot, g1);
                 if (__any(bad >= 0)) h.settle(1, kn, slot, bad);
             }
             copy_row(kc + 5);
-            if (!MCR_EXP_CHUNK_BARRIER) __syncthreads();   // tick 6
+            __syncthreads();   // tick 6
             copy_row(kc + 6);
             __syncthreads();                 // tick 7
             copy_row(kc + 7);
@@ -307,7 +269,7 @@ void wavefront_flow(WaveArgs a) {
     uint64_t up[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + lid, mem, kb, wend - kb, T);
+        load_slot(S[p], a, (int64_t)w * RS + p * SLOTS + lid, 0, kb, wend - kb, T);
         up[p] = a.up4[S[p].d];
         xbp[(((kb - 1) & 7) * PL) / 8 + p * SLOTS + lid] = S[p].op;
     }
@@ -325,7 +287,6 @@ void wavefront_flow(WaveArgs a) {
 
     const unsigned epoch = a.epoch;
     int64_t t_loop = 0, c_loop = 0;
-    int64_t bar_cyc = 0;     // MCR_EXP_BARRIER_CLOCK: shader cycles this lane spent in tick barriers
     if constexpr (MEMB) {
         // ---- member dataflow: tick k runs member e = k - G of each slot.  Per-member inputs
         // (state, lateral inflow) are prefetched kRing ticks ahead into a register ring.  Large
@@ -523,8 +484,9 @@ void wavefront_flow(WaveArgs a) {
                     hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
                 }
                 const double f = __hiloint2double(e.w, e.z);
-                const double qq = (1.0 - f) * lo + f * hi;
-                return MCR_EXP_NO_Q ? 0.0 : qq;   // clamped steps: hi = lo, frac = 0
+                // clamped steps (row_lo == row_hi): the row itself (nutils.py:24-27)
+                const double qq = e.x == e.y ? lo : (1.0 - f) * lo + f * hi;
+                return qq;
             };
             double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
             if constexpr (kBatchQ) {
@@ -551,11 +513,10 @@ void wavefront_flow(WaveArgs a) {
                 double prev = 0.0;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    const bool act = MCR_EXP_NO_ACT || (unsigned)(k - S[p].G) < (unsigned)T;
+                    const bool act = (unsigned)(k - S[p].Ga) < (unsigned)T;
                     const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                    const double xx = ((S[p].al * I + S[p].be * S[p].ip) + S[p].ch * S[p].op) +
-                                      S[p].ga * qv[p];
-                    const double rr = MCR_EXP_NO_ZERO_ADD ? xx : 0.0 + xx;
+                    const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
+                                              S[p].ch * S[p].op) + S[p].ga * qv[p]);
                     const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
                     S[p].op = act ? o : S[p].op;
                     S[p].ip = act ? I : S[p].ip;
@@ -578,13 +539,7 @@ void wavefront_flow(WaveArgs a) {
                             gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
                     }
                 }
-#if MCR_EXP_BARRIER_CLOCK
-                const int64_t tb0 = clock64();
                 __syncthreads();
-                bar_cyc += clock64() - tb0;
-#else
-                if (!MCR_EXP_CHUNK_BARRIER || i == kChunk - 1) __syncthreads();
-#endif
             }
 #pragma unroll
             for (int p = 0; p < K; ++p) {
@@ -595,11 +550,12 @@ void wavefront_flow(WaveArgs a) {
                 f2[p] = g2[p];
             }
         }
-        // session state after the horizon; never-processed reaches hold o = 0
+        // session state after the horizon; never-processed reaches hold o = 0 (nutils.py:68:
+        // the kernel's own value for them, 0 q + ..., is NaN for non-finite inputs)
 #pragma unroll
         for (int p = 0; p < K; ++p) {
-            a.st_o_out[sm + S[p].d] = S[p].op;
-            a.st_i_out[sm + S[p].d] = S[p].ip;
+            a.st_o_out[S[p].d] = S[p].unr ? 0.0 : S[p].op;
+            a.st_i_out[S[p].d] = S[p].ip;
         }
     }
     if (a.trace && tid == 0) {
@@ -607,7 +563,7 @@ void wavefront_flow(WaveArgs a) {
         rec[0] = t_start;
         rec[1] = t_loop;
         rec[2] = wall_clock64();
-        rec[3] = MCR_EXP_BARRIER_CLOCK ? bar_cyc : (int64_t)__smid();
+        rec[3] = (int64_t)__smid();
         rec[4] = c_loop;
         rec[5] = clock64();
     }
@@ -726,7 +682,7 @@ __global__ __launch_bounds__(256) void member_inputs(
             i = i + ig;
         }
         IO[c] = make_double2(o, i);
-        Qm[c] = ent.y < 0 ? lo : (1.0 - f) * lo + f * hi;
+        Qm[c] = ent.x == ent.y ? lo : (1.0 - f) * lo + f * hi;   // clamped: row copy
     }
 }
 
@@ -804,7 +760,7 @@ __global__ __launch_bounds__(256) void member_inputs_ring(
             o = o + og;
             i = i + ig;
         }
-        q = ent.y < 0 ? lo : (1.0 - f) * lo + f * hi;
+        q = ent.x == ent.y ? lo : (1.0 - f) * lo + f * hi;       // clamped: row copy
     };
     if (ghi - glo > kStageRing - kStageChunk) {            // wide group (wave-uniform)
         if (real)
@@ -886,7 +842,11 @@ __global__ __launch_bounds__(256) void member_unpack_ring(
     const int64_t d0 = ((int64_t)blockIdx.x * 4 + wv) * kStageSlots;
     if (d0 >= ns) return;                                  // wave-uniform
     const int64_t d = d0 + s;
-    const bool real = mw.flags[d] != kSlotPad;
+    const uint8_t fl = mw.flags[d];
+    const bool real = fl != kSlotPad;
+    // never-processed reaches keep o = 0 (nutils.py:68; their cell holds the kernel's 0 q + ...),
+    // partial sums a zero state (device_common.hpp Slot::Ga)
+    const bool zo = fl == kSlotUnrouted || fl == kSlotSum, zi = fl == kSlotSum;
     const int64_t w = d0 / mw.rs;
     const int gs = real ? mw.G[d] - mw.gmin[w] : 0;
     int glo = real ? gs : 0x7fffffff, ghi = real ? gs : -1;
@@ -911,8 +871,8 @@ __global__ __launch_bounds__(256) void member_unpack_ring(
                 for (int h = 0; h < kStageLoads; ++h) {
                     const int64_t e = e0 + 4 * h + sub;
                     if (e < E) {
-                        st_o[e * ns + d] = v[h].x;
-                        st_i[e * ns + d] = v[h].y;
+                        st_o[e * ns + d] = zo ? 0.0 : v[h].x;
+                        st_i[e * ns + d] = zi ? 0.0 : v[h].y;
                     }
                 }
             }
@@ -947,8 +907,8 @@ __global__ __launch_bounds__(256) void member_unpack_ring(
                 const int e = e0 + sub;
                 if (real && e < upto) {
                     const int k = (e & (kStageRing - 1)) * kStageSlots + s;
-                    st_o[(int64_t)e * ns + d] = Ro[k];
-                    st_i[(int64_t)e * ns + d] = Ri[k];
+                    st_o[(int64_t)e * ns + d] = zo ? 0.0 : Ro[k];
+                    st_i[(int64_t)e * ns + d] = zi ? 0.0 : Ri[k];
                 }
             }
             done = upto;
@@ -1000,14 +960,17 @@ __global__ __launch_bounds__(256) void member_unpack(
         int64_t ns, int64_t E, MemberWin mw) {
     const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= ns || mw.flags[d] == kSlotPad) return;
+    // never-processed reaches: o stays 0 (nutils.py:68); partial sums: zero state (Slot::Ga)
+    const bool zo = mw.flags[d] == kSlotUnrouted || mw.flags[d] == kSlotSum;
+    const bool zi = mw.flags[d] == kSlotSum;
     const int64_t e0 = (int64_t)blockIdx.y * kMemberRun;
     const int ne = (int)(E - e0 < kMemberRun ? E - e0 : kMemberRun);
     const RunCells rc = member_run(mw, d, e0);
 #pragma unroll 4
     for (int k = 0; k < ne; ++k) {
         const double2 v = IO[rc.c0 + k * rc.cs];
-        st_o[(e0 + k) * ns + d] = v.x;
-        st_i[(e0 + k) * ns + d] = v.y;
+        st_o[(e0 + k) * ns + d] = zo ? 0.0 : v.x;
+        st_i[(e0 + k) * ns + d] = zi ? 0.0 : v.y;
     }
 }
 
@@ -1019,8 +982,9 @@ __global__ void gather_io(const double2* __restrict__ IO, const int64_t* __restr
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= n * E) return;
     const int64_t j = x / E, e = x - j * E;
-    const double2 v = IO[member_cell(mw, pos[j], e)];
-    out[x] = inflow ? v.y : v.x;
+    const int64_t d = pos[j];
+    const double2 v = IO[member_cell(mw, d, e)];
+    out[x] = inflow ? v.y : (mw.flags[d] == kSlotUnrouted ? 0.0 : v.x);   // unrouted: o = 0
 }
 
 static dim3 member_grid(int64_t ns, int64_t E) {

@@ -20,18 +20,6 @@
 
 #pragma clang fp contract(off)
 
-// Diagnostic builds only (scripts/exp_variants.sh): each MCR_EXP_* switch removes one part of the
-// tick to measure its cost.  Results of such a build are wrong by construction.
-#ifndef MCR_EXP_NO_STORES
-#define MCR_EXP_NO_STORES 0
-#endif
-#ifndef MCR_EXP_NO_BARRIER
-#define MCR_EXP_NO_BARRIER 0
-#endif
-#ifndef MCR_EXP_NO_Q
-#define MCR_EXP_NO_Q 0
-#endif
-
 namespace mcr {
 
 namespace {
@@ -56,15 +44,9 @@ using dev::read_inputs;
 // DENSE: some chunk needs more than 3 forcing rows (model step >= ~1/3 of the forcing interval);
 // those lanes read the forcing straight from global memory.  A separate instantiation keeps the
 // direct loads (and the waits they need) out of the common kernel.
-#ifndef MCR_DET_WAVES
-#define MCR_DET_WAVES 2
-#endif
-#ifndef MCR_DET_BATCHQ
-#define MCR_DET_BATCHQ 1
-#endif
 template <int SLOTS, int K, bool DENSE>
 __global__ __launch_bounds__(SLOTS)
-__attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : MCR_DET_WAVES, K >= 4 ? 1 : MCR_DET_WAVES)))
+__attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
 void wavefront_det(WaveArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int RS = K * SLOTS;
@@ -164,7 +146,7 @@ void wavefront_det(WaveArgs a) {
     const int64_t t_loop = a.trace ? wall_clock64() : 0;
     const int64_t c_loop = a.trace ? clock64() : 0;
 
-    constexpr bool kBatchQ = MCR_DET_BATCHQ && K <= 2;                    // lateral inflows per chunk (registers)
+    constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         // this chunk's forcing rows -> the slots' LDS rows (private: no barrier needed)
@@ -216,8 +198,10 @@ void wavefront_det(WaveArgs a) {
                 hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
             }
             const double f = __hiloint2double(e.w, e.z);
-            const double qq = (1.0 - f) * lo + f * hi;
-            return MCR_EXP_NO_Q ? 0.0 : qq;   // clamped steps: hi = lo, frac = 0
+            // clamped steps (row_lo == row_hi) copy the row as the reference does
+            // (nutils.py:24-27): exact for +-Inf / NaN, where (1 - 0) f + 0 f is not
+            const double qq = e.x == e.y ? lo : (1.0 - f) * lo + f * hi;
+            return qq;
         };
         double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
         if constexpr (kBatchQ) {
@@ -252,12 +236,13 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 act[p] = (unsigned)(k - S[p].G) < (unsigned)T;
+                const bool upd = (unsigned)(k - S[p].Ga) < (unsigned)T;   // not partial sums
                 const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
                 const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
                                           S[p].ch * S[p].op) + S[p].ga * qv[p]);
                 const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
-                S[p].op = act[p] ? o : S[p].op;
-                S[p].ip = act[p] ? I : S[p].ip;
+                S[p].op = upd ? o : S[p].op;
+                S[p].ip = upd ? I : S[p].ip;
                 ov[p] = o;
                 prev = o;
             }
@@ -270,7 +255,7 @@ void wavefront_det(WaveArgs a) {
             // (slots are sorted by G, so a wave's active lanes are a contiguous run and the
             // masked rows stay whole 32-B sectors except at the run's ends): the window cells a
             // slot does not run in are never read (window_index), so they are not written
-            if (!MCR_EXP_NO_STORES) {
+            {
                 double* orow = Om + wb + (int64_t)(k - gminw) * RS;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
@@ -281,7 +266,7 @@ void wavefront_det(WaveArgs a) {
                     }
                 }
             }
-            if (!MCR_EXP_NO_BARRIER) __syncthreads();
+            __syncthreads();
         }
 #pragma unroll
         for (int p = 0; p < K; ++p) {
@@ -299,7 +284,7 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         if (S[p].G != (1 << 29)) {
-            a.st_o[sb + S[p].d] = S[p].op;
+            a.st_o[sb + S[p].d] = S[p].unr ? 0.0 : S[p].op;   // unrouted: o stays 0
             a.st_i[sb + S[p].d] = S[p].ip;
         }
     }
@@ -376,6 +361,7 @@ __global__ void forcing_to_slots(const double* __restrict__ fp, double* __restri
 }
 
 __global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __restrict__ G,
+                             const uint8_t* __restrict__ flags,
                              const int32_t* __restrict__ wg_gmin,
                              const int64_t* __restrict__ wbase, int slots, int64_t n,
                              int64_t* __restrict__ jbase) {
@@ -383,7 +369,11 @@ __global__ void window_index(const int64_t* __restrict__ pos, const int32_t* __r
          j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t d = pos[j];
         const int64_t w = d / slots;
-        jbase[j] = wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * slots + (d - w * slots);
+        // never-processed reaches: -1, their outflow reads as 0 (nutils.py:68); the kernels'
+        // own value for them (0 q + ...) is NaN for non-finite inputs
+        jbase[j] = flags[d] == kSlotUnrouted
+                       ? -1
+                       : wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * slots + (d - w * slots);
     }
 }
 
@@ -414,8 +404,9 @@ __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
         const int64_t t = tj / n;
         const int64_t j = tj - t * n;
         const double* Oe = O + e * mO;
+        const int64_t jb = jbase[j];
         out[x] = inflow ? inflow_at(Oe, jbase, in_off, in_list, j, t0 + t, slots)
-                        : Oe[jbase[j] + (t0 + t) * slots];
+                        : (jb < 0 ? 0.0 : Oe[jb + (t0 + t) * slots]);
     }
 }
 
@@ -433,8 +424,9 @@ __global__ void gather_series(const double* __restrict__ O, int64_t mO,
         const int64_t j = jt / T;
         const int64_t t = jt - j * T;
         const double* Oe = O + e * mO;
+        const int64_t jb = jbase[j];
         out[x] = inflow ? inflow_at(Oe, jbase, in_off, in_list, j, t, slots)
-                        : Oe[jbase[j] + t * slots];
+                        : (jb < 0 ? 0.0 : Oe[jb + t * slots]);
     }
 }
 
@@ -449,8 +441,9 @@ __global__ void lateral_correction(const double* __restrict__ O, const int64_t* 
                                    int64_t ns, int64_t dslot, int64_t T) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < T;
          r += (int64_t)gridDim.x * blockDim.x) {
-        const double inext = O[jbase[j] + r * slots];
-        const double iprev = r == 0 ? o_start : O[jbase[j] + (r - 1) * slots];
+        const int64_t jb = jbase[j];                  // < 0: an unrouted outlet, o = 0
+        const double inext = jb < 0 ? 0.0 : O[jb + r * slots];
+        const double iprev = r == 0 ? o_start : (jb < 0 ? 0.0 : O[jb + (r - 1) * slots]);
         double* f = F + r * ns + dslot;
         *f = *f + (alpha * inext / gamma + beta * iprev / gamma);
     }
@@ -556,12 +549,12 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
     return hipGetLastError();
 }
 
-hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
-                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
-                               hipStream_t s) {
+hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const uint8_t* flags,
+                               const int32_t* wg_gmin, const int64_t* wbase, int slots, int64_t n,
+                               int64_t* jbase, hipStream_t s) {
     if (n > 0)
-        hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, wg_gmin, wbase,
-                           slots, n, jbase);
+        hipLaunchKernelGGL(window_index, grid_for(n, 256), 256, 0, s, pos, G, flags, wg_gmin,
+                           wbase, slots, n, jbase);
     return hipGetLastError();
 }
 

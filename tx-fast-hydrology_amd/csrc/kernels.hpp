@@ -106,16 +106,6 @@ struct WaveArgs {
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
-    // ensemble dataflow (flow.hip, E > 1 horizon): every (workgroup, member) instance takes a
-    // ticket from `queue` (zeroed before the launch); ticket t routes workgroup order[t / qE]
-    // for member t % qE.  `order` is a topological order of the workgroup graph (producers
-    // first), so an instance waits only for instances that took earlier tickets: deadlock-free
-    // without co-residency.  mXG: granule words per member.  queue == NULL: the one-member
-    // horizon (the grid is every workgroup, all resident).
-    int32_t* queue;
-    const int32_t* order;
-    int32_t qE;
-    int64_t mXG;
 };
 
 // LDS bytes of the multi-launch kernel for `slots` lanes (chain * slots node slots): the
@@ -225,9 +215,10 @@ hipError_t launch_forcing_to_slots(const double* fp, double* F, const int64_t* s
                                    int64_t n, int64_t nslots, int64_t n_rows, int64_t E,
                                    hipStream_t s, bool reach_major = false);
 // jbase[j] = window index of step 0 of caller reach j
-hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const int32_t* wg_gmin,
-                               const int64_t* wbase, int slots, int64_t n, int64_t* jbase,
-                               hipStream_t s);
+// (-1 for never-processed reaches: their outflow reads as 0)
+hipError_t launch_window_index(const int64_t* pos, const int32_t* G, const uint8_t* flags,
+                               const int32_t* wg_gmin, const int64_t* wbase, int slots, int64_t n,
+                               int64_t* jbase, hipStream_t s);
 // Output gathers (caller order, member innermost).  inflow = false: outflow O; true: the inflow
 // of reach j, summed from O over its inflow list.
 // step-major out[t - t0][j][e] for t in [t0, t1)

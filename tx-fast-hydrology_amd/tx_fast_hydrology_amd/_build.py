@@ -129,7 +129,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_variant(name: str, extra_flags, verbose: bool = False) -> str:
-    """Diagnostic / A-B build of the whole library with extra compile flags (e.g. an MCR_EXP_*
+    """Diagnostic / A-B build of the whole library with extra compile flags (e.g. a -D switch
     switch) into lib/exp/lib_<name>.so; bench.py / tests load it with MCROUTE_LIB=<path>."""
     out_dir = os.path.join(LIB_DIR, "exp")
     obj_dir = os.path.join(out_dir, "obj_" + name)

@@ -403,11 +403,10 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
-    MODES = {"auto": 0, "launches": 1, "dataflow": 2, "ensemble": 3, "sweep": 4}
+    MODES = {"auto": 0, "launches": 1, "dataflow": 2}
 
     def set_mode(self, mode: str):
-        """Execution path: "auto" (default), "launches", "dataflow", "ensemble" or "sweep"
-        (see mcroute.h mc_set_mode)."""
+        """Execution path: "auto" (default), "launches" or "dataflow" (mcroute.h mc_set_mode)."""
         nat.check(nat.lib().mc_set_mode(self._h, self.MODES[mode]))
 
     def set_flow_patience(self, wall_ticks: int):
@@ -416,12 +415,12 @@ class RoutingNet:
         nat.check(nat.lib().mc_set_flow_patience(self._h, int(wall_ticks)))
 
     def mode(self) -> tuple:
-        """(requested mode, path of the last run: "launches" / "dataflow" / "sweep" / None)."""
+        """(requested mode, path of the last run: "launches" / "dataflow" / None)."""
         m = ctypes.c_int()
         p = ctypes.c_int()
         nat.check(nat.lib().mc_get_mode(self._h, ctypes.byref(m), ctypes.byref(p)))
         names = {v: k for k, v in self.MODES.items()}
-        return names[m.value], {1: "launches", 2: "dataflow", 3: "sweep"}.get(p.value)
+        return names[m.value], {1: "launches", 2: "dataflow"}.get(p.value)
 
     def set_trace(self, enable: bool):
         nat.check(nat.lib().mc_set_trace(self._h, 1 if enable else 0))
