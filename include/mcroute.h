@@ -185,9 +185,12 @@ int mc_ens_unpack_apply(void* net, int64_t nranks, const double* Grecv_dev);
  *   mc_ens_analysis_dist: one analysis of this rank's E members (y_local [m][E]; gauges and R
  *                      identical on every rank): the stages above with the all-gathers and
  *                      all-to-alls on the session's stream, the member -> slice all-to-all on a
- *                      side stream while the Et x Et weights are formed.  Bit-identical to the
- *                      staged Python driver (ensemble.distributed_analysis) and, with one rank,
- *                      to mc_enkf_analysis.
+ *                      side stream while the Et x Et weights are formed.  With one rank it is
+ *                      bit-identical to mc_enkf_analysis (tested); the same stages with N ranks
+ *                      are bit-identical to the one-session analysis when driven by
+ *                      ensemble.emulated_analysis (8 shards, tested), but the multi-rank RCCL run
+ *                      itself is UNVERIFIED until tests/test_gpu_dist.py's multi-GPU test runs
+ *                      on a node with two or more GPUs (it is skipped on one).
  * MC_E_STATE when no RCCL library can be loaded. */
 int mc_comm_unique_id(uint8_t* id128);
 int mc_comm_init(int32_t nranks, int32_t rank, const uint8_t* id128, void** comm);
@@ -197,7 +200,8 @@ int mc_ens_analysis_dist(void* net, void* comm, int64_t m, const int64_t* gauges
 
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
                   const double* gamma);
-/* State (o_t_next, i_t_next) of the model, caller order. */
+/* State (o_t_next, i_t_next) of the model, caller order.  Like every upload of this ABI it
+ * has read the caller's arrays when it returns (page-locked sources are waited for). */
 int mc_set_state(void* net, const double* o_t_next, const double* i_t_next);
 int mc_get_state(void* net, double* o_t_next, double* i_t_next);
 /* Device-to-device state hand-over between two sessions of the SAME network (e.g. plans with

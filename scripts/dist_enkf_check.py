@@ -22,6 +22,10 @@ def main():
     ap.add_argument("--reaches", type=int, default=20000)
     ap.add_argument("--members", type=int, default=8, help="members per rank")
     ap.add_argument("--gauges", type=int, default=50)
+    ap.add_argument("--capi", action="store_true",
+                    help="run the analysis through the C ABI's own RCCL communicator "
+                         "(mc_comm_* / mc_ens_analysis_dist; one GPU per rank); torch.distributed "
+                         "(gloo) only hands the communicator id around and gathers the results")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -53,8 +57,15 @@ def main():
     net = engine.RoutingNet(end, indeg, start[indeg == 0], members=El)
     net.set_coeffs(*coef)
     net.set_state(np.ascontiguousarray(X[:, cols]), np.ascontiguousarray(I0[:, cols]))
-    ensemble.distributed_analysis(net, s, np.ascontiguousarray(Y[:, cols]), R,
-                                  device=torch.device("cuda", dev))
+    if args.capi:
+        uid = [engine.Communicator.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = engine.Communicator(world, rank, uid[0])
+        net.ens_analysis_dist(comm, s, np.ascontiguousarray(Y[:, cols]), R)
+        net.synchronize()
+    else:
+        ensemble.distributed_analysis(net, s, np.ascontiguousarray(Y[:, cols]), R,
+                                      device=torch.device("cuda", dev))
     o, i = net.get_state()
     ot = torch.from_numpy(np.ascontiguousarray(o))
     it = torch.from_numpy(np.ascontiguousarray(i))
@@ -75,7 +86,7 @@ def main():
         ro, ri = ref.get_state()
         ok = np.array_equal(got_o, ro) and np.array_equal(got_i, ri)
         err = max(np.abs(got_o - ro).max(), np.abs(got_i - ri).max())
-        print(f"DIST_ENKF world={world} members/rank={El} backend={args.backend} "
+        print(f"DIST_ENKF world={world} members/rank={El} backend={args.backend} capi={args.capi} "
               f"bitexact={ok} maxabs={err:.3e} gain_scale={np.abs(ro - X).max():.3e}",
               flush=True)
     dist.barrier()

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG="${1:-r05}"
 shift || true
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest -m gpu ${PYTEST_X:--x} -v --timeout 300 --timeout-method thread \
     -p no:cacheprovider "${@:-tests}" > gpurun_out/${TAG}_pytest_gpu.txt 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/${TAG}_pytest_gpu.txt

@@ -30,24 +30,53 @@ def test_two_rank_device_analysis_bitexact():
 @pytest.mark.timeout(420)
 def test_bench_two_ranks_gloo_line():
     """bench.py's N > 1 branch end to end on the one GPU of a test box: two ranks (gloo,
-    host-staged collectives), the member-sharded configs[3] EnKF as the headline (3 analysis
-    steps to bound the run), the replicated det run beside it, the CPU baseline timed on rank 0."""
+    host-staged collectives), the member-sharded configs[3] EnKF as the headline (16 members and
+    3 analysis steps, so that both ranks' sessions fit the one GPU), the replicated det run beside
+    it, the CPU baseline timed on rank 0."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend",
            "gloo", "--steps", "1", "--warmup", "0", "--timing-runs", "1", "--no-api",
-           "--obs-hours", "0.25", "--cpu-seconds", "1"]
+           "--obs-hours", "0.25", "--cpu-seconds", "1", "--members", "16", "--enkf"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     out = r.stdout + r.stderr
-    assert r.returncode == 0, out[-3000:]
+    # the first failing rank's traceback, not only the launcher's summary
+    ranks = "\n".join(ln for ln in out.splitlines() if ln.startswith("[rank"))
+    assert r.returncode == 0, ranks[:4000] + "\n...\n" + out[-1500:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out[-3000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["parallelism"] == "members sharded x2"
-    assert line["config"]["members"] == 256 and line["config"]["members_per_gpu"] == 128
+    assert line["config"]["members"] == 16 and line["config"]["members_per_gpu"] == 8
     assert line["value"] > 0 and line["value"] == line["value"]          # finite, not NaN
     assert line["det_replicas"]["parallelism"] == "replicas x2"
     assert line["det_replicas"]["value"] > 0
     cpu = line["cpu_baseline"]
     assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
+
+
+def _visible_gpus():
+    import torch
+    return torch.cuda.device_count()      # counts devices without initialising HIP
+
+
+@pytest.mark.timeout(300)
+def test_capi_communicator_multi_gpu_bitexact():
+    """mc_ens_analysis_dist with N > 1 ranks, one GPU each: the per-peer counts, the
+    member -> slice all-to-all on the side stream under the weights and the gathered results
+    must give every member exactly the one-session analysis.  Needs >= 2 GPUs (skipped on the
+    one-GPU test box; the driver's 8-GPU node runs it)."""
+    n = _visible_gpus()
+    if n < 2:
+        pytest.skip("needs at least two GPUs")
+    world = min(n, 8)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", "29519",
+           os.path.join(ROOT, "scripts", "dist_enkf_check.py"), "--backend", "gloo", "--capi",
+           "--reaches", "8000", "--members", "8", "--gauges", "40"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "bitexact=True" in out, out[-3000:]

@@ -454,6 +454,18 @@ struct Net {
         sb.reserve((size_t)(n * m));
         HIPC(hipMemcpyAsync(sb.p, host, n * m * sizeof(double), hipMemcpyHostToDevice, stream));
         HIPC(mcr::launch_scatter_to_slots(sb.p, dst.p, slot_reach.p, plan.nslots, m, stream));
+        // a copy from pageable memory has read the caller's array when it returns; one from
+        // page-locked memory (e.g. a yielded pinned output row) is truly asynchronous, so wait
+        // for it: the C ABI promises that the caller may reuse its arrays on return
+        if (host_pinned(host)) HIPC(hipStreamSynchronize(stream));
+    }
+    static bool host_pinned(const void* p) {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+            (void)hipGetLastError();                    // unregistered pageable memory
+            return false;
+        }
+        return at.type == hipMemoryTypeHost;
     }
     // Resolve pending dataflow runs (status word, re-run on give-up) before results are read.
     void settle() {
@@ -1062,8 +1074,8 @@ struct Net {
                                           stream, reach_major));
         // a copy from pageable host memory has read the caller's array when it returns, and the
         // persistent staging is reused stream-ordered: only the temporary staging must be
-        // drained before it is freed
-        if (&st == &tmp) sync();
+        // drained before it is freed, and a page-locked source (an asynchronous copy) read
+        if (&st == &tmp || host_pinned(fp)) sync();
     }
     static constexpr size_t kKeepStage = (size_t)1 << 23;   // 64 MiB
     DBuf<double> fstage, stage2;

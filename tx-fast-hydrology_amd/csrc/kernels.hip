@@ -114,9 +114,17 @@ void wavefront_det(WaveArgs a) {
         for (int k = 0; k < 8; ++k)
             if (base + k * SLOTS < ntot) xe[base + k * SLOTS] = v[k];
     }
-    // the consumer (one tick behind) reads step t_first - 1 at the first tick
+    // the consumer (one tick behind) reads step t_first - 1 at the first tick: the producer's
+    // state o, or for a partial sum (whose state stays 0, Slot::Ga) its output of tick k0 - 1,
+    // stored by the previous launch in the output window.  (S.G is huge for a slot with no step
+    // in THIS launch -- e.g. a partial sum whose last step was tick k0 - 1 -- so the plan's G.)
 #pragma unroll
-    for (int p = 0; p < K; ++p) xbp[(p * SLOTS + tid) * 2 + ((k0 - 1) & 1)] = S[p].op;
+    for (int p = 0; p < K; ++p) {
+        double carry = S[p].op;
+        if (S[p].psum && (unsigned)(k0 - 1 - a.G[S[p].d]) < (unsigned)T)
+            carry = Om[wb + (int64_t)(k0 - 1 - gminw) * RS + p * SLOTS + tid];
+        xbp[(p * SLOTS + tid) * 2 + ((k0 - 1) & 1)] = carry;
+    }
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;               // zero slot for unused codes
     // drain every prologue load: otherwise the wait-count pass carries "pending" state into
     // the tick loop and waits for each chunk's stores at every tick

@@ -153,6 +153,7 @@ class RoutingNet:
         self._h = h
         self.T = 0
         self.E = 1
+        self.runs = 0          # routing calls so far (mc_run / mc_step replace the outputs)
         if members != 1:
             self.set_members(members)
 
@@ -236,6 +237,7 @@ class RoutingNet:
         i_out = np.empty(self._shape())
         o_out = np.empty(self._shape())
         nat.check(nat.lib().mc_step(self._h, ptr(o), ptr(i), ptr(q), ptr(i_out), ptr(o_out)))
+        self.runs += 1
         return i_out, o_out
 
     # -- ensemble analysis -------------------------------------------------
@@ -336,6 +338,7 @@ class RoutingNet:
         x = f64(x)
         nat.check(nat.lib().mc_run(self._h, x.size, ptr(x)))
         self.T = x.size
+        self.runs += 1
 
     def fetch_outputs(self, t0=0, t1=None):
         """Step-major host copies (out_o[t][j](e), out_i[t][j](e)) of steps [t0, t1)."""

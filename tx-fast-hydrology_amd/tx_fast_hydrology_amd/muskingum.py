@@ -150,6 +150,68 @@ def _host_array(shape, dtype):
     return np.empty(shape, dtype=dtype)
 
 
+class _InflowBlock:
+    """The inflow rows of one fetch block of a fused horizon (steps [b0, b1) of the session's
+    last run), copied from the device only when a caller first reads one of them.  The
+    reference's own caller reads only the outflows (simulation.py:126-130), so a horizon whose
+    inflows nobody reads moves half the bytes over PCIe."""
+
+    __slots__ = ("net", "run_id", "b0", "b1", "n", "rows", "digests")
+
+    def __init__(self, net, b0, b1, n):
+        self.net, self.run_id, self.b0, self.b1, self.n = net, net.runs, b0, b1, n
+        self.rows = self.digests = None
+
+    def fetch(self):
+        if self.rows is None:
+            if self.net.runs != self.run_id:
+                # the model settles its lazy rows before anything reruns its session
+                raise RuntimeError("inflow rows of an earlier run were requested after the "
+                                   "session routed again")
+            rows = _host_array((self.b1 - self.b0, self.n), np.float64)
+            dig = np.empty(self.b1 - self.b0, dtype=np.uint64)
+            self.net.fetch_wait(self.net.fetch_outputs_async(self.b0, self.b1, None, rows,
+                                                             None, dig))
+            self.rows, self.digests = rows, dig
+        return self.rows
+
+
+class _LazyInflow:
+    """``i_t_next`` of one yielded step until a caller reads it (``Muskingum.i_t_next``): then
+    the step's row of its fetch block (a copy of its own for the last two steps, so the model's
+    final state keeps no block alive)."""
+
+    __slots__ = ("block", "k", "own", "value")
+
+    def __init__(self, block, k, own):
+        self.block, self.k, self.own, self.value = block, k, own, None
+
+    def get(self):
+        if self.value is None:
+            row = self.block.fetch()[self.k]
+            self.value = row.copy() if self.own else row
+        return self.value
+
+    def digest(self):
+        return int(self.block.digests[self.k])
+
+
+def _inflow_property(name):
+    key = "_" + name
+
+    def fget(self):
+        v = self.__dict__.get(key)
+        if isinstance(v, _LazyInflow):
+            v = self.__dict__[key] = v.get()
+        return v
+
+    def fset(self, value):
+        self.__dict__[key] = value
+
+    return property(fget, fset, doc=f"{name} (host float64 [n]; a fused horizon fetches it from "
+                                    "the device when it is first read)")
+
+
 def _upload_forcing(net, xp, dataframe):
     """Forcing frame -> the session (mc_load_forcing): a frame whose float64 block is stored
     reach-major (any frame pandas copied or built column by column) goes up in its own layout
@@ -231,6 +293,8 @@ class Muskingum:
     beta = _coef_property("beta")
     chi = _coef_property("chi")
     gamma = _coef_property("gamma")
+    i_t_next = _inflow_property("i_t_next")
+    i_t_prev = _inflow_property("i_t_prev")
 
     def __init__(self, data, load_optional=True, create_state_space=False, sparse=False):
         self.sparse = sparse
@@ -264,8 +328,15 @@ class Muskingum:
             self.create_state_space()
         self.save_state()
 
+    def _settle_inflows(self):
+        """Materialise inflow rows still left on the device by a fused horizon (before anything
+        routes on the session again, and before the model is copied)."""
+        for name in ("i_t_next", "i_t_prev"):
+            getattr(self, name)
+
     # -- copying: the device session is never shared or copied ---------------------------------
     def __getstate__(self):
+        self._settle_inflows()
         state = self.__dict__.copy()
         state["_device"] = None
         return state
@@ -276,6 +347,7 @@ class Muskingum:
         self._own_coefs()
 
     def __deepcopy__(self, memo):
+        self._settle_inflows()
         clone = self.__class__.__new__(self.__class__)
         memo[id(self)] = clone
         for key, value in self.__dict__.items():
@@ -529,6 +601,7 @@ class Muskingum:
             self.logger.warning("Timestep has changed. Recomputing Muskingum coefficients.")
             self.compute_muskingum_coeffs(dt=dt)
         _fire(self.callbacks, "__on_step_start__")
+        self._settle_inflows()
         net = self._device.session(self)
         i_t_next, o_t_next = net.step(p_t_next, o_t_prev, i_t_prev)
         self.o_t_next = o_t_next
@@ -556,6 +629,14 @@ class Muskingum:
         switches the rest of the horizon to step-by-step routing from the state found, as the
         reference would route it; so does changing a coefficient array (``_CoefArray`` counts
         writes).  Topology is read when a fused call starts.
+
+        Limit of the coefficient tracking: only writes through the model's own arrays (or their
+        ndarray views created from them) are counted.  Writes through a base-class alias --
+        ``np.asarray(model.alpha)`` (a plain ndarray sharing the memory), ``.view(np.ndarray)``,
+        ``torch.from_numpy``, numba or ctypes buffers -- are NOT seen; a fused horizon then keeps
+        routing with the coefficients uploaded when it started.  To change coefficients in the
+        middle of a horizon, assign through the model (``model.alpha[j] = v``,
+        ``model.alpha = new``) or bind a non-idle callback.
         """
         assert isinstance(dataframe.index, pd.DatetimeIndex)
         assert dataframe.index.tz == _dt.timezone.utc
@@ -608,6 +689,7 @@ class Muskingum:
         if not xs:
             return
         from . import engine
+        self._settle_inflows()
         net = self._device.session(self)
         _upload_forcing(net, xp, dataframe)
         net.set_state(self.o_t_next, self.i_t_next)
@@ -616,29 +698,29 @@ class Muskingum:
         block = max(1, _FETCH_BLOCK_VALUES // max(n, 1))
         timedelta = self.timedelta
         rev = self._coef_rev[0]
-        row_digest = engine.RowDigest()
         # the reference formats its per-step debug message unconditionally; formatting a
         # Timestamp costs more than the rest of a yielded step, so it is built only when emitted
         debug = self.logger.isEnabledFor(logging.DEBUG)
+        d = self.__dict__
         pending = []          # fetch tickets not yet waited for
         try:
             for c0 in range(0, T, chunk):
                 x = np.asarray(xs[c0:c0 + chunk])
+                self._settle_inflows()          # rows of the previous chunk still on the device
                 net.run(x)
-                # the chunk's steps in blocks: every block's copy (pinned host rows + the
+                # the chunk's outflows in blocks: every block's copy (pinned host rows + the
                 # device's row digests) is queued now; the steps of block b are yielded while
-                # blocks b + 1, ... are still being copied
+                # blocks b + 1, ... are still being copied.  The inflows stay on the device
+                # until a caller reads one (_LazyInflow: the block's inflow rows are fetched then)
                 blocks = []
-                digests = _host_array((2, x.size), np.uint64)
+                digests = _host_array((x.size,), np.uint64)
                 for b0 in range(0, x.size, block):
                     b1 = min(x.size, b0 + block)
                     oo = _host_array((b1 - b0, n), np.float64)
-                    ii = _host_array((b1 - b0, n), np.float64)
-                    tk = net.fetch_outputs_async(b0, b1, oo, ii, digests[0, b0:b1],
-                                                 digests[1, b0:b1])
+                    tk = net.fetch_outputs_async(b0, b1, oo, None, digests[b0:b1], None)
                     pending.append(tk)
-                    blocks.append((b0, oo, ii, tk))
-                for b0, oo, ii, tk in blocks:
+                    blocks.append((b0, oo, _InflowBlock(net, b0, b1, n), tk))
+                for b0, oo, iblk, tk in blocks:
                     net.fetch_wait(tk)
                     pending.remove(tk)
                     for k in range(oo.shape[0]):
@@ -652,27 +734,36 @@ class Muskingum:
                         # revision) and the rest of the horizon is routed step by step from
                         # the state found
                         step = c0 + b0 + k
-                        o_next, i_next = oo[k], ii[k]
-                        if step >= T - 2:
-                            o_next, i_next = o_next.copy(), i_next.copy()
-                        self.o_t_prev, self.i_t_prev = self.o_t_next, self.i_t_next
-                        self.o_t_next, self.i_t_next = o_next, i_next
+                        last = step >= T - 2
+                        o_next = oo[k].copy() if last else oo[k]
+                        i_ref = _LazyInflow(iblk, k, last)
+                        self.o_t_prev = self.o_t_next
+                        d["_i_t_prev"] = d.get("_i_t_next")    # (not materialised)
+                        self.o_t_next = o_next
+                        d["_i_t_next"] = i_ref
                         # (a UTC Timestamp plus a Timedelta: the setter's checks hold)
                         self._datetime = expected_time = self._datetime + timedelta
                         if debug:
                             self.logger.debug(f"Stepped to time {self.datetime}")
                         yield self
-                        h_o, h_i = row_digest(o_next, i_next)
-                        edited = h_o != digests[0, b0 + k] or h_i != digests[1, b0 + k]
-                        if (self.o_t_next is not o_next or self.i_t_next is not i_next or edited
-                                or self._coef_rev[0] != rev or not self._callbacks_idle()
+                        i_now = d.get("_i_t_next")
+                        edited = (self.o_t_next is not o_next or
+                                  int(engine.host_digest(o_next)[0]) != int(digests[b0 + k]))
+                        if not edited and i_now is not i_ref:
+                            # read (materialised) or replaced: an edit unless it is the row
+                            # itself with the device's digest
+                            edited = (i_now is not i_ref.value or
+                                      int(engine.host_digest(i_now)[0]) != i_ref.digest())
+                        if (edited or self._coef_rev[0] != rev or not self._callbacks_idle()
                                 or self.datetime != expected_time
                                 or self.timedelta != timedelta):
+                            self._settle_inflows()
                             yield from self._simulate_steps(dataframe, xp, end_time, kwargs)
                             return
         finally:
             for tk in pending:
                 net.fetch_wait(tk)
+            self._settle_inflows()
 
     def simulate(self, dataframe, start_time=None, end_time=None, o_t_init=None, **kwargs):
         """Route over a time range; returns the ``simulate_iter`` generator (yields ``self``).

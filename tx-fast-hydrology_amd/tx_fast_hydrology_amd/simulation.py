@@ -98,7 +98,14 @@ class Simulation:
 
 class AsyncSimulation(Simulation):
     """Dependency-ordered asyncio driver; ``outputs[name]`` is the outflow frame of each
-    sub-basin (start time row included)."""
+    sub-basin (start time row included).
+
+    Memory note (device DAG): the outflow frames of one ``simulate`` are views into ONE
+    page-locked host block (so all fetches are asynchronous, full-speed copies).  Any frame kept
+    alive keeps that whole block alive, and torch's caching host allocator keeps page-locked
+    memory cached for reuse by later horizons rather than returning it to the OS.  Callers that
+    keep results of large collections for long should copy the frames they keep
+    (``frame.copy()``) and drop the rest."""
 
     async def simulate(self):
         try:
@@ -224,6 +231,7 @@ def _device_dag(sim):
                 return False
     nets = {}
     for name in runs:
+        models[name]._settle_inflows()      # rows a fused horizon left on the session
         net = models[name]._device.session(models[name])
         if not hasattr(net, "add_lateral_correction"):
             return False
