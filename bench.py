@@ -98,7 +98,7 @@ def parse(argv=None, world=None):
     ap.add_argument("--huc8", action="store_true",
                     help="BASELINE configs[0]: one HUC-8 sub-basin (1000 reaches, one outlet, "
                          "deepest path ~100 reaches), deterministic")
-    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow"],
+    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow", "paths"],
                     help="execution path (mcroute.h mc_set_mode)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -276,7 +276,9 @@ def build_workload(args, rank=0, world=1):
         # launches: the multi-launch ensemble shape), the state handed over on the device
         fnet = engine.RoutingNet(end, indeg, heads, slots=getattr(args, "fslots", 256),
                                  tile=getattr(args, "ftile", 64), members=E)
-        fnet.set_mode(getattr(args, "mode", "auto"))
+        # (the one-step modes "dataflow" / "paths" select the analysis plan's member-step path;
+        # the forecast is a multi-step ensemble horizon: launches)
+        fnet.set_mode("launches" if getattr(args, "mode", "auto") == "launches" else "auto")
         fnet.set_coeffs(alpha, beta, chi, gamma)
         fnet.load_forcing(xp, fp)
         enkf.fnet = fnet

@@ -89,7 +89,7 @@ def test_config3_texas_enkf256_member_step_and_analysis():
     ek = wl.enkf
     E = wl.E
     assert E == 256 and ek.m == 500 and np.array_equal(ek.R, 1e-2 * np.eye(500))
-    # one member step: all 256 members bit-exact
+    # one member step: all 256 members bit-exact (auto: the member-dataflow launch at 256)
     net.run(wl.x[0:1])
     assert net.mode()[1] == "dataflow"
     X, I = net.get_state()

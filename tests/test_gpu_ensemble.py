@@ -116,18 +116,24 @@ def test_ensemble_rejects_dataflow_and_bad_shapes():
         net.run(xp[0] + 300e9 * np.arange(1, 5))
 
 
-@pytest.mark.parametrize("n,E,slots,tile", [(3000, 33, 256, 0), (1200, 2, 128, 0),
-                                            (4000, 256, 384, 0), (2500, 137, 192, 0),
-                                            (190_000, 32, 384, 0), (190_000, 32, 192, 16)])
-def test_member_dataflow_single_steps(n, E, slots, tile):
-    """One-step runs of an ensemble (the analysis cycle of the EnKF) as member-dataflow launches:
-    member e of slot d at tick G[d] + e.  Several consecutive one-step runs (interpolated
-    between forcing rows) then a multi-step run must equal every member's serial run."""
+@pytest.mark.parametrize("n,E,slots,tile,mode", [
+    (3000, 33, 256, 0, "dataflow"), (1200, 2, 128, 0, "dataflow"), (4000, 256, 384, 0, "dataflow"),
+    (2500, 137, 192, 0, "dataflow"), (190_000, 32, 384, 0, "dataflow"),
+    (190_000, 32, 192, 16, "dataflow"),
+    (3000, 33, 256, 0, "paths"), (1200, 2, 128, 0, "paths"), (4000, 256, 384, 0, "paths"),
+    (2500, 137, 192, 0, "paths"), (2500, 64, 192, 16, "paths"), (190_000, 32, 192, 16, "paths")])
+def test_member_dataflow_single_steps(n, E, slots, tile, mode):
+    """One-step runs of an ensemble (the analysis cycle of the EnKF) on both one-step paths: the
+    member-dataflow launch (member e of slot d at tick G[d] + e) and the member paths (paths.hip:
+    heavy paths swept by waves, members on the lanes, several member groups beyond 64).  Several
+    consecutive one-step runs (interpolated between forcing rows) then a multi-step run must
+    equal every member's serial run."""
     depth = 1500 if n > 100_000 else 120
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4 if n < 100_000 else 300, depth,
                                                       n + E, E)
     n = end.size
     net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile, members=E)
+    net.set_mode(mode)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
     net.load_forcing(xp, fpe)
@@ -135,10 +141,11 @@ def test_member_dataflow_single_steps(n, E, slots, tile):
     outs_o, outs_i = [], []
     for k in range(5):
         net.run(x[k:k + 1])
-        assert net.mode()[1] == "dataflow", k
+        assert net.mode()[1] == mode, k
         oo, ii = net.fetch_outputs()
         outs_o.append(oo[0])
         outs_i.append(ii[0])
+    net.set_mode("auto")                        # (dataflow mode refuses ensemble horizons)
     net.run(x[5:])
     assert net.mode()[1] == "launches"
     oo, ii = net.fetch_outputs()
@@ -158,7 +165,7 @@ def test_member_dataflow_matches_launches_path():
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(2000, 3, 80, 99, E)
     x = xp[0] + 300e9 * np.arange(1, 4)
     res = []
-    for mode in ("auto", "launches"):
+    for mode in ("dataflow", "launches", "paths"):
         net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=256, members=E)
         net.set_mode(mode)
         net.set_coeffs(*coef)
@@ -168,11 +175,12 @@ def test_member_dataflow_matches_launches_path():
         for k in range(3):
             net.run(x[k:k + 1])
             seq.append(net.fetch_outputs())
-        assert net.mode()[1] == ("dataflow" if mode == "auto" else "launches")
+        assert net.mode()[1] == mode
         res.append((seq, net.get_state()))
-    for (a_o, a_i), (b_o, b_i) in zip(res[0][0], res[1][0]):
-        assert np.array_equal(a_o, b_o) and np.array_equal(a_i, b_i)
-    assert all(np.array_equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    for other in res[1:]:
+        for (a_o, a_i), (b_o, b_i) in zip(res[0][0], other[0]):
+            assert np.array_equal(a_o, b_o) and np.array_equal(a_i, b_i)
+        assert all(np.array_equal(a, b) for a, b in zip(res[0][1], other[1]))
 
 
 def test_copy_state_between_plans_continues_bitexact():

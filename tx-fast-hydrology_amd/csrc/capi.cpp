@@ -26,6 +26,7 @@
 #include "capi_common.hpp"
 #include "digest.hpp"
 #include "kernels.hpp"
+#include "paths.hpp"
 #include "plan.hpp"
 
 #pragma clang fp contract(off)
@@ -190,6 +191,25 @@ struct Net {
 
     // outputs of the last run are the {o, i} pairs of a member-dataflow step (IOb, member windows)
     bool out_io = false;
+    // outputs of the last run (a one-step member-paths run) are the session state itself; a call
+    // that changes the state first copies them aside (keep_outputs: out_saved, outS)
+    bool out_state = false, out_saved = false;
+    DBuf<double> outS;
+
+    // ---- member paths (paths.hip): one-step ensemble runs swept along heavy paths, members on
+    // the lanes; the path plan is built from the schedule plan on first use
+    std::unique_ptr<mcr::PathPlan> pplan;
+    int pplan_state = 0;                 // 1 built, -1 not available for this network
+    DBuf<int32_t> prec, povf, ptask, pseq, pqueue;
+    DBuf<double> Pbuf;
+    DBuf<uint32_t> GRb;
+    size_t gr_words = 0;
+    uint32_t pepoch = 0;
+    bool palpha_stale = true;            // records carry alpha: refreshed after set_coeffs
+    // auto mode sweeps one-step runs of up to this many members along paths (E <= 64: one member
+    // group per wave; larger ensembles keep the member-dataflow launch, whose staging passes are
+    // bandwidth-efficient for them -- mode 3 forces the paths for any E)
+    static constexpr int64_t kPathsAutoMax = 64;
 
     // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
     DBuf<int64_t> mwbase;
@@ -427,6 +447,111 @@ struct Net {
         return ok;
     }
 
+    // the step outputs of a member-paths run are the state: copy them aside before the state
+    // changes (settle_gain, set_state, apply_gain, a state hand-over into this session)
+    void keep_outputs() {
+        if (!out_state) return;
+        const size_t cells = (size_t)(plan.nslots * E);
+        outS.reserve(2 * cells);
+        HIPC(hipMemcpyAsync(outS.p, st_o.p, cells * sizeof(double), hipMemcpyDeviceToDevice,
+                            stream));
+        HIPC(hipMemcpyAsync(outS.p + cells, st_i.p, cells * sizeof(double),
+                            hipMemcpyDeviceToDevice, stream));
+        out_state = false;
+        out_saved = true;
+    }
+    // member-major [E][nslots] source of the step outputs (outflow c = 0, inflow c = 1)
+    const double* state_outputs(int c) const {
+        if (out_saved) return outS.p + (size_t)c * (size_t)(plan.nslots * E);
+        return c == 0 ? st_o.p : st_i.p;
+    }
+
+    bool paths_ready() {
+        if (pplan_state != 0) return pplan_state > 0;
+        pplan_state = -1;
+        auto pp = std::make_unique<mcr::PathPlan>();
+        if (!mcr::build_path_plan(plan, *pp).empty()) return false;
+        std::vector<int32_t> sq((size_t)std::max<int64_t>(plan.nslots, 1), -1);
+        for (int64_t q = 0; q < pp->n; ++q) sq[plan.pos[pp->seq_reach[q]]] = (int32_t)q;
+        prec.upload(pp->rec.data(), pp->rec.size(), stream);
+        povf.upload(pp->ovf.data(), pp->ovf.size(), stream);
+        ptask.upload(pp->task_off.data(), pp->task_off.size(), stream);
+        pseq.upload(sq.data(), sq.size(), stream);
+        sync();                          // (host staging vectors)
+        pplan = std::move(pp);
+        palpha_stale = true;
+        pplan_state = 1;
+        return true;
+    }
+    bool use_paths() {
+        if (E < 2 || mode == 1 || mode == 2 || force_mode == 1) return false;
+        if (mode != 3 && E > kPathsAutoMax) return false;
+        return plan.n > 0 && plan.n < (1ll << 30) && paths_ready();
+    }
+    // one step of all E members (T = 1) along the path plan; the pending analysis increments are
+    // applied in the prep pass; the new state is written in place and IS the step's output
+    void run_paths(const double* Fsrc, int64_t rows, int4 ent) {
+        const mcr::PathPlan& pp = *pplan;
+        const int64_t n = pp.n, groups = (E + mcr::kPathLanes - 1) / mcr::kPathLanes;
+        if (palpha_stale) {
+            HIPC(mcr::launch_path_alpha(prec.p, alpha.p, n, stream));
+            palpha_stale = false;
+        }
+        Pbuf.reserve((size_t)(groups * n * 192));
+        const size_t words = (size_t)pp.n_tasks * (size_t)groups * mcr::kPathLanes * 4;
+        REQUIRE(words * 4 < ((size_t)1 << 31), "network too large for the member paths");
+        if (words > gr_words || pepoch == 0xffffffffu) {
+            GRb.reserve(std::max<size_t>(words, 4));
+            HIPC(hipMemsetAsync(GRb.p, 0, std::max<size_t>(words, 4) * 4, stream));
+            gr_words = std::max(gr_words, words);
+            pepoch = 0;
+        }
+        ++pepoch;
+        pqueue.reserve(1);
+        HIPC(hipMemsetAsync(pqueue.p, 0, sizeof(int32_t), stream));
+        HIPC(mcr::launch_path_prep(Fsrc, rows * plan.nslots, (int)rows, ent, st_o.p, st_i.p,
+                                   beta.p, chi.p, gamma.p, flags.p, pseq.p,
+                                   gain_pending ? Gn.p : nullptr, sup_off.p, sup.p, Pbuf.p,
+                                   plan.nslots, n, E, stream));
+        gain_pending = false;
+        mcr::PathArgs a{};
+        a.rec = prec.p;
+        a.ovf = povf.p;
+        a.task_off = ptask.p;
+        a.P = Pbuf.p;
+        a.st_o = st_o.p;
+        a.st_i = st_i.p;
+        a.GR = GRb.p;
+        a.queue = pqueue.p;
+        a.status = status.p;
+        a.patience = patience;
+        a.ns = plan.nslots;
+        a.n = n;
+        a.n_tasks = pp.n_tasks;
+        a.groups = (int32_t)groups;
+        a.E = (int32_t)E;
+        a.gr_bytes = (uint32_t)(std::max<size_t>(words, 4) * 4);
+        a.epoch = pepoch;
+        if (timing) {
+            ensure_events(2);
+            HIPC(hipEventRecord(events[0], stream));
+        }
+        HIPC(mcr::launch_member_paths(a, std::max(cu_count, 1) * 8, stream));
+        if (timing) {
+            HIPC(hipEventRecord(events[1], stream));
+            HIPC(hipEventSynchronize(events[1]));
+            float ms = 0.f;
+            HIPC(hipEventElapsedTime(&ms, events[0], events[1]));
+            kernel_ms += ms;
+            run_ms += ms;
+            launches += 1;
+        }
+        ++flow_runs;                     // a wait that gave up is reported at the next sync
+        last_flow.valid = false;         // (never re-routed: the state was updated in place)
+        out_state = true;
+        last_path = 3;
+    }
+
     bool members_fit(size_t& lds) {
         if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
@@ -499,6 +624,7 @@ struct Net {
     bool gain_pending = false;
     void settle_gain() {
         if (!gain_pending) return;
+        keep_outputs();
         gain_pending = false;
         HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, plan.nslots,
                                     E, stream));
@@ -509,6 +635,7 @@ struct Net {
         if (plan.n == 0) return;
         settle_state();
         settle_gain();
+        keep_outputs();
         const size_t ns = (size_t)plan.nslots;
         Gn.reserve(ns * E);
         to_slots(gain, Gn, E);
@@ -770,6 +897,7 @@ struct Net {
         to_slots(b, beta);
         to_slots(c, chi);
         to_slots(g, gamma);
+        palpha_stale = true;
         // partial sums pass their fold through, unrouted reaches and padding output 0
         HIPC(mcr::launch_set_slot_coeffs(flags.p, alpha.p, beta.p, chi.p, gamma.p, plan.nslots,
                                          stream));
@@ -781,6 +909,7 @@ struct Net {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
         settle_state();
         gain_pending = false;            // replaced
+        keep_outputs();
         to_slots(o, st_o, E);
         to_slots(i, st_i, E, &stage2);   // its own staging (stream-ordered reuse, no sync)
     }
@@ -869,6 +998,14 @@ struct Net {
         }
         last_path = 0;
         out_io = false;
+        out_state = out_saved = false;
+        if (E > 1 && T == 1 && use_paths()) {
+            // ---- one step of all members along the path plan (paths.hip)
+            settle_state();
+            run_paths(Fsrc, rows, tabh[0]);
+            T_out = T;
+            return;
+        }
         ensure_schedule(T);
         const int64_t nl = (int64_t)cur->off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
@@ -1127,7 +1264,10 @@ struct Net {
         for (int c = 0; c < 2; ++c) {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
-            if (out_io)                    // T = 1: t0 = 0, t1 = 1
+            if (out_state || out_saved)    // T = 1: the state after the step
+                HIPC(mcr::launch_gather_from_slots(state_outputs(c), outT.p, pos.p, n, plan.nslots,
+                                                   E, stream));
+            else if (out_io)               // T = 1: t0 = 0, t1 = 1
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, outT.p, n, E,
                                            stream));
             else {
@@ -1169,7 +1309,10 @@ struct Net {
             uint64_t* dg = c == 0 ? dgo : dgi;
             if (!dst && !dg) continue;
             double* buf = c == 0 ? outT.p : outT2.p;
-            if (out_io)
+            if (out_state || out_saved)
+                HIPC(mcr::launch_gather_from_slots(state_outputs(c), buf, pos.p, n, plan.nslots, E,
+                                                   stream));
+            else if (out_io)
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, buf, n, E, stream));
             else {
                 const OutView ov = out_view();
@@ -1215,7 +1358,10 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            if (out_io)                    // T = 1: [j][0][e] is the step layout
+            if (out_state || out_saved)    // T = 1: [j][0][e] is the step layout
+                HIPC(mcr::launch_gather_from_slots(state_outputs(k), outT.p, pos.p, n, plan.nslots,
+                                                   E, stream));
+            else if (out_io)               // T = 1: [j][0][e] is the step layout
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, k == 1, outT.p, n, E,
                                            stream));
             else {
@@ -1369,6 +1515,25 @@ int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint
         cp(ext_off, P.ext_off);
         cp(ext_src, P.ext_src);
         cp(ext_g, P.ext_g);
+    });
+}
+
+int mc_plan_paths(const void* plan, int64_t* n_tasks, int64_t* n_ovf, int32_t* task_off,
+                  int64_t* seq_reach, int32_t* rec, int32_t* ovf) {
+    return guarded([&] {
+        REQUIRE(plan && n_tasks && n_ovf, "null argument");
+        mcr::PathPlan pp;
+        const std::string err = mcr::build_path_plan(*static_cast<const mcr::Plan*>(plan), pp);
+        if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
+        *n_tasks = pp.n_tasks;
+        *n_ovf = (int64_t)pp.ovf.size();
+        auto cp = [](auto* dst, const auto& v) {
+            if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+        };
+        cp(task_off, pp.task_off);
+        cp(seq_reach, pp.seq_reach);
+        cp(rec, pp.rec);
+        cp(ovf, pp.ovf);
     });
 }
 
@@ -1581,6 +1746,7 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         S->settle_gain();
         D->settle_state();
         D->gain_pending = false;         // its state is replaced
+        D->keep_outputs();
         // order: after the source's pending work, on the destination's stream; the source waits
         // for the copy before it may overwrite its state again
         hipEvent_t ev;
@@ -1616,7 +1782,7 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         REQUIRE(D->E == 1 && S->E == 1, "lateral corrections route single-member sessions");
         REQUIRE(0 <= dst_reach && dst_reach < D->plan.n && 0 <= src_reach && src_reach < S->plan.n,
                 "reach index out of range");
-        REQUIRE(S->T_out > 0 && S->cur && !S->out_io,
+        REQUIRE(S->T_out > 0 && S->cur && !S->out_io && !S->out_state && !S->out_saved,
                 "the source session has no horizon outputs");
         REQUIRE(D->n_rows == S->T_out,
                 "the destination's forcing rows must be the source horizon's steps (one input "
@@ -1752,8 +1918,10 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 2,
-                "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow)");
+        REQUIRE(mode >= 0 && mode <= 3,
+                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow; one-step ensemble runs "
+                "as member-dataflow launches) or 3 (auto with one-step ensemble runs always "
+                "along the member paths)");
         as_net(net)->mode = mode;
     });
 }

@@ -484,8 +484,11 @@ void wavefront_flow(WaveArgs a) {
                     hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
                 }
                 const double f = __hiloint2double(e.w, e.z);
-                // clamped steps (row_lo == row_hi): the row itself (nutils.py:24-27)
-                const double qq = e.x == e.y ? lo : (1.0 - f) * lo + f * hi;
+                // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself
+                // (nutils.py:24-27) also for +-Inf / NaN rows (0 * hi would be NaN); the sign of
+                // a zero q cannot reach the outflow (its update ends in 0 + ...)
+                hi = f == 0.0 ? 0.0 : hi;
+                const double qq = (1.0 - f) * lo + f * hi;
                 return qq;
             };
             double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];

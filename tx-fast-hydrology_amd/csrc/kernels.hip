@@ -206,9 +206,13 @@ void wavefront_det(WaveArgs a) {
                 hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
             }
             const double f = __hiloint2double(e.w, e.z);
-            // clamped steps (row_lo == row_hi) copy the row as the reference does
-            // (nutils.py:24-27): exact for +-Inf / NaN, where (1 - 0) f + 0 f is not
-            const double qq = e.x == e.y ? lo : (1.0 - f) * lo + f * hi;
+            // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself as the
+            // reference copies it (nutils.py:24-27), also for +-Inf / NaN rows, where
+            // (1 - 0) f + 0 f is not (the sign of a zero q cannot reach the outflow, whose
+            // update ends in 0 + ...).  (A select of lo instead costs the dataflow kernel 32
+            // VGPRs in its batched q.)
+            hi = f == 0.0 ? 0.0 : hi;
+            const double qq = (1.0 - f) * lo + f * hi;
             return qq;
         };
         double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
