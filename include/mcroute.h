@@ -270,7 +270,7 @@ int mc_reset_timing(void* net);
  * whole horizon when the network fits the device at once, else launches of `tile` ticks;
  * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit; a
  * one-step ensemble run is a member-dataflow launch); 3: auto, with every one-step ensemble run
- * swept along the member paths (paths.hpp; auto takes them up to 64 members).
+ * swept along the member paths instead (paths.hpp; opt-in: modes 0-2 never take them).
  * last_path: 1 launches, 2 dataflow, 3 member paths (0 before any run). */
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);

@@ -288,14 +288,14 @@ def test_enkf256_large_mean_and_zero_spread_reaches():
     np.testing.assert_allclose(o[rest] - X[rest], G[rest], rtol=0, atol=1e-10 * np.abs(G).max())
 
 
-@pytest.mark.parametrize("E,mode", [(32, "auto"), (256, "auto"), (32, "dataflow"),
+@pytest.mark.parametrize("E,mode", [(32, "auto"), (256, "auto"), (32, "paths"),
                                     (100, "paths")])
 def test_lazy_gain_folded_into_member_step(E, mode):
     """The analysis increments are applied lazily: the next one-step member run applies them
     while it stages its inputs (launch_member_inputs / path_prep with the pending gain) instead
     of a separate apply_gain pass.  An EnKF cycle run that way is bit-identical to the same cycle
     with the gain settled right after every analysis (get_state forces it), outputs included --
-    on both one-step paths (auto: member paths up to 64 members, member dataflow beyond)."""
+    on both one-step paths (auto: the member-dataflow launch; the member paths opt-in)."""
     end = synthetic.river_network(5000, 5, 150, np.random.default_rng(4))
     n = end.size
     m = 25
@@ -320,7 +320,7 @@ def test_lazy_gain_folded_into_member_step(E, mode):
             net.enkf_analysis(s, Ys[k], R)
             if settle:
                 net.get_state()
-        want = mode if mode != "auto" else ("paths" if E <= 64 else "dataflow")
+        want = mode if mode != "auto" else "dataflow"
         assert net.mode()[1] == want
         res.append((net.get_state(), outs))
         net.close()

@@ -206,10 +206,9 @@ struct Net {
     size_t gr_words = 0;
     uint32_t pepoch = 0;
     bool palpha_stale = true;            // records carry alpha: refreshed after set_coeffs
-    // auto mode sweeps one-step runs of up to this many members along paths (E <= 64: one member
-    // group per wave; larger ensembles keep the member-dataflow launch, whose staging passes are
-    // bandwidth-efficient for them -- mode 3 forces the paths for any E)
-    static constexpr int64_t kPathsAutoMax = 64;
+    // the member paths are opt-in (mode 3): on the bench networks the member-dataflow launch is
+    // faster at every E measured (Texas E=32 0.70 vs 0.38 ms per step;
+    // the single-wave node chain costs ~270 ns a node against the dataflow's shared tick)
 
     // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
     DBuf<int64_t> mwbase;
@@ -484,8 +483,7 @@ struct Net {
         return true;
     }
     bool use_paths() {
-        if (E < 2 || mode == 1 || mode == 2 || force_mode == 1) return false;
-        if (mode != 3 && E > kPathsAutoMax) return false;
+        if (E < 2 || mode != 3 || force_mode == 1) return false;
         return plan.n > 0 && plan.n < (1ll << 30) && paths_ready();
     }
     // one step of all E members (T = 1) along the path plan; the pending analysis increments are
@@ -536,7 +534,7 @@ struct Net {
             ensure_events(2);
             HIPC(hipEventRecord(events[0], stream));
         }
-        HIPC(mcr::launch_member_paths(a, std::max(cu_count, 1) * 8, stream));
+        HIPC(mcr::launch_member_paths(a, std::max(cu_count, 1) * 2, stream));
         if (timing) {
             HIPC(hipEventRecord(events[1], stream));
             HIPC(hipEventSynchronize(events[1]));
