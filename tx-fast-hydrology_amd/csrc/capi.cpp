@@ -990,6 +990,20 @@ struct Net {
             const int last = std::max(tabh[t2].x, tabh[t2].y);
             dense = last - tabh[t].x + 1 > 3;
         }
+        // unclamped steps [qc0, qc1]: clamped steps ({row, row, 0}, a row copy) are a prefix
+        // and a suffix of the horizon (monotonic step times); the kernels mask the high row
+        // only in chunks that reach them.  Any other pattern masks every chunk (safe).
+        int32_t qc0 = 0, qc1 = (int32_t)T - 1;
+        {
+            auto clamped = [&](int64_t t) { return tabh[t].x == tabh[t].y; };
+            int64_t f = 0, l = T - 1;
+            while (f < T && clamped(f)) ++f;
+            while (l >= f && clamped(l)) --l;
+            bool mid = false;
+            for (int64_t t = f; t <= l && !mid; ++t) mid = clamped(t);
+            qc0 = mid ? (int32_t)T : (int32_t)f;
+            qc1 = mid ? -1 : (int32_t)l;
+        }
         if (tabh != stab_host) {           // repeated horizons reuse the uploaded table
             upload_async(stab, tabh.data(), tabh.size());
             stab_host = tabh;
@@ -1026,6 +1040,8 @@ struct Net {
         a.st_i = st_i.p;
         a.F = Fsrc;
         a.stab = stab.p;
+        a.qc0 = qc0;
+        a.qc1 = qc1;
         a.wg_gmin = wg_gmin.p;
         a.wg_gmax = wg_gmax.p;
         a.wbase = cur->wbase.p;

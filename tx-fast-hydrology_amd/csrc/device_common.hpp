@@ -41,10 +41,10 @@ __device__ __forceinline__ double lds_f64(const char* lds, unsigned byte) {
 struct Slot {
     int64_t d;            // node slot
     int G;                // tick of step 0 (huge when the slot has no work in this launch)
-    int Ga;               // G for the state update: huge for partial sums, whose state stays 0
-                          // (their update 0 + (((1 I + 0 Ip) + 0 Op) + 0 q) is then exactly I,
-                          // also for non-finite I: 0 Ip with Ip = +-Inf would be NaN)
-    bool routed, psum, unr, xsrc;   // unr: never processed by the reference walk (o = 0)
+    // psum: a partial sum, whose state is never updated -- it stays 0, so its update
+    // 0 + (((1 I + 0 Ip) + 0 Op) + 0 q) is exactly I, also for non-finite I (0 Ip with
+    // Ip = +-Inf would be NaN).  unr: never processed by the reference walk (o = 0)
+    bool routed, psum, unr, xsrc;
     double al, be, ch, ga, op, ip;
     int cnt;
     unsigned ubase[kUpInline];  // LDS byte base of each input
@@ -65,7 +65,6 @@ __device__ __forceinline__ void load_slot(Slot& s, const WaveArgs& a, int64_t d,
     s.G = live ? Gr : (1 << 29);                        // never active when not live
     s.routed = fl == kSlotRouted;
     s.psum = fl == kSlotSum;
-    s.Ga = s.psum ? (1 << 29) : s.G;
     s.unr = fl == kSlotUnrouted;
     // state after the last step this slot ran in an earlier launch (or the initial state)
     s.op = a.st_o[mem * a.mS + d];
@@ -136,5 +135,18 @@ __device__ __forceinline__ double fold_values(const double* v, bool chained, boo
     return I;
 }
 
+}  // namespace dev
+}  // namespace mcr
+
+namespace mcr {
+namespace dev {
+// does any step of this lane's chunk [kc, kc + kChunk) fall outside the unclamped range?
+// (inactive ticks excluded; wave-uniform after __any)
+__device__ __forceinline__ bool chunk_clamped(int kc, int G, int T, int qc0, int qc1) {
+    int t0 = kc - G, t1 = t0 + kChunk - 1;
+    t0 = t0 < 0 ? 0 : t0;
+    t1 = t1 >= T ? T - 1 : t1;
+    return t0 <= t1 && (t0 < qc0 || t1 > qc1);
+}
 }  // namespace dev
 }  // namespace mcr

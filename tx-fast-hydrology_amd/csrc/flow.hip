@@ -473,7 +473,7 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int u = 0; u < kUpInline; ++u)
                     m[p][u] = S[p].uext[u] ? S[p].ubase[u] + sb : S[p].ubase[u];
-            auto q_of = [&](int p, int j) -> double {
+            auto q_of = [&](int p, int j, bool mask) -> double {
                 const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
                 double lo, hi;
                 if (DENSE && slow) {
@@ -487,16 +487,31 @@ void wavefront_flow(WaveArgs a) {
                 // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself
                 // (nutils.py:24-27) also for +-Inf / NaN rows (0 * hi would be NaN); the sign of
                 // a zero q cannot reach the outflow (its update ends in 0 + ...)
-                hi = f == 0.0 ? 0.0 : hi;
+                if (mask) hi = f == 0.0 ? 0.0 : hi;
                 const double qq = (1.0 - f) * lo + f * hi;
                 return qq;
             };
+            // clamped steps (a prefix / suffix of the horizon) need the masked high row; the
+            // chunks that reach none -- all of them when the forcing covers the horizon -- skip
+            // the mask (a select per value: +6 % on the det horizon)
+            bool clq = false;
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+                clq = clq || dev::chunk_clamped(kc, S[p].G, T, a.qc0, a.qc1);
+            clq = __any(clq);
             double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
             if constexpr (kBatchQ) {
+                if (clq) {
 #pragma unroll
-                for (int j = 0; j < kChunk; ++j)
+                    for (int j = 0; j < kChunk; ++j)
 #pragma unroll
-                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j);
+                        for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, true);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kChunk; ++j)
+#pragma unroll
+                        for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, false);
+                }
                 if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
             }
 #pragma unroll
@@ -507,7 +522,7 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     if constexpr (kBatchQ) qv[p] = qb[p][i];
-                    else qv[p] = q_of(p, i);
+                    else qv[p] = q_of(p, i, clq);
                 }
                 double vin[K][kUpInline];
 #pragma unroll
@@ -516,7 +531,8 @@ void wavefront_flow(WaveArgs a) {
                 double prev = 0.0;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    const bool act = (unsigned)(k - S[p].Ga) < (unsigned)T;
+                    // partial sums keep a zero state (Slot::psum)
+                    const bool act = (unsigned)(k - S[p].G) < (unsigned)T && !S[p].psum;
                     const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
                     const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
                                               S[p].ch * S[p].op) + S[p].ga * qv[p]);

@@ -195,7 +195,7 @@ void wavefront_det(WaveArgs a) {
                 m[p][u] = S[p].uext[u] ? S[p].ubase[u] + 8u * c - 8u : S[p].ubase[u];
         // lateral inflow of position p at tick j of the chunk, interpolate_sample
         // (nutils.py:23-33); it does not depend on the routing state (off the tick's chain)
-        auto q_of = [&](int p, int j) -> double {
+        auto q_of = [&](int p, int j, bool mask) -> double {
             const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
             double lo, hi;
             if (DENSE && slow) {
@@ -211,16 +211,28 @@ void wavefront_det(WaveArgs a) {
             // (1 - 0) f + 0 f is not (the sign of a zero q cannot reach the outflow, whose
             // update ends in 0 + ...).  (A select of lo instead costs the dataflow kernel 32
             // VGPRs in its batched q.)
-            hi = f == 0.0 ? 0.0 : hi;
+            if (mask) hi = f == 0.0 ? 0.0 : hi;
             const double qq = (1.0 - f) * lo + f * hi;
             return qq;
         };
+        // the masked high row only in chunks that reach clamped steps (flow.hip)
+        bool clq = false;
+#pragma unroll
+        for (int p = 0; p < K; ++p) clq = clq || dev::chunk_clamped(kc, S[p].G, T, a.qc0, a.qc1);
+        clq = __any(clq);
         double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
         if constexpr (kBatchQ) {
+            if (clq) {
 #pragma unroll
-            for (int j = 0; j < kChunk; ++j)
+                for (int j = 0; j < kChunk; ++j)
 #pragma unroll
-                for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j);
+                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, true);
+            } else {
+#pragma unroll
+                for (int j = 0; j < kChunk; ++j)
+#pragma unroll
+                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, false);
+            }
             if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
         }
 #pragma unroll
@@ -237,7 +249,7 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 if constexpr (kBatchQ) qv[p] = qb[p][i];
-                else qv[p] = q_of(p, i);
+                else qv[p] = q_of(p, i, clq);
             }
             double vin[K][kUpInline];
 #pragma unroll
@@ -248,7 +260,7 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 act[p] = (unsigned)(k - S[p].G) < (unsigned)T;
-                const bool upd = (unsigned)(k - S[p].Ga) < (unsigned)T;   // not partial sums
+                const bool upd = act[p] && !S[p].psum;   // partial sums keep a zero state
                 const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
                 const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
                                           S[p].ch * S[p].op) + S[p].ga * qv[p]);

@@ -106,6 +106,9 @@ struct WaveArgs {
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
+    // steps outside [qc0, qc1] may be clamped (row copies, frac 0: nutils.py:24-27); the
+    // interpolation masks the high row only in chunks that reach them (host: clamp_range)
+    int32_t qc0, qc1;
 };
 
 // LDS bytes of the multi-launch kernel for `slots` lanes (chain * slots node slots): the
