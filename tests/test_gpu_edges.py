@@ -153,3 +153,47 @@ def test_non_finite_inputs_match_reference(mode):
     wi, wo = orc.ax_bu(heads, end, *coef, i0, o0, q, indeg)
     assert _same(o1, wo) and _same(i1, wi)
     net.close()
+
+
+@pytest.mark.parametrize("mode", ["launches", "auto"])
+def test_overflow_through_partial_sums_matches_reference(mode):
+    """Finite inputs whose fold overflows inside the partial sums of a high fan-in reach.  The
+    resident kernel's fast form (finite state and forcing: partial sums carry a state, exact for
+    finite values) reports the non-finite partial sum at the end of the horizon and the horizon
+    is re-routed from its input state in the exact form: every cell equals the oracle's (+Inf
+    from the overflow, NaN from Inf - Inf), and a set_state with finite values re-arms the fast
+    form."""
+    end = np.array([1, 2, 1, 5, 5, 5, 1, 3] + [5] * 6, dtype=np.int64)
+    n = end.size
+    start = np.arange(n, dtype=np.int64)
+    indeg = orc.compute_indegree(start, end)
+    heads = start[indeg == 0]
+    coef = orc.muskingum_coeffs(np.full(n, 3600.0), np.full(n, 0.2), 300.0)
+    o0 = np.linspace(1.0, 2.0, n)
+    i0 = orc.init_inflows(start, end, o0)
+    xp = (1.7e18 + 3600e9 * np.arange(4)).astype(float)
+    fp = np.full((4, n), 0.5)
+    fp[1:, 8:11] = 1.2e308                  # three huge tributaries: their sum overflows
+    fp[2:, 12] = -1.5e308                   # ... and one huge negative one: Inf - Inf later
+    x = xp[0] + 300e9 * np.arange(1, 41)
+    want_o, want_i, want_so, want_si = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    assert not np.isfinite(want_o[:, 5]).all() and np.isfinite(fp).all()
+    net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16)
+    net.set_mode(mode)
+    net.set_coeffs(*coef)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fp)
+    net.run(x)
+    got_o, got_i = net.fetch_outputs()
+    assert _same(got_o, want_o) and _same(got_i, want_i)
+    so, si = net.get_state()
+    assert _same(so, want_so) and _same(si, want_si)
+    # finite state again: the next horizon runs in the fast form (and is exact: no overflow)
+    fp2 = np.full((4, n), 0.5)
+    net.set_state(o0, i0)
+    net.load_forcing(xp, fp2)
+    net.run(x)
+    w2 = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp2)
+    g2 = net.fetch_outputs()
+    assert _same(g2[0], w2[0]) and _same(g2[1], w2[1])
+    net.close()

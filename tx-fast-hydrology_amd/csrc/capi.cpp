@@ -174,6 +174,11 @@ struct Net {
     size_t xg_words = 0;
     uint32_t epoch = 0;
     DBuf<int32_t> status;
+    // non-finite flags of the state and the forcing (WaveArgs::nf): set by the flag kernels
+    // when either is loaded, by a kernel epilogue that leaves a non-finite state, and
+    // conservatively by every other state writer (mark_state)
+    DBuf<int32_t> nf;
+    void mark_state() { HIPC(hipMemsetAsync(nf.p, 1, 1, stream)); }
     int32_t* status_host = nullptr;  // pinned mirror, read at sync()
     int flow_runs = 0;               // dataflow launches since the status word was last read
     // the last dataflow horizon of one member, re-routed with launches when its waits gave up
@@ -346,6 +351,8 @@ struct Net {
         }
         status.reserve(1);
         HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
+        nf.reserve(2);                   // {state, forcing}: a zero state and no forcing yet
+        HIPC(hipMemsetAsync(nf.p, 0, 2 * sizeof(int32_t), stream));
         HIPC(hipHostMalloc(reinterpret_cast<void**>(&status_host), sizeof(int32_t),
                            hipHostMallocDefault));
         *status_host = 0;
@@ -399,15 +406,20 @@ struct Net {
             if (*status_host != 0) {
                 *status_host = 0;
                 HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
+                const int32_t why = *status_host;
                 if (runs == 1 && last_flow.valid) {
-                    // the device was shared (another stream held CUs the resident launch
-                    // needed): route the same horizon again from its input state with launches
+                    // bit 0: the device was shared (another stream held CUs the resident launch
+                    // needed); bit 1: a partial sum met a non-finite value in the fast form.
+                    // Route the same horizon again from its input state with launches (exact)
                     st_o.swap(st_o2);
                     st_i.swap(st_i2);
                     last_flow.valid = false;
                     ++reroutes;
-                    std::fprintf(stderr, "[mcroute] dataflow launch gave up waiting for upstream "
-                                         "workgroups; the horizon was re-routed with launches\n");
+                    if (why & 1)
+                        std::fprintf(stderr, "[mcroute] dataflow launch gave up waiting for "
+                                             "upstream workgroups; the horizon was re-routed "
+                                             "with launches\n");
+                    mark_state();
                     force_mode = 1;
                     try {
                         run_tables(last_flow.T, last_flow.F, last_flow.rows, last_flow.tab);
@@ -419,9 +431,16 @@ struct Net {
                     HIPC(hipStreamSynchronize(stream));
                     return;
                 }
-                throw Fail(MC_E_HIP, "dataflow kernel: a wait for upstream results gave up "
-                                     "(outputs of the runs since the last synchronisation are "
-                                     "invalid)");
+                if (why & 1)
+                    throw Fail(MC_E_HIP, "dataflow kernel: a wait for upstream results gave up "
+                                         "(outputs of the runs since the last synchronisation "
+                                         "are invalid)");
+                mark_state();
+                throw Fail(MC_E_STATE, "dataflow kernel: a partial sum met a non-finite value "
+                                       "produced from finite inputs (overflow) in the fast form; "
+                                       "the outputs of the runs since the last synchronisation "
+                                       "may differ from the reference's there (set the state "
+                                       "again and re-run: the next run is exact)");
             }
         }
     }
@@ -535,6 +554,7 @@ struct Net {
             HIPC(hipEventRecord(events[0], stream));
         }
         HIPC(mcr::launch_member_paths(a, std::max(cu_count, 1) * 2, stream));
+        mark_state();
         if (timing) {
             HIPC(hipEventRecord(events[1], stream));
             HIPC(hipEventSynchronize(events[1]));
@@ -626,6 +646,7 @@ struct Net {
         gain_pending = false;
         HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, plan.nslots,
                                     E, stream));
+        mark_state();
     }
 
     void apply_gain(const double* gain) {
@@ -639,6 +660,7 @@ struct Net {
         to_slots(gain, Gn, E);
         HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p,
                                     plan.nslots, E, stream));
+        mark_state();
         sync();
     }
 
@@ -883,6 +905,7 @@ struct Net {
             b->reserve(ns * m);
             HIPC(hipMemsetAsync(b->p, 0, ns * m * sizeof(double), stream));
         }
+        HIPC(hipMemsetAsync(nf.p, 0, sizeof(int32_t), stream));   // a zero state
         n_rows = 0;                    // forcing and outputs are per member: load again
         T_out = 0;
         sync();
@@ -910,6 +933,9 @@ struct Net {
         keep_outputs();
         to_slots(o, st_o, E);
         to_slots(i, st_i, E, &stage2);   // its own staging (stream-ordered reuse, no sync)
+        HIPC(hipMemsetAsync(nf.p, 0, sizeof(int32_t), stream));
+        HIPC(mcr::launch_flag_nonfinite(st_o.p, plan.nslots * E, nf.p, stream));
+        HIPC(mcr::launch_flag_nonfinite(st_i.p, plan.nslots * E, nf.p, stream));
     }
 
     // Per-horizon layout: active workgroups of every launch and the output windows (cached
@@ -1040,6 +1066,7 @@ struct Net {
         a.st_i = st_i.p;
         a.F = Fsrc;
         a.stab = stab.p;
+        a.nf = nf.p;
         a.qc0 = qc0;
         a.qc1 = qc1;
         a.wg_gmin = wg_gmin.p;
@@ -1109,6 +1136,7 @@ struct Net {
                                               stream));
                 if (timing) HIPC(hipEventRecord(events[1], stream));
                 HIPC(mcr::launch_member_unpack(IOp, mw, st_o.p, st_i.p, plan.nslots, E, stream));
+                mark_state();
                 out_io = true;             // the step's outputs stay in IO (fetch)
                 ++flow_runs;
                 last_flow.valid = false;       // member runs update the state in place
@@ -1223,6 +1251,8 @@ struct Net {
         st.upload(fp, cells, stream);
         HIPC(mcr::launch_forcing_to_slots(st.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
                                           stream, reach_major));
+        HIPC(hipMemsetAsync(nf.p + 1, 0, sizeof(int32_t), stream));
+        HIPC(mcr::launch_flag_nonfinite(F.p, rows * plan.nslots * E, nf.p + 1, stream));
         // a copy from pageable host memory has read the caller's array when it returns, and the
         // persistent staging is reused stream-ordered: only the temporary staging must be
         // drained before it is freed, and a page-locked source (an asynchronous copy) read
@@ -1781,6 +1811,7 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
             HIPC(mcr::launch_permute_slots(from.p, to.p, map, S->plan.nslots, D->plan.nslots, E,
                                            D->stream));
         }
+        D->mark_state();
         HIPC(hipEventRecord(ev, D->stream));
         HIPC(hipStreamWaitEvent(S->stream, ev, 0));
     });
@@ -1815,6 +1846,8 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, S->row_width(),
                                             o_start, alpha, beta, gamma, D->F.p, D->plan.nslots,
                                             D->plan.pos[dst_reach], S->T_out, D->stream));
+        HIPC(mcr::launch_flag_nonfinite(D->F.p, D->n_rows * D->plan.nslots, D->nf.p + 1,
+                                        D->stream));
         HIPC(hipEventRecord(ev, D->stream));
         HIPC(hipStreamWaitEvent(S->stream, ev, 0));
     });

@@ -443,6 +443,18 @@ void wavefront_flow(WaveArgs a) {
         // K <= 2 forms the whole chunk's values up front; longer lanes form them per tick
         // (register budget)
         constexpr bool kBatchQ = K <= 2;
+        // partial sums keep a zero state only when a non-finite value may occur (flags of the
+        // session's state and forcing): their update 0 + (((1 I + 0 Ip) + 0 Op) + 0 q) is I
+        // exactly for any finite state, and the select costs the common form ~6 % (same box).
+        // A partial sum that meets a non-finite value in the fast form anyway (an overflow of
+        // finite inputs) reports it, and the host re-routes the horizon exactly (sync()).
+        const bool exact = a.nf == nullptr ||
+                           __hip_atomic_load(a.nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                           __hip_atomic_load(a.nf + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        bool anyps = false;                                 // a partial sum in this wave
+#pragma unroll
+        for (int p = 0; p < K; ++p) anyps = anyps || S[p].psum;
+        anyps = __any(anyps) && exact;
         for (int kc = kb; kc < wend; kc += kChunk) {
             const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
             unsigned frp[K], tp[K];
@@ -473,92 +485,99 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int u = 0; u < kUpInline; ++u)
                     m[p][u] = S[p].uext[u] ? S[p].ubase[u] + sb : S[p].ubase[u];
-            auto q_of = [&](int p, int j, bool mask) -> double {
-                const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
-                double lo, hi;
-                if (DENSE && slow) {
-                    lo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
-                    hi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
-                } else {
-                    lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
-                    hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
-                }
-                const double f = __hiloint2double(e.w, e.z);
-                // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself
-                // (nutils.py:24-27) also for +-Inf / NaN rows (0 * hi would be NaN); the sign of
-                // a zero q cannot reach the outflow (its update ends in 0 + ...)
-                if (mask) hi = f == 0.0 ? 0.0 : hi;
-                const double qq = (1.0 - f) * lo + f * hi;
-                return qq;
-            };
-            // clamped steps (a prefix / suffix of the horizon) need the masked high row; the
-            // chunks that reach none -- all of them when the forcing covers the horizon -- skip
-            // the mask (a select per value: +6 % on the det horizon)
+            // clamped steps (a prefix / suffix of the horizon) need the masked high row, and
+            // partial-sum slots a frozen state; the chunk runs in one of four straight-line
+            // forms, so the common one (no clamped step, no partial sum in the wave) carries
+            // neither select (with them in every tick: +9 % on the det horizon, same box)
             bool clq = false;
 #pragma unroll
             for (int p = 0; p < K; ++p)
                 clq = clq || dev::chunk_clamped(kc, S[p].G, T, a.qc0, a.qc1);
             clq = __any(clq);
-            double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
-            if constexpr (kBatchQ) {
-                if (clq) {
-#pragma unroll
-                    for (int j = 0; j < kChunk; ++j)
-#pragma unroll
-                        for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, true);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < kChunk; ++j)
-#pragma unroll
-                        for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, false);
-                }
-                if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
-            }
-#pragma unroll
-            for (int i = 0; i < kChunk; ++i) {
-                const unsigned rd = (unsigned)((i + 7) & 7) * PL;   // plane of tick k - 1
-                const int k = kc + i;
-                double qv[K];
-#pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    if constexpr (kBatchQ) qv[p] = qb[p][i];
-                    else qv[p] = q_of(p, i, clq);
-                }
-                double vin[K][kUpInline];
-#pragma unroll
-                for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
-                double ov[K];
-                double prev = 0.0;
-#pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    // partial sums keep a zero state (Slot::psum)
-                    const bool act = (unsigned)(k - S[p].G) < (unsigned)T && !S[p].psum;
-                    const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                    const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
-                                              S[p].ch * S[p].op) + S[p].ga * qv[p]);
-                    const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
-                    S[p].op = act ? o : S[p].op;
-                    S[p].ip = act ? I : S[p].ip;
-                    ov[p] = o;
-                    prev = o;
-                }
-#pragma unroll
-                for (int p = 0; p < K; ++p)
-                    *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
-                // the tick's outputs reach the output window through the helper wave (plane
-                // k & 7 -> window row, copy_row; Texas det 0.515 -> 0.502 ms); the cross-cluster
-                // values leave from here (moving them to the helper too: 0.524, the helper's
-                // tick got longer than the compute waves')
-#pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T) {
-                        const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
-                        const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32), epoch};
-                        __builtin_amdgcn_raw_buffer_store_b128(
-                            gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
+            auto run_chunk = [&](auto mtag, auto ptag) {
+                constexpr bool MASKQ = decltype(mtag)::value, PSUM = decltype(ptag)::value;
+                auto q_of = [&](int p, int j) -> double {
+                    const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
+                    double lo, hi;
+                    if (DENSE && slow) {
+                        lo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
+                        hi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
+                    } else {
+                        lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
+                        hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
                     }
+                    const double f = __hiloint2double(e.w, e.z);
+                    // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself
+                    // (nutils.py:24-27) also for +-Inf / NaN rows (0 * hi would be NaN); the
+                    // sign of a zero q cannot reach the outflow (its update ends in 0 + ...)
+                    if constexpr (MASKQ) hi = f == 0.0 ? 0.0 : hi;
+                    const double qq = (1.0 - f) * lo + f * hi;
+                    return qq;
+                };
+                double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
+                if constexpr (kBatchQ) {
+#pragma unroll
+                    for (int j = 0; j < kChunk; ++j)
+#pragma unroll
+                        for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j);
+                    if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);
                 }
-                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < kChunk; ++i) {
+                    const unsigned rd = (unsigned)((i + 7) & 7) * PL;   // plane of tick k - 1
+                    const int k = kc + i;
+                    double qv[K];
+#pragma unroll
+                    for (int p = 0; p < K; ++p) {
+                        if constexpr (kBatchQ) qv[p] = qb[p][i];
+                        else qv[p] = q_of(p, i);
+                    }
+                    double vin[K][kUpInline];
+#pragma unroll
+                    for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
+                    double ov[K];
+                    double prev = 0.0;
+#pragma unroll
+                    for (int p = 0; p < K; ++p) {
+                        bool act = (unsigned)(k - S[p].G) < (unsigned)T;
+                        if constexpr (PSUM) act = act && !S[p].psum;   // zero state (Slot::psum)
+                        const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
+                        const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
+                                                  S[p].ch * S[p].op) + S[p].ga * qv[p]);
+                        const double o = rr;   // psum / unrouted / pad: set_slot_coeffs
+                        S[p].op = act ? o : S[p].op;
+                        S[p].ip = act ? I : S[p].ip;
+                        ov[p] = o;
+                        prev = o;
+                    }
+#pragma unroll
+                    for (int p = 0; p < K; ++p)
+                        *reinterpret_cast<double*>(lds + own[p] + (unsigned)i * PL) = ov[p];
+                    // the tick's outputs reach the output window through the helper wave (plane
+                    // k & 7 -> window row, copy_row; Texas det 0.515 -> 0.502 ms); the
+                    // cross-cluster values leave from here (moving them to the helper too: 0.524,
+                    // the helper's tick got longer than the compute waves')
+#pragma unroll
+                    for (int p = 0; p < K; ++p) {
+                        if (S[p].xsrc && (unsigned)(k - S[p].G) < (unsigned)T) {
+                            const uint64_t bits = (uint64_t)__double_as_longlong(ov[p]);
+                            const u32x4 gv = {(unsigned)bits, epoch, (unsigned)(bits >> 32),
+                                              epoch};
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
+                        }
+                    }
+                    __syncthreads();
+                }
+            };
+            using yes = std::true_type;
+            using no = std::false_type;
+            if (clq) {
+                if (anyps) run_chunk(yes{}, yes{});
+                else run_chunk(yes{}, no{});
+            } else {
+                if (anyps) run_chunk(no{}, yes{});
+                else run_chunk(no{}, no{});
             }
 #pragma unroll
             for (int p = 0; p < K; ++p) {
@@ -571,11 +590,22 @@ void wavefront_flow(WaveArgs a) {
         }
         // session state after the horizon; never-processed reaches hold o = 0 (nutils.py:68:
         // the kernel's own value for them, 0 q + ..., is NaN for non-finite inputs)
+        bool nonfin = false, psum_hit = false;
 #pragma unroll
         for (int p = 0; p < K; ++p) {
-            a.st_o_out[S[p].d] = S[p].unr ? 0.0 : S[p].op;
+            const double so = S[p].unr ? 0.0 : S[p].op;
+            a.st_o_out[S[p].d] = so;
             a.st_i_out[S[p].d] = S[p].ip;
+            const bool bad = !__builtin_isfinite(so) || !__builtin_isfinite(S[p].ip);
+            nonfin = nonfin || bad;
+            // fast form: a partial sum's state that went non-finite stays non-finite (0 x it is
+            // NaN from then on), so the end of the horizon sees every such case
+            psum_hit = psum_hit || (!exact && S[p].psum && bad);
         }
+        if (a.nf && __any(nonfin) && (lid & 63) == 0)
+            __hip_atomic_store(a.nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__any(psum_hit) && (lid & 63) == 0)
+            __hip_atomic_fetch_or(a.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (a.trace && tid == 0) {
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;

@@ -15,6 +15,8 @@
 //   o = 0 + (((alpha*I + beta*I_prev) + chi*o_prev) + gamma*q)            nutils.py:80-83
 //   q = (1 - frac) * f[ix-1] + frac * f[ix]   (or a row copy at the ends)  nutils.py:23-33
 #include "kernels.hpp"
+
+#include <algorithm>
 #include "plan.hpp"
 #include "device_common.hpp"
 
@@ -155,6 +157,10 @@ void wavefront_det(WaveArgs a) {
     const int64_t c_loop = a.trace ? clock64() : 0;
 
     constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
+    bool anyps = false;                                 // a partial sum in this wave
+#pragma unroll
+    for (int p = 0; p < K; ++p) anyps = anyps || S[p].psum;
+    anyps = __any(anyps);
     for (int c = 0; c < tile; c += kChunk) {
         const int kc = k0 + c;
         // this chunk's forcing rows -> the slots' LDS rows (private: no barrier needed)
@@ -193,104 +199,111 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int u = 0; u < kUpInline; ++u)
                 m[p][u] = S[p].uext[u] ? S[p].ubase[u] + 8u * c - 8u : S[p].ubase[u];
-        // lateral inflow of position p at tick j of the chunk, interpolate_sample
-        // (nutils.py:23-33); it does not depend on the routing state (off the tick's chain)
-        auto q_of = [&](int p, int j, bool mask) -> double {
-            const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
-            double lo, hi;
-            if (DENSE && slow) {
-                lo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
-                hi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
-            } else {
-                lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
-                hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
-            }
-            const double f = __hiloint2double(e.w, e.z);
-            // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself as the
-            // reference copies it (nutils.py:24-27), also for +-Inf / NaN rows, where
-            // (1 - 0) f + 0 f is not (the sign of a zero q cannot reach the outflow, whose
-            // update ends in 0 + ...).  (A select of lo instead costs the dataflow kernel 32
-            // VGPRs in its batched q.)
-            if (mask) hi = f == 0.0 ? 0.0 : hi;
-            const double qq = (1.0 - f) * lo + f * hi;
-            return qq;
-        };
-        // the masked high row only in chunks that reach clamped steps (flow.hip)
+        // the masked high row only in chunks that reach clamped steps, and a frozen state only
+        // in waves with partial sums: four straight-line forms of the chunk (flow.hip)
         bool clq = false;
 #pragma unroll
         for (int p = 0; p < K; ++p) clq = clq || dev::chunk_clamped(kc, S[p].G, T, a.qc0, a.qc1);
         clq = __any(clq);
-        double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
-        if constexpr (kBatchQ) {
-            if (clq) {
+        auto run_chunk = [&](auto mtag, auto ptag) {
+            constexpr bool MASKQ = decltype(mtag)::value, PSUM = decltype(ptag)::value;
+            // lateral inflow of position p at tick j of the chunk, interpolate_sample
+            // (nutils.py:23-33); it does not depend on the routing state (off the tick's chain)
+            auto q_of = [&](int p, int j) -> double {
+                const int4 e = *reinterpret_cast<const int4*>(lds + tp[p] + 16u * j);
+                double lo, hi;
+                if (DENSE && slow) {
+                    lo = Fm[(int64_t)clamp_row(e.x < 0 ? 0 : e.x, nrow) * ns + S[p].d];
+                    hi = Fm[(int64_t)clamp_row(e.y < 0 ? 0 : e.y, nrow) * ns + S[p].d];
+                } else {
+                    lo = lds_f64(lds, frp[p] + 8u * (unsigned)e.x);
+                    hi = lds_f64(lds, frp[p] + 8u * (unsigned)e.y);
+                }
+                const double f = __hiloint2double(e.w, e.z);
+                // clamped steps (frac = 0, row_lo == row_hi): lo + 0 * 0 -- the row itself as the
+                // reference copies it (nutils.py:24-27), also for +-Inf / NaN rows, where
+                // (1 - 0) f + 0 f is not (the sign of a zero q cannot reach the outflow, whose
+                // update ends in 0 + ...).  (A select of lo instead costs the dataflow kernel 32
+                // VGPRs in its batched q.)
+                if constexpr (MASKQ) hi = f == 0.0 ? 0.0 : hi;
+                const double qq = (1.0 - f) * lo + f * hi;
+                return qq;
+            };
+            double qb[kBatchQ ? K : 1][kBatchQ ? kChunk : 1];
+            if constexpr (kBatchQ) {
 #pragma unroll
                 for (int j = 0; j < kChunk; ++j)
 #pragma unroll
-                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, true);
-            } else {
-#pragma unroll
-                for (int j = 0; j < kChunk; ++j)
-#pragma unroll
-                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j, false);
+                    for (int p = 0; p < K; ++p) qb[p][j] = q_of(p, j);
+                if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
             }
-            if (DENSE && slow) __builtin_amdgcn_s_waitcnt(0);  // settle the direct loads here
-        }
 #pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-            if (i & 1) {
+            for (int i = 0; i < kChunk; ++i) {
+                if (i & 1) {
 #pragma unroll
-                for (int p = 0; p < K; ++p)
+                    for (int p = 0; p < K; ++p)
 #pragma unroll
-                    for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uext[u] ? 16u : 0u;
-            }
-            const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
-            const int k = kc + i;
-            double qv[K];
-#pragma unroll
-            for (int p = 0; p < K; ++p) {
-                if constexpr (kBatchQ) qv[p] = qb[p][i];
-                else qv[p] = q_of(p, i, clq);
-            }
-            double vin[K][kUpInline];
-#pragma unroll
-            for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
-            double ov[K];
-            bool act[K];
-            double prev = 0.0;
-#pragma unroll
-            for (int p = 0; p < K; ++p) {
-                act[p] = (unsigned)(k - S[p].G) < (unsigned)T;
-                const bool upd = act[p] && !S[p].psum;   // partial sums keep a zero state
-                const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
-                                          S[p].ch * S[p].op) + S[p].ga * qv[p]);
-                const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
-                S[p].op = upd ? o : S[p].op;
-                S[p].ip = upd ? I : S[p].ip;
-                ov[p] = o;
-                prev = o;
-            }
-            // inactive ticks write garbage that no active node reads (its consumer is inactive
-            // one tick later); never-processed reaches (no consumer) output 0
-#pragma unroll
-            for (int p = 0; p < K; ++p)
-                *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
-            // row k - gmin of the workgroup's window; only active (slot, tick) cells are stored
-            // (slots are sorted by G, so a wave's active lanes are a contiguous run and the
-            // masked rows stay whole 32-B sectors except at the run's ends): the window cells a
-            // slot does not run in are never read (window_index), so they are not written
-            {
-                double* orow = Om + wb + (int64_t)(k - gminw) * RS;
+                        for (int u = 0; u < kUpInline; ++u) m[p][u] += S[p].uext[u] ? 16u : 0u;
+                }
+                const unsigned rd = 8u * ((i + 1) & 1);     // parity of tick k - 1
+                const int k = kc + i;
+                double qv[K];
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    // non-temporal: rows are written once and read only by later fetches
-                    if (act[p]) {
-                        __builtin_nontemporal_store(ov[p], orow + p * SLOTS + tid);
-                        if (S[p].xsrc) XSm[S[p].xs0 + k] = ov[p];
+                    if constexpr (kBatchQ) qv[p] = qb[p][i];
+                    else qv[p] = q_of(p, i);
+                }
+                double vin[K][kUpInline];
+#pragma unroll
+                for (int p = 0; p < K; ++p) read_inputs(lds, m[p], rd, any3[p], vin[p]);
+                double ov[K];
+                bool act[K];
+                double prev = 0.0;
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    act[p] = (unsigned)(k - S[p].G) < (unsigned)T;
+                    bool upd = act[p];
+                    if constexpr (PSUM) upd = upd && !S[p].psum;   // partial sums: zero state
+                    const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
+                    const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
+                                              S[p].ch * S[p].op) + S[p].ga * qv[p]);
+                    const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
+                    S[p].op = upd ? o : S[p].op;
+                    S[p].ip = upd ? I : S[p].ip;
+                    ov[p] = o;
+                    prev = o;
+                }
+                // inactive ticks write garbage that no active node reads (its consumer is inactive
+                // one tick later); never-processed reaches (no consumer) output 0
+#pragma unroll
+                for (int p = 0; p < K; ++p)
+                    *reinterpret_cast<double*>(lds + own[p] + 8u * (i & 1)) = ov[p];
+                // row k - gmin of the workgroup's window; only active (slot, tick) cells are stored
+                // (slots are sorted by G, so a wave's active lanes are a contiguous run and the
+                // masked rows stay whole 32-B sectors except at the run's ends): the window cells a
+                // slot does not run in are never read (window_index), so they are not written
+                {
+                    double* orow = Om + wb + (int64_t)(k - gminw) * RS;
+#pragma unroll
+                    for (int p = 0; p < K; ++p) {
+                        // non-temporal: rows are written once and read only by later fetches
+                        if (act[p]) {
+                            __builtin_nontemporal_store(ov[p], orow + p * SLOTS + tid);
+                            if (S[p].xsrc) XSm[S[p].xs0 + k] = ov[p];
+                        }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
+        };
+        using yes = std::true_type;
+        using no = std::false_type;
+        if (clq) {
+            if (anyps) run_chunk(yes{}, yes{});
+            else run_chunk(yes{}, no{});
+        } else {
+            if (anyps) run_chunk(no{}, yes{});
+            else run_chunk(no{}, no{});
         }
 #pragma unroll
         for (int p = 0; p < K; ++p) {
@@ -305,13 +318,18 @@ void wavefront_det(WaveArgs a) {
     // o_t_next.  Slots that did not run in this launch (load_slot: G = 1 << 29) keep theirs
     // unchanged, so only the live ones are stored
     const int64_t sb = (int64_t)blockIdx.y * a.mS;
+    bool nonfin = false;
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         if (S[p].G != (1 << 29)) {
-            a.st_o[sb + S[p].d] = S[p].unr ? 0.0 : S[p].op;   // unrouted: o stays 0
+            const double so = S[p].unr ? 0.0 : S[p].op;        // unrouted: o stays 0
+            a.st_o[sb + S[p].d] = so;
             a.st_i[sb + S[p].d] = S[p].ip;
+            nonfin = nonfin || !__builtin_isfinite(so) || !__builtin_isfinite(S[p].ip);
         }
     }
+    if (a.nf && __any(nonfin) && (tid & 63) == 0)          // the dataflow kernel's fast form
+        __hip_atomic_store(a.nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.trace && tid == 0 && mem == 0) {
         const int64_t c_end = clock64();
         int64_t* rec = a.trace + kTraceWords * (int64_t)blockIdx.x;
@@ -517,6 +535,25 @@ hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, int chain, s
                             bool dense, int members, hipStream_t s) {
     return dense ? launch_wavefront_t<true>(a, grid, slots, chain, lds, members, s)
                  : launch_wavefront_t<false>(a, grid, slots, chain, lds, members, s);
+}
+
+namespace {
+__global__ __launch_bounds__(256) void flag_nonfinite(const double* __restrict__ src, int64_t n,
+                                                      int32_t* __restrict__ flag) {
+    bool bad = false;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        bad = bad || !__builtin_isfinite(src[x]);
+    if (__any(bad) && (threadIdx.x & 63) == 0)
+        __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
+
+hipError_t launch_flag_nonfinite(const double* src, int64_t n, int32_t* flag, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(flag_nonfinite, dim3((unsigned)blocks), 256, 0, s, src, n, flag);
+    return hipGetLastError();
 }
 
 hipError_t launch_set_slot_coeffs(const uint8_t* flags, double* alpha, double* beta, double* chi,

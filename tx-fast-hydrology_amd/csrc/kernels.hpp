@@ -94,7 +94,12 @@ struct WaveArgs {
     uint32_t* XG;                 // external-input granules [n_ext][T] x {lo, epoch, hi, epoch}
     uint32_t xg_bytes;            // size of XG in bytes (< 2^31)
     uint32_t epoch;               // tag of this run's granules (never 0)
-    int32_t* status;              // set to 1 when a wait gave up
+    int32_t* status;              // bit 0: a wait gave up; bit 1: a partial sum met a non-finite
+                                  // value in the fast form (the horizon is re-routed exactly)
+    // non-finite flags {state, forcing} (device, stream-ordered): when both are 0 the dataflow
+    // kernel runs its fast form, which lets partial sums carry a state (exact for finite values);
+    // its epilogue sets the state flag when the new state holds a non-finite value
+    int32_t* nf;
     int64_t patience;             // wall-clock (100 MHz) ticks a wait polls before giving up
     const double* Qm;             // member dataflow: lateral inflow [E][nslots] of the step
     const double* IO;             // member dataflow: state {o, i} (staging cells, MemberWin)
@@ -201,6 +206,8 @@ bool flow_shape_ok(int slots, int chain);
 
 // Device coefficients by slot kind (partial sums alpha = 1, unrouted reaches and padding 0;
 // kernels.hip set_slot_coeffs), applied after every coefficient upload
+// flag = 1 when some src[0 .. n) is NaN or +-Inf (otherwise the flag is left as it is)
+hipError_t launch_flag_nonfinite(const double* src, int64_t n, int32_t* flag, hipStream_t s);
 hipError_t launch_set_slot_coeffs(const uint8_t* flags, double* alpha, double* beta, double* chi,
                                   double* gamma, int64_t nslots, hipStream_t s);
 // Layout conversions between the caller (reach order, member innermost: [n][E]) and the device
