@@ -174,7 +174,8 @@ struct Net {
     size_t xg_words = 0;
     uint32_t epoch = 0;
     DBuf<int32_t> status;
-    // non-finite flags of the state and the forcing (WaveArgs::nf): set by the flag kernels
+    // non-finite flags of the state, the forcing F and the step row Fstep (WaveArgs::nf, nff):
+    // set by the flag kernels
     // when either is loaded, by a kernel epilogue that leaves a non-finite state, and
     // conservatively by every other state writer (mark_state)
     DBuf<int32_t> nf;
@@ -351,8 +352,8 @@ struct Net {
         }
         status.reserve(1);
         HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
-        nf.reserve(2);                   // {state, forcing}: a zero state and no forcing yet
-        HIPC(hipMemsetAsync(nf.p, 0, 2 * sizeof(int32_t), stream));
+        nf.reserve(3);                   // {state, forcing F, step row}: a zero state, no forcing
+        HIPC(hipMemsetAsync(nf.p, 0, 3 * sizeof(int32_t), stream));
         HIPC(hipHostMalloc(reinterpret_cast<void**>(&status_host), sizeof(int32_t),
                            hipHostMallocDefault));
         *status_host = 0;
@@ -1016,20 +1017,6 @@ struct Net {
             const int last = std::max(tabh[t2].x, tabh[t2].y);
             dense = last - tabh[t].x + 1 > 3;
         }
-        // unclamped steps [qc0, qc1]: clamped steps ({row, row, 0}, a row copy) are a prefix
-        // and a suffix of the horizon (monotonic step times); the kernels mask the high row
-        // only in chunks that reach them.  Any other pattern masks every chunk (safe).
-        int32_t qc0 = 0, qc1 = (int32_t)T - 1;
-        {
-            auto clamped = [&](int64_t t) { return tabh[t].x == tabh[t].y; };
-            int64_t f = 0, l = T - 1;
-            while (f < T && clamped(f)) ++f;
-            while (l >= f && clamped(l)) --l;
-            bool mid = false;
-            for (int64_t t = f; t <= l && !mid; ++t) mid = clamped(t);
-            qc0 = mid ? (int32_t)T : (int32_t)f;
-            qc1 = mid ? -1 : (int32_t)l;
-        }
         if (tabh != stab_host) {           // repeated horizons reuse the uploaded table
             upload_async(stab, tabh.data(), tabh.size());
             stab_host = tabh;
@@ -1067,8 +1054,7 @@ struct Net {
         a.F = Fsrc;
         a.stab = stab.p;
         a.nf = nf.p;
-        a.qc0 = qc0;
-        a.qc1 = qc1;
+        a.nff = nf.p + (Fsrc == Fstep.p ? 2 : 1);
         a.wg_gmin = wg_gmin.p;
         a.wg_gmax = wg_gmax.p;
         a.wbase = cur->wbase.p;
@@ -1288,7 +1274,11 @@ struct Net {
         REQUIRE(plan.n == 0 || (q && i_out && o_out), "q/outputs must not be NULL");
         const int64_t n = plan.n;
         Fstep.reserve((size_t)(std::max<int64_t>(plan.nslots, 1) * E));
-        if (n) to_slots(q, Fstep, E);
+        if (n) {
+            to_slots(q, Fstep, E);
+            HIPC(hipMemsetAsync(nf.p + 2, 0, sizeof(int32_t), stream));
+            HIPC(mcr::launch_flag_nonfinite(Fstep.p, plan.nslots * E, nf.p + 2, stream));
+        }
         run_tables(1, Fstep.p, 1, std::vector<int4>(1, step_entry(0, 0, 0.0)));
         if (n) {  // the new state is the output of the step
             from_slots(st_o, o_out, E);

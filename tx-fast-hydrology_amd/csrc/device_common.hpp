@@ -137,16 +137,3 @@ __device__ __forceinline__ double fold_values(const double* v, bool chained, boo
 
 }  // namespace dev
 }  // namespace mcr
-
-namespace mcr {
-namespace dev {
-// does any step of this lane's chunk [kc, kc + kChunk) fall outside the unclamped range?
-// (inactive ticks excluded; wave-uniform after __any)
-__device__ __forceinline__ bool chunk_clamped(int kc, int G, int T, int qc0, int qc1) {
-    int t0 = kc - G, t1 = t0 + kChunk - 1;
-    t0 = t0 < 0 ? 0 : t0;
-    t1 = t1 >= T ? T - 1 : t1;
-    return t0 <= t1 && (t0 < qc0 || t1 > qc1);
-}
-}  // namespace dev
-}  // namespace mcr

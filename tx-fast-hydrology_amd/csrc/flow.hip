@@ -443,18 +443,16 @@ void wavefront_flow(WaveArgs a) {
         // K <= 2 forms the whole chunk's values up front; longer lanes form them per tick
         // (register budget)
         constexpr bool kBatchQ = K <= 2;
-        // partial sums keep a zero state only when a non-finite value may occur (flags of the
-        // session's state and forcing): their update 0 + (((1 I + 0 Ip) + 0 Op) + 0 q) is I
-        // exactly for any finite state, and the select costs the common form ~6 % (same box).
-        // A partial sum that meets a non-finite value in the fast form anyway (an overflow of
-        // finite inputs) reports it, and the host re-routes the horizon exactly (sync()).
+        // the exact form only when a non-finite value may occur (device flags of the session's
+        // state and forcing): partial sums then keep a zero state (their update 0 + (((1 I +
+        // 0 Ip) + 0 Op) + 0 q) is I for a non-finite I too) and clamped steps mask their high
+        // row.  Both selects cost the common form ~6 % (same box), and neither is needed for
+        // finite values.  A partial sum that meets a non-finite value in the fast form anyway
+        // (an overflow of finite inputs) reports it, and the host re-routes the horizon with
+        // the exact launches (sync()).
         const bool exact = a.nf == nullptr ||
                            __hip_atomic_load(a.nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-                           __hip_atomic_load(a.nf + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-        bool anyps = false;                                 // a partial sum in this wave
-#pragma unroll
-        for (int p = 0; p < K; ++p) anyps = anyps || S[p].psum;
-        anyps = __any(anyps) && exact;
+                           __hip_atomic_load(a.nff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         for (int kc = kb; kc < wend; kc += kChunk) {
             const unsigned sb = (unsigned)((kc >> 3) & 1) * XSLOT;   // this chunk's ring slot
             unsigned frp[K], tp[K];
@@ -485,15 +483,10 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int u = 0; u < kUpInline; ++u)
                     m[p][u] = S[p].uext[u] ? S[p].ubase[u] + sb : S[p].ubase[u];
-            // clamped steps (a prefix / suffix of the horizon) need the masked high row, and
-            // partial-sum slots a frozen state; the chunk runs in one of four straight-line
-            // forms, so the common one (no clamped step, no partial sum in the wave) carries
-            // neither select (with them in every tick: +9 % on the det horizon, same box)
-            bool clq = false;
-#pragma unroll
-            for (int p = 0; p < K; ++p)
-                clq = clq || dev::chunk_clamped(kc, S[p].G, T, a.qc0, a.qc1);
-            clq = __any(clq);
+            // two straight-line forms of the chunk (EXACT: the session's state or forcing holds a
+            // non-finite value): the masked high row of clamped steps and the frozen state of
+            // partial sums are needed only then -- for finite forcing (1 - 0) lo + 0 lo is lo
+            // exactly, and a partial sum's update is I exactly for any finite state
             auto run_chunk = [&](auto mtag, auto ptag) {
                 constexpr bool MASKQ = decltype(mtag)::value, PSUM = decltype(ptag)::value;
                 auto q_of = [&](int p, int j) -> double {
@@ -572,13 +565,10 @@ void wavefront_flow(WaveArgs a) {
             };
             using yes = std::true_type;
             using no = std::false_type;
-            if (clq) {
-                if (anyps) run_chunk(yes{}, yes{});
-                else run_chunk(yes{}, no{});
-            } else {
-                if (anyps) run_chunk(no{}, yes{});
-                else run_chunk(no{}, no{});
-            }
+            // the fast form is the fall-through path and the exact one out of line (inline, the
+            // unexecuted forms cost the executed one ~3 %, same box)
+            if (__builtin_expect(!exact, 1)) [[likely]] run_chunk(no{}, no{});
+            else run_chunk(yes{}, yes{});
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 rb[p] = rbn[p];

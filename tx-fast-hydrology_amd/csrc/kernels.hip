@@ -157,6 +157,8 @@ void wavefront_det(WaveArgs a) {
     const int64_t c_loop = a.trace ? clock64() : 0;
 
     constexpr bool kBatchQ = K <= 2;                    // lateral inflows per chunk (registers)
+    const bool maskq = a.nf == nullptr ||               // non-finite forcing (device flag)
+                       __hip_atomic_load(a.nff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     bool anyps = false;                                 // a partial sum in this wave
 #pragma unroll
     for (int p = 0; p < K; ++p) anyps = anyps || S[p].psum;
@@ -199,12 +201,9 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
             for (int u = 0; u < kUpInline; ++u)
                 m[p][u] = S[p].uext[u] ? S[p].ubase[u] + 8u * c - 8u : S[p].ubase[u];
-        // the masked high row only in chunks that reach clamped steps, and a frozen state only
-        // in waves with partial sums: four straight-line forms of the chunk (flow.hip)
-        bool clq = false;
-#pragma unroll
-        for (int p = 0; p < K; ++p) clq = clq || dev::chunk_clamped(kc, S[p].G, T, a.qc0, a.qc1);
-        clq = __any(clq);
+        // the masked high row of clamped steps only for non-finite forcing (for finite forcing
+        // (1 - 0) lo + 0 lo is lo exactly), the frozen state of partial sums only in waves that
+        // hold one: four straight-line forms of the chunk, the common one inline (flow.hip)
         auto run_chunk = [&](auto mtag, auto ptag) {
             constexpr bool MASKQ = decltype(mtag)::value, PSUM = decltype(ptag)::value;
             // lateral inflow of position p at tick j of the chunk, interpolate_sample
@@ -298,12 +297,13 @@ void wavefront_det(WaveArgs a) {
         };
         using yes = std::true_type;
         using no = std::false_type;
-        if (clq) {
+        if (__builtin_expect(!maskq && !anyps, 1)) [[likely]] {
+            run_chunk(no{}, no{});
+        } else if (maskq) {
             if (anyps) run_chunk(yes{}, yes{});
             else run_chunk(yes{}, no{});
         } else {
-            if (anyps) run_chunk(no{}, yes{});
-            else run_chunk(no{}, no{});
+            run_chunk(no{}, yes{});
         }
 #pragma unroll
         for (int p = 0; p < K; ++p) {

@@ -99,7 +99,8 @@ struct WaveArgs {
     // non-finite flags {state, forcing} (device, stream-ordered): when both are 0 the dataflow
     // kernel runs its fast form, which lets partial sums carry a state (exact for finite values);
     // its epilogue sets the state flag when the new state holds a non-finite value
-    int32_t* nf;
+    int32_t* nf;                  // the state flag
+    const int32_t* nff;           // the flag of the forcing buffer this run reads
     int64_t patience;             // wall-clock (100 MHz) ticks a wait polls before giving up
     const double* Qm;             // member dataflow: lateral inflow [E][nslots] of the step
     const double* IO;             // member dataflow: state {o, i} (staging cells, MemberWin)
@@ -111,9 +112,6 @@ struct WaveArgs {
     int32_t tile;                 // ticks in this launch (multiple of kChunk)
     int32_t table_cap;            // LDS entries reserved for the step-table window
     int32_t ext_cap;              // LDS rows reserved for external inputs
-    // steps outside [qc0, qc1] may be clamped (row copies, frac 0: nutils.py:24-27); the
-    // interpolation masks the high row only in chunks that reach them (host: clamp_range)
-    int32_t qc0, qc1;
 };
 
 // LDS bytes of the multi-launch kernel for `slots` lanes (chain * slots node slots): the
