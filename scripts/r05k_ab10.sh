@@ -8,5 +8,5 @@ run() {  # tag dir args
   local rc=$?; echo "$tag rc=$rc $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r05k10_$tag.log)"; [ $rc -ne 0 ] && exit $rc
   return 0
 }
-for r in 1 2; do run det_cur$r . ; run det_fast$r ab_v1 ; run det_nops$r ab_v2 ; run det_old$r ab_r04; done
+for r in 1 2; do run det_cur$r . ; run det_fast$r ab_v1 ; run det_old$r ab_r04; done
 exit 0

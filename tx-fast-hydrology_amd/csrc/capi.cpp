@@ -404,10 +404,10 @@ struct Net {
             const int runs = flow_runs;
             flow_runs = 0;
             HIPC(hipMemcpy(status_host, status.p, sizeof(int32_t), hipMemcpyDeviceToHost));
-            if (*status_host != 0) {
+            const int32_t why = *status_host;
+            if (why != 0) {
                 *status_host = 0;
                 HIPC(hipMemsetAsync(status.p, 0, sizeof(int32_t), stream));
-                const int32_t why = *status_host;
                 if (runs == 1 && last_flow.valid) {
                     // bit 0: the device was shared (another stream held CUs the resident launch
                     // needed); bit 1: a partial sum met a non-finite value in the fast form.
@@ -430,6 +430,7 @@ struct Net {
                     }
                     force_mode = -1;
                     HIPC(hipStreamSynchronize(stream));
+                    flow_runs = 0;           // (the launches report nothing)
                     return;
                 }
                 if (why & 1)
@@ -438,10 +439,11 @@ struct Net {
                                          "are invalid)");
                 mark_state();
                 throw Fail(MC_E_STATE, "dataflow kernel: a partial sum met a non-finite value "
-                                       "produced from finite inputs (overflow) in the fast form; "
-                                       "the outputs of the runs since the last synchronisation "
-                                       "may differ from the reference's there (set the state "
-                                       "again and re-run: the next run is exact)");
+                                       "produced from finite inputs (an overflow) in the fast "
+                                       "form; the outputs of the runs since the last "
+                                       "synchronisation may differ from the reference's there "
+                                       "(the session's next run takes the exact form: set the "
+                                       "state again and re-run)");
             }
         }
     }
@@ -1037,6 +1039,7 @@ struct Net {
         if (timing) HIPC(hipEventRecord(events[2 * nl], stream));
 
         mcr::WaveArgs a{};
+        a.status = status.p;
         a.G = G.p;
         a.flags = flags.p;
         a.up_cnt = up_cnt.p;
