@@ -260,7 +260,9 @@ def build_workload(args, rank=0, world=1):
 
     # 192 lanes (3 compute waves + the helper: one wave per SIMD, two workgroups per CU) for
     # the resident dataflow kernels (det horizon, EnKF member steps); ensemble forecasts 256
-    slots = args.slots or (192 if E == 1 or enkf is not None else 256)
+    # (0: the session's default, engine._det_shape -- one compute wave of single-slot lanes for
+    # a small network such as HUC-8)
+    slots = args.slots or (0 if E == 1 else 192 if enkf is not None else 256)
     # ensemble forecasts (multi-launch path): 64-tick launches amortise the per-launch slot
     # loads (Texas ens64 14.1 -> 13.1 ms per horizon); the dataflow workloads at a 16-tick
     # cross-cluster slack (two chunks, the minimum): Texas det 0.605 -> 0.594 ms
@@ -650,8 +652,8 @@ def main():
                 "kernel_ms_per_step": round(tm["kernel_ms"] / args.timing_runs, 4)}
     # the routing recurrence keeps coefficients and state in registers / LDS: it is bound by its
     # dependency chain (schedule ticks x per-tick latency), not by DRAM bandwidth
-    if wl.enkf is None and E == 1 and path == "dataflow" and info["chain"] == 2 and \
-            info["slots"] in (192, 384):
+    if wl.enkf is None and E == 1 and path == "dataflow" and \
+            (info["slots"], info["chain"]) in ((192, 2), (384, 2), (64, 1)):
         ticks = info["gmax"] + args.T
         ns_tick = engine.probe_tick_floor(info["slots"], info["chain"], 8192)
         floor_ms = ticks * ns_tick * 1e-6

@@ -304,9 +304,10 @@ int mc_net_reroutes(const void* net, int64_t* count);
 
 /* Diagnostic (bench.py roofline): device time per tick of the bare dataflow tick chain -- LDS
  * inputs of the previous tick, `chain` chained Muskingum updates per lane, LDS outputs, the
- * workgroup barrier -- for the (slots, chain) = (192, 2) / (384, 2) kernel shape, two resident
- * workgroups per CU on the current device, no global memory traffic.  Schedule ticks x
- * *ns_per_tick is the latency floor of a horizon.  ticks: a multiple of 8. */
+ * workgroup barrier -- for the (slots, chain) = (192, 2) / (384, 2) kernel shape (two / one
+ * resident workgroups per CU) or the small-network shape (64, 1) (one per CU), on the current
+ * device, no global memory traffic.  Schedule ticks x *ns_per_tick is the latency floor of a
+ * horizon.  ticks: a multiple of 8. */
 int mc_probe_tick_floor(int32_t slots, int32_t chain, int64_t ticks, double* ns_per_tick);
 
 /* Launch trace of the last mc_run (off by default; diagnostic).  One record of 8 int64 per

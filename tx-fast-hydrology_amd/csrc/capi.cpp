@@ -7,6 +7,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -180,6 +181,18 @@ struct Net {
     // conservatively by every other state writer (mark_state)
     DBuf<int32_t> nf;
     void mark_state() { HIPC(hipMemsetAsync(nf.p, 1, 1, stream)); }
+    // a flag from the caller's host arrays when they are small (one memset instead of a memset
+    // and a flag kernel per array: sub-basin sessions reload state and forcing every horizon)
+    static constexpr size_t kHostFlagMax = (size_t)1 << 16;
+    static bool host_nonfinite(const double* a, size_t k) {
+        for (size_t x = 0; x < k; ++x)
+            if (!std::isfinite(a[x])) return true;
+        return false;
+    }
+    void set_flag(int32_t* f, bool bad) {
+        HIPC(hipMemsetAsync(f, 0, sizeof(int32_t), stream));
+        if (bad) HIPC(hipMemsetAsync(f, 1, 1, stream));
+    }
     int32_t* status_host = nullptr;  // pinned mirror, read at sync()
     int flow_runs = 0;               // dataflow launches since the status word was last read
     // the last dataflow horizon of one member, re-routed with launches when its waits gave up
@@ -942,9 +955,14 @@ struct Net {
         keep_outputs();
         to_slots(o, st_o, E);
         to_slots(i, st_i, E, &stage2);   // its own staging (stream-ordered reuse, no sync)
-        HIPC(hipMemsetAsync(nf.p, 0, sizeof(int32_t), stream));
-        HIPC(mcr::launch_flag_nonfinite(st_o.p, plan.nslots * E, nf.p, stream));
-        HIPC(mcr::launch_flag_nonfinite(st_i.p, plan.nslots * E, nf.p, stream));
+        const size_t cells = (size_t)(plan.n * E);
+        if (cells <= kHostFlagMax) {
+            set_flag(nf.p, host_nonfinite(o, cells) || host_nonfinite(i, cells));
+        } else {
+            HIPC(hipMemsetAsync(nf.p, 0, sizeof(int32_t), stream));
+            HIPC(mcr::launch_flag_nonfinite(st_o.p, plan.nslots * E, nf.p, stream));
+            HIPC(mcr::launch_flag_nonfinite(st_i.p, plan.nslots * E, nf.p, stream));
+        }
     }
 
     // Per-horizon layout: active workgroups of every launch and the output windows (cached
@@ -1246,8 +1264,12 @@ struct Net {
         st.upload(fp, cells, stream);
         HIPC(mcr::launch_forcing_to_slots(st.p, F.p, slot_reach.p, n, plan.nslots, rows, E,
                                           stream, reach_major));
-        HIPC(hipMemsetAsync(nf.p + 1, 0, sizeof(int32_t), stream));
-        HIPC(mcr::launch_flag_nonfinite(F.p, rows * plan.nslots * E, nf.p + 1, stream));
+        if (cells <= kHostFlagMax) {
+            set_flag(nf.p + 1, host_nonfinite(fp, cells));
+        } else {
+            HIPC(hipMemsetAsync(nf.p + 1, 0, sizeof(int32_t), stream));
+            HIPC(mcr::launch_flag_nonfinite(F.p, rows * plan.nslots * E, nf.p + 1, stream));
+        }
         // a copy from pageable host memory has read the caller's array when it returns, and the
         // persistent staging is reused stream-ordered: only the temporary staging must be
         // drained before it is freed, and a page-locked source (an asynchronous copy) read
@@ -1347,14 +1369,20 @@ struct Net {
         REQUIRE(0 <= t0 && t0 <= t1 && t1 <= T_out, "step range out of bounds");
         const int64_t n = plan.n, k = t1 - t0;
         const size_t cells = (size_t)std::max<int64_t>(n * k * E, 1);
-        if (!cstream) {
+        // small blocks (sub-basin sessions) gain nothing from the overlap: slot 0, the session
+        // stream, no copy stream of their own
+        const bool ring = cells * sizeof(double) >= ((size_t)4 << 20);
+        if (ring && !cstream) {
             HIPC(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-            for (int r = 0; r < 2; ++r) {
-                HIPC(hipEventCreateWithFlags(&a_ready[r], hipEventDisableTiming));
-                HIPC(hipEventCreateWithFlags(&a_copied[r], hipEventDisableTiming));
+            for (int q = 0; q < 2; ++q) {
+                HIPC(hipEventCreateWithFlags(&a_ready[q], hipEventDisableTiming));
+                HIPC(hipEventCreateWithFlags(&a_copied[q], hipEventDisableTiming));
             }
         }
-        const int r = (int)(a_seq++ & 1);
+        const int r = ring ? (int)(a_seq++ & 1) : 0;
+        if (!ring && fetch_pending > 0 &&
+            (aO[0].cap < cells || aI[0].cap < cells || aDg[0].cap < (size_t)(2 * k)))
+            HIPC(hipStreamSynchronize(stream));   // a pending direct copy may read the old slot
         if (a_used[r]) {
             // the slot's previous copy must be done before it is gathered into (stream order),
             // and before its buffers are replaced (host order)
@@ -1385,21 +1413,27 @@ struct Net {
             if (dg) HIPC(mcr::launch_row_digests(buf, k, n * E, aDg[r].p + c * k, stream));
             any = true;
         }
-        HIPC(hipEventRecord(a_ready[r], stream));
-        HIPC(hipStreamWaitEvent(cstream, a_ready[r], 0));
+        hipStream_t cs = stream;
+        if (ring) {
+            HIPC(hipEventRecord(a_ready[r], stream));
+            HIPC(hipStreamWaitEvent(cstream, a_ready[r], 0));
+            cs = cstream;
+        }
         for (int c = 0; c < 2 && any; ++c) {
             double* dst = c == 0 ? oo : io;
             uint64_t* dg = c == 0 ? dgo : dgi;
             if (dg)
                 HIPC(hipMemcpyAsync(dg, aDg[r].p + c * k, (size_t)k * sizeof(uint64_t),
-                                    hipMemcpyDeviceToHost, cstream));
+                                    hipMemcpyDeviceToHost, cs));
             if (dst)
                 HIPC(hipMemcpyAsync(dst, c == 0 ? aO[r].p : aI[r].p,
                                     (size_t)(n * k * E) * sizeof(double), hipMemcpyDeviceToHost,
-                                    cstream));
+                                    cs));
         }
-        HIPC(hipEventRecord(a_copied[r], cstream));
-        a_used[r] = true;
+        if (ring) {
+            HIPC(hipEventRecord(a_copied[r], cstream));
+            a_used[r] = true;
+        }
         int64_t t = 0;
         while (t < (int64_t)fetch_ev.size() && fetch_live[t]) ++t;
         if (t == (int64_t)fetch_ev.size()) {
@@ -1408,7 +1442,7 @@ struct Net {
             fetch_ev.push_back(e);
             fetch_live.push_back(0);
         }
-        HIPC(hipEventRecord(fetch_ev[t], cstream));
+        HIPC(hipEventRecord(fetch_ev[t], cs));
         fetch_live[t] = 1;
         ++fetch_pending;
         return t;
@@ -2012,10 +2046,13 @@ int mc_probe_tick_floor(int32_t slots, int32_t chain, int64_t ticks, double* ns_
     return guarded([&] {
         REQUIRE(ns_per_tick && ticks > 0 && ticks % mcr::kChunk == 0 && ticks < (1ll << 30),
                 "ticks must be a positive multiple of 8");
-        REQUIRE((slots == 192 || slots == 384) && chain == 2, "instantiated: (192, 2), (384, 2)");
+        REQUIRE(((slots == 192 || slots == 384) && chain == 2) || (slots == 64 && chain == 1),
+                "instantiated: (192, 2), (384, 2), (64, 1)");
         int dev = 0, cus = 0;
         HIPC(hipGetDevice(&dev));
         HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        // two workgroups per CU as the Texas launch runs them; the small-network shape (64, 1)
+        // one per CU (its launches hold a few workgroups)
         const int grid = (slots == 192 ? 2 : 1) * cus;
         hipStream_t s = nullptr;
         HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));

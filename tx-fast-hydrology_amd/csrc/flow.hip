@@ -1156,6 +1156,9 @@ hipError_t probe_tick_floor(int slots, int chain, int grid, int ticks, hipStream
     else if (slots == 384 && chain == 2)
         hipLaunchKernelGGL((tick_floor<384, 2>), dim3(grid), dim3(384 + kHelperLanes), lds, s,
                            ticks, out);
+    else if (slots == 64 && chain == 1)
+        hipLaunchKernelGGL((tick_floor<64, 1>), dim3(grid), dim3(64 + kHelperLanes), lds, s,
+                           ticks, out);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

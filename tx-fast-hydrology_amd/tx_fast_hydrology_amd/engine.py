@@ -20,6 +20,34 @@ def _params(slots=0, tile=0, ext_cap=0, chain=0):
     return nat.PlanParams(int(slots), int(tile), int(ext_cap), int(chain))
 
 
+# Resident shapes of a single-member session (lanes, slots per lane, ns per tick): one compute
+# wave of single-slot lanes ticks at ~0.29 us, 192 lanes x 2 at ~0.44 us but over a shorter
+# schedule (chained slots cost no tick).  Same-box sweeps (profiles/r05v_shapes.txt): HUC-8
+# 0.114 vs 0.162 ms per horizon, 4,000 reaches 0.163 vs 0.179; from ~12,000 reaches the 192 x 2
+# schedule wins (0.269 vs 0.338).
+_DET_SHAPES = ((64, 1, 0.29), (192, 2, 0.44))
+_DET_SHAPE_MAX_N = 50_000
+_DET_SHAPE_T = 288            # nominal horizon for the estimate: (schedule + T) ticks
+
+
+def _det_shape(end, deg, heads, chain):
+    """(lanes, chain) of a single-member session's default plan: the shape whose schedule of a
+    nominal horizon ticks least long (host plans of both, small networks only)."""
+    if chain or end.size == 0 or end.size > _DET_SHAPE_MAX_N:
+        return 192, chain
+    best = None
+    for lanes, k, ns_tick in _DET_SHAPES:
+        try:
+            p = Plan(end, deg, heads, slots=lanes, tile=16, chain=k)
+        except Exception:       # (a shape the plan cannot build: keep the other)
+            continue
+        est = (p.info["gmax"] + _DET_SHAPE_T) * ns_tick
+        p.close()
+        if best is None or est < best[0]:
+            best = (est, lanes, k)
+    return (best[1], best[2]) if best else (192, chain)
+
+
 class Plan:
     """Compiled schedule of a network (no device memory)."""
 
@@ -157,10 +185,12 @@ class RoutingNet:
             raise ValueError("indegree and endnodes must have the same length")
         h = ctypes.c_void_p()
         if slots == 0 and members == 1:
-            # 3 compute waves + the dataflow helper: one wave per SIMD (Texas det horizon 0.61 ms
-            # vs 0.66 at 384 lanes and 0.82 through the multi-launch path at 256), cross-cluster
-            # slack of two chunks (0.605 -> 0.594 ms)
-            slots = 192
+            # the resident dataflow launch: 192 lanes x 2 slots (3 compute waves + the helper,
+            # one wave per SIMD; Texas det 0.61 ms vs 0.66 at 384 lanes and 0.82 through the
+            # multi-launch path at 256), or for a small network whichever of that and one
+            # compute wave of single-slot lanes ticks its horizon faster; cross-cluster slack of
+            # two chunks (0.605 -> 0.594 ms)
+            slots, chain = _det_shape(end, deg, heads, chain)
             tile = tile or 16
         p = _params(slots, tile, ext_cap, chain)
         nat.check(L.mc_net_create(self.n, ptr(end), ptr(deg), ptr(heads), heads.size,
