@@ -20,12 +20,14 @@
  *   - the library never retains a caller pointer past the call;
  *   - a session handle is not thread-safe: use one thread per handle (or lock externally);
  *   - results are bit-identical to the reference's float64 arithmetic (same association, no
- *     FMA contraction, inflows summed in the reference's finalisation order) for FINITE inputs.
- *     The kernels evaluate a clamped forcing step as (1 - 0) f + 0 f and give unrouted reaches
- *     and padding slots zero coefficients instead of branching, so an Inf / NaN forcing value
- *     or state on an unrouted reach, or an Inf forcing row beyond the last interpolation
- *     point, yields NaN where the reference copies the row or keeps o = 0 (nutils.py:24-27,
- *     72-88).  Non-finite inputs are outside the contract (no reference test pins them).
+ *     FMA contraction, inflows summed in the reference's finalisation order), non-finite inputs
+ *     included: a step beyond the forcing index copies the clamped row (nutils.py:24-27), a
+ *     reach the reference walk never processes keeps o = 0 whatever its state and forcing hold
+ *     (nutils.py:68-88), and an overflow inside a partial-sum fold gives the reference's Inf /
+ *     NaN (tests/test_gpu_edges.py, single-member and ensemble sessions, every execution mode).  The
+ *     kernels run a fast form while the state and forcing in use are finite (device flags set
+ *     by every upload) and the exact form otherwise; a fast-form horizon whose partial sum
+ *     overflowed is re-routed from its input state at the next synchronising call.
  */
 #ifndef MCROUTE_H
 #define MCROUTE_H
@@ -128,13 +130,12 @@ int mc_net_set_stream(void* net, void* hip_stream);
  * mc_load_forcing / mc_simulate is [n_rows][n][E], mc_fetch_outputs returns [t][n][E] and
  * mc_fetch_series [n][T][E].  Members share topology and coefficients (each member
  * is an independent deterministic run with its own forcing and initial state).  Setting the
- * member count zeroes the state and drops loaded forcing and outputs.  Ensembles always run the
- * multi-launch path. */
+ * member count zeroes the state and drops loaded forcing and outputs.  Ensemble horizons run the
+ * multi-launch path; a one-step ensemble run (the assimilation cycle) is one member-dataflow
+ * launch when it fits the device (mc_set_mode). */
 int mc_net_set_members(void* net, int64_t members);
 int mc_net_get_members(const void* net, int64_t* members);
 
-
-/* Coefficients alpha, beta, chi, gamma (muskingum.py:332-360), caller order. */
 /* _apply_gain (nutils.py:116-134, applied as da.py:124-126) on the session state:
  * o += 0 + gain for reaches the reference walk processes; i += one-hop sums of those gains in
  * the reference's finalisation order.  gain: [n] (or [n][E] for an ensemble session). */
@@ -203,6 +204,7 @@ int mc_comm_destroy(void* comm);
 int mc_ens_analysis_dist(void* net, void* comm, int64_t m, const int64_t* gauges,
                          const double* y_local, const double* R);
 
+/* Coefficients alpha, beta, chi, gamma (muskingum.py:332-360), caller order. */
 int mc_set_coeffs(void* net, const double* alpha, const double* beta, const double* chi,
                   const double* gamma);
 /* State (o_t_next, i_t_next) of the model, caller order.  Like every upload of this ABI it

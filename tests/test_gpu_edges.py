@@ -197,3 +197,76 @@ def test_overflow_through_partial_sums_matches_reference(mode):
     g2 = net.fetch_outputs()
     assert _same(g2[0], w2[0]) and _same(g2[1], w2[1])
     net.close()
+
+
+def _edge_net():
+    # the network of the two tests above: a cycle (reaches 1, 2 never processed) and reach 5's
+    # eight upstreams folded through partial-sum nodes
+    end = np.array([1, 2, 1, 5, 5, 5, 1, 3] + [5] * 6, dtype=np.int64)
+    n = end.size
+    start = np.arange(n, dtype=np.int64)
+    indeg = orc.compute_indegree(start, end)
+    coef = orc.muskingum_coeffs(np.full(n, 3600.0), np.full(n, 0.2), 300.0)
+    return start, end, indeg, start[indeg == 0], coef
+
+
+@pytest.mark.parametrize("mode", ["launches", "auto", "dataflow", "paths"])
+def test_non_finite_ensemble_matches_reference(mode):
+    """The same contract for an ensemble session: member e is an independent reference run
+    (SURVEY a5).  Member 0 carries the non-finite forcing and state of the single-member test,
+    member 1 is finite, member 2 overflows inside reach 5's partial sums from finite inputs.
+    A horizon (multi-launch) and one-step runs (member dataflow, or member paths in mode
+    "paths") give every cell of every member exactly as the oracle does."""
+    start, end, indeg, heads, coef = _edge_net()
+    n, E = end.size, 3
+    o0 = np.stack([np.linspace(1.0, 2.0, n)] * E, axis=1)
+    o0[2, 0] = np.nan                                # unrouted reach: state never read
+    i0 = np.stack([orc.init_inflows(start, end, np.nan_to_num(o0[:, e])) for e in range(E)], 1)
+    xp = (1.7e18 + 3600e9 * np.arange(4)).astype(float)
+    fp = np.full((4, n, E), 0.5)
+    fp[1, 1, 0] = np.nan
+    fp[3, 7, 0] = np.inf
+    fp[0, 4, 0] = -np.inf
+    fp[1, 9, 0] = np.inf
+    fp[2, 12, 0] = -np.inf
+    fp[1:, 8:11, 2] = 1.2e308
+    fp[2:, 12, 2] = -1.5e308
+    x = xp[0] + 300e9 * np.arange(1, 61)
+    c = np.ascontiguousarray
+    want = [orc.simulate(start, end, indeg, *coef, c(o0[:, e]), c(i0[:, e]), x, xp, c(fp[:, :, e]))
+            for e in range(E)]
+    net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16, members=E)
+    net.set_coeffs(*coef)
+    if mode != "dataflow":                           # dataflow mode routes one step only
+        net.set_mode(mode)
+        net.set_state(o0, i0)
+        net.load_forcing(xp, fp)
+        net.run(x)
+        got_o, got_i = net.fetch_outputs()
+        so, si = net.get_state()
+        for e in range(E):
+            assert _same(got_o[:, :, e], want[e][0]) and _same(got_i[:, :, e], want[e][1])
+            assert _same(so[:, e], want[e][2]) and _same(si[:, e], want[e][3])
+    net.set_mode(mode)
+    # one step at a time over the first hours, from the reference's own states
+    o, i = o0.copy(), i0.copy()
+    net.set_state(o, i)
+    net.load_forcing(xp, fp)
+    for t in range(14):
+        net.run(x[t:t + 1])
+        got_o, got_i = net.fetch_outputs()
+        for e in range(E):
+            assert _same(got_o[0, :, e], want[e][0][t]), (t, e)
+            assert _same(got_i[0, :, e], want[e][1][t]), (t, e)
+    path = {"launches": "launches", "auto": "dataflow", "dataflow": "dataflow", "paths": "paths"}
+    assert net.mode()[1] == path[mode]
+    # mc_step: the forcing row is q itself
+    net.set_state(o0, i0)
+    q = np.full((n, E), 0.25)
+    q[[1, 3, 5, 7, 11], 0] = [np.nan, np.inf, -np.inf, np.inf, np.inf]
+    q[8:11, 2] = 1.5e308
+    i1, o1 = net.step(q)
+    for e in range(E):
+        wi, wo = orc.ax_bu(heads, end, *coef, c(i0[:, e]), c(o0[:, e]), c(q[:, e]), indeg)
+        assert _same(o1[:, e], wo) and _same(i1[:, e], wi), e
+    net.close()
