@@ -662,8 +662,9 @@ def main():
             "floor_ns_per_tick": round(ns_tick, 2), "floor_ms": round(floor_ms, 4),
             "frac": round(floor_ms / launch_ms, 4),
             "floor": "mc_probe_tick_floor: the bare tick chain of this kernel shape (LDS inputs, "
-                     "chained updates, LDS outputs, barrier; 2 workgroups per CU, no memory "
-                     "traffic), measured now on this device"}
+                     "chained updates, LDS outputs, barrier; %s per CU, no memory traffic), "
+                     "measured now on this device"
+                     % ("2 workgroups" if info["slots"] == 192 else "1 workgroup")}
     elif wl.enkf is None and E > 1:
         # an ensemble horizon is throughput-bound: its critical path (the schedule's ticks at the
         # bare tick latency) is a small fraction of it, and the bound it is measured against is
