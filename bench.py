@@ -85,6 +85,9 @@ def parse(argv=None, world=None):
     ap.add_argument("--one-plan", action="store_true",
                     help="EnKF: route the forecast on the analysis plan too (no hand-over)")
     ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--sync", type=int, default=None,
+                    help="1 / 0: chunk-synchronous / classic plan for the dataflow sessions "
+                         "(default: the session's own choice, engine.RoutingNet)")
     ap.add_argument("--fslots", type=int, default=256,
                     help="EnKF: lanes of the forecast plan (after the last analysis)")
     ap.add_argument("--ftile", type=int, default=64,
@@ -268,7 +271,7 @@ def build_workload(args, rank=0, world=1):
     # cross-cluster slack (two chunks, the minimum): Texas det 0.605 -> 0.594 ms
     tile = args.tile or (64 if E > 1 and enkf is None else 16)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E,
-                            chain=args.chain)
+                            chain=args.chain, sync=getattr(args, "sync", None))
     net.set_mode(getattr(args, "mode", "auto"))
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)

@@ -52,6 +52,9 @@ typedef struct mc_plan_params {
     int32_t ext_cap;  /* max cross-cluster inputs per workgroup; 0 = default */
     int32_t chain;    /* node slots per lane, 1..4 (0 = default 2): a run of up to `chain`
                          consecutive reaches along a flow path shares one lane and one tick */
+    int32_t sync;     /* 1: chunk-synchronous plan (plan.hpp: unit-slack edges inside one wave,
+                         8-tick local edges between the waves of a workgroup), so the dataflow
+                         kernel joins its waves once per 8 ticks; 0: classic plan */
 } mc_plan_params;
 
 typedef struct mc_plan_info {
@@ -70,7 +73,7 @@ typedef struct mc_plan_info {
     int64_t n_ext;        /* cross-cluster inputs over all workgroups */
     int64_t n_pairs;      /* chained edges (a node and its consumer in one lane and tick) */
     int32_t chain;        /* node slots per lane */
-    int32_t reserved;
+    int32_t n_local;      /* sync plans: 8-tick local edges between the waves of a workgroup */
 } mc_plan_info;
 
 /* Thread-local description of the last error (never NULL). */
@@ -96,6 +99,11 @@ int mc_plan_export(const void* plan, int64_t* rank, int64_t* pos, int32_t* G,
  * Any pointer may be NULL. */
 int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint64_t* up4,
                          int32_t* ext_off, int64_t* ext_src, int32_t* ext_g);
+/* Local edges of a chunk-synchronous plan (mc_plan_params.sync): lx_off [nwg+1] (the local
+ * inputs of workgroup w are its external columns ext_off[w+1]-ext_off[w] + 0 .. after its
+ * cross-workgroup ones) and lx_src [n_local] (the producing node slot of each).  A local input
+ * delivers at tick k the producer's output of tick k - 4.  Any pointer may be NULL. */
+int mc_plan_export_local(const void* plan, int32_t* lx_off, int32_t* lx_src);
 /* Launch schedule for a horizon of T steps: launch k covers ticks [k*tile, (k+1)*tile) and
  * runs workgroups list[off[k] .. off[k+1]).  Call with off/list NULL to get the sizes
  * (*n_launch, *n_list); then with arrays of at least n_launch+1 / n_list entries. */

@@ -66,6 +66,7 @@ class OracleNet:
         self.n = self.end.size
         self.runs = 0
         self.steps = 0
+        self._h = True            # engine.RoutingNet: None once closed
 
     def set_coeffs(self, a, b, c, g):
         self.coef = [np.array(v, dtype=np.float64) for v in (a, b, c, g)]
@@ -116,7 +117,7 @@ class OracleNet:
         return 0
 
     def close(self):
-        pass
+        self._h = None
 
 
 def use_oracle_device(monkeypatch):

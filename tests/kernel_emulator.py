@@ -13,6 +13,7 @@ bit-for-bit against the oracle without a GPU:
 import numpy as np
 
 ROUTED, UNROUTED, PSUM = 1, 2, 3
+WAVE_SLACK = 4
 EXT = 0x8000
 SELF = 0x7FFF
 
@@ -76,6 +77,12 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
     O = np.full((n + nslots, T), np.nan)
     I = np.full((n + nslots, T), np.nan)
 
+    # chunk-synchronous plans: local inputs (external columns after a workgroup's granule
+    # inputs) deliver at tick k the producer's output of tick k - WAVE_SLACK, written within the
+    # same workgroup (plan.hpp kWaveSlack)
+    loc = plan.export_local()
+    lx_off, lx_src = loc["lx_off"], loc["lx_src"]
+
     for k in range(len(off) - 1):
         k0 = k * tile
         Os, Is = O.copy(), I.copy()          # reads see only earlier launches
@@ -83,7 +90,8 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
             d = w * RS + np.arange(RS)
             e0, e1 = ln["ext_off"][w], ln["ext_off"][w + 1]
             ne = e1 - e0
-            xe = np.zeros((max(ne, 1), tile))
+            lsrc = lx_src[lx_off[w]:lx_off[w + 1]]
+            xe = np.zeros((max(ne + lsrc.size, 1), tile))
             for e in range(ne):
                 tt = k0 + np.arange(tile) - ln["ext_g"][e0 + e]
                 ok = (tt >= 0) & (tt < T)
@@ -107,6 +115,9 @@ def run(plan, alpha, beta, chi, gamma, o0, i0, x, xp, fp):
             cn = cnt[d]
             for i in range(tile):
                 kk = k0 + i
+                for li, src in enumerate(lsrc):
+                    ts = kk - WAVE_SLACK - G[src]
+                    xe[ne + li, i] = O[orow[src], ts] if 0 <= ts < T else 0.0
                 t = kk - g
                 act = live & (t >= 0) & (t < T)
                 if not act.any():

@@ -402,3 +402,51 @@ def test_copy_does_not_share_device_session(golden, monkeypatch):
     c = m.copy()
     assert c._device.net is None and m._device.net is not None
     assert np.array_equal(c.o_t_next, m.o_t_next) and c.o_t_next is not m.o_t_next
+
+
+def test_close_with_held_generator_keeps_state_readable(golden, monkeypatch):
+    """close() inside a fused horizon settles the lazy inflow rows first, so the
+    state stays readable, the generator can finish and the model routes again."""
+    use_oracle_device(monkeypatch)
+    g = golden("g3_confluence.npz")
+    m = golden_model(g)
+    df = golden_frame(g, m.reach_ids)
+    gen = m.simulate(df)
+    for k, _ in enumerate(gen):
+        if k == 5:
+            break
+    m.close()
+    assert np.array_equal(m.i_t_next, g["i"][5]) and np.array_equal(m.i_t_prev, g["i"][4])
+    gen.close()                                     # its finally settles on the closed session
+    m.step(np.zeros(m.n))                           # a new session
+    assert np.isfinite(m.o_t_next).all()
+
+
+def test_lazy_inflow_block_refuses_stale_or_closed_session(monkeypatch):
+    from api_helpers import OracleNet
+    from tx_fast_hydrology_amd.muskingum import _InflowBlock
+    net = OracleNet(np.array([1, 1]), np.array([1, 0]), np.array([0]))
+    net.out_i = np.zeros((4, 2))
+    net.out_o = np.zeros((4, 2))
+    blk = _InflowBlock(net, 0, 2, 2)
+    net.runs += 1                                    # the session routed again
+    with pytest.raises(RuntimeError, match="routed again"):
+        blk.fetch()
+    blk = _InflowBlock(net, 0, 2, 2)
+    net.close()
+    with pytest.raises(RuntimeError, match="closed"):
+        blk.fetch()
+
+
+def test_unpickle_model_with_eager_inflow_keys(golden):
+    """A model pickled before the inflows became lazy properties keeps its inflow state."""
+    import pickle
+    g, m = _g10_model(golden)
+    state = m.__getstate__()
+    state["i_t_next"] = state.pop("_i_t_next")
+    state["i_t_prev"] = state.pop("_i_t_prev")
+    m2 = Muskingum.__new__(Muskingum)
+    m2.__setstate__(state)
+    assert np.array_equal(m2.i_t_next, m.i_t_next) and np.array_equal(m2.i_t_prev, m.i_t_prev)
+    m3 = pickle.loads(pickle.dumps(m2))
+    assert np.array_equal(m3.i_t_next, m.i_t_next)

@@ -228,12 +228,15 @@ def test_session_rejects_unaligned_tile():
         engine.RoutingNet(np.array([0]), np.array([0]), np.array([0]), tile=5)
 
 
-@pytest.mark.parametrize("slots,tile", [(192, 16), (192, 32), (256, 32), (384, 32), (448, 32)])
-def test_texas_scale_bitexact_vs_oracle(exec_mode, slots, tile):
+@pytest.mark.parametrize("slots,tile,sync", [(192, 16, 1), (192, 16, 0), (192, 32, 0),
+                                             (256, 32, 0), (256, 16, 1), (384, 32, 0),
+                                             (448, 32, 0)])
+def test_texas_scale_bitexact_vs_oracle(exec_mode, slots, tile, sync):
     """Full Texas-size network (190k reaches, depth ~1500), 24 h @ 300 s: every output of every
     step bit-identical to the serial oracle.  At 192 / 384 / 448 lanes the network fits one
-    resident dataflow launch (auto mode takes it; 192 lanes with a 16-tick slack is the bench
-    default); at 256 it does not (auto falls back to launches)."""
+    resident dataflow launch (auto mode takes it; 192 lanes with a 16-tick slack on a
+    chunk-synchronous plan is the bench default); at 256 it does not (auto falls back to
+    launches, which route the sync plan's 4-tick local edges too)."""
     end = synthetic.texas(seed=0)
     n = end.size
     K, X, o0 = synthetic.model_arrays(n, seed=0)
@@ -243,7 +246,8 @@ def test_texas_scale_bitexact_vs_oracle(exec_mode, slots, tile):
     xp = xp.astype(float)
     x = xp[0] + 300e9 * np.arange(1, 289)
     want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
-    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=tile)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=slots, tile=tile, sync=sync)
+    assert (net.info["n_local"] > 0) == bool(sync)
     got_o, got_i = net.simulate(x, xp, fp)
     flow = exec_mode != "launches" and slots in (192, 384, 448)
     assert net.mode()[1] == ("dataflow" if flow else "launches")
@@ -391,7 +395,8 @@ def test_texas_scale_lane_chains_bitexact(exec_mode, chain, slots):
     assert np.array_equal(got_i, want_i)
 
 
-def test_dataflow_give_up_reroutes_with_launches():
+@pytest.mark.parametrize("sync", [1, 0])
+def test_dataflow_give_up_reroutes_with_launches(sync):
     """A dataflow run whose waits give up (forced here: patience < 0 gives up at the first stale
     upstream value) is re-routed from its input state with launches at the next synchronising
     call -- outputs and final state stay bit-exact; two such runs before a synchronisation
@@ -405,7 +410,7 @@ def test_dataflow_give_up_reroutes_with_launches():
     xp = xp.astype(float)
     x = xp[0] + 300e9 * np.arange(1, 289)
     want_o, want_i, fo, fi = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
-    net = _net(end, indeg, heads, coef, o0, i0, slots=192, tile=16)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=192, tile=16, sync=sync)
     net.set_mode("auto")
     net.set_flow_patience(-1)
     net.load_forcing(xp, fp)

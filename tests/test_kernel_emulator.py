@@ -105,3 +105,65 @@ def test_emulator_member_plans(slots, chain, tile):
     O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
     assert np.array_equal(O.T, want_o)
     assert np.array_equal(I.T, want_i)
+
+
+@pytest.mark.parametrize("slots,chain,tile", [(192, 2, 16), (128, 2, 16), (64, 1, 16),
+                                              (192, 3, 16), (256, 2, 32)])
+@pytest.mark.parametrize("kind", ["river", "fan_in"])
+def test_emulator_sync_plans(slots, chain, tile, kind):
+    """Chunk-synchronous plans (plan.hpp sync): unit-slack edges inside one wave, 4-tick local
+    edges between the waves of a workgroup (read from the producer's output of tick k - 4).
+    The emulator reads a local input only from ticks the producer already ran, so a schedule
+    that violated the slack would read NaN."""
+    rng = np.random.default_rng(slots * 3 + chain)
+    if kind == "river":
+        end = synthetic.river_network(6000, 6, 400, rng)
+    else:
+        end = synthetic.fan_in_forest(3000, rng)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=3)
+    start, indeg, coef, i0 = _case(end, K, X, 300.0, o0)
+    xp, fp = synthetic.forcing(n, rows=4, seed=4)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 31)
+    want_o, want_i, _, _ = orc.simulate(start, end, indeg, *coef, o0, i0, x, xp, fp)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=slots, tile=tile, chain=chain,
+                       sync=1)
+    if slots > 64 and kind == "river":
+        assert plan.info["n_local"] > 0
+    O, I = emu.run(plan, *coef, o0, i0, x, xp, fp)
+    assert np.array_equal(O.T, want_o) and np.array_equal(I.T, want_i)
+
+
+def test_sync_plan_invariants():
+    """Every unit-slack edge of a sync plan stays inside one wave of 64 lanes; every local edge
+    has slack exactly 4 and stays inside its workgroup."""
+    rng = np.random.default_rng(11)
+    end = synthetic.river_network(20000, 20, 800, rng)
+    n = end.size
+    start = np.arange(n)
+    indeg = orc.compute_indegree(start, end)
+    plan = engine.Plan(end, indeg, start[indeg == 0], slots=192, tile=16, chain=2, sync=1)
+    info, ex, ln, loc = plan.info, plan.export(), plan.export_links(), plan.export_local()
+    RS = 2 * 192
+    G = ex["G"]
+    n_unit = n_loc = 0
+    for d in np.flatnonzero(ln["flags"]):
+        w = d // RS
+        ne = ln["ext_off"][w + 1] - ln["ext_off"][w]
+        for c in range(int(ln["up_cnt"][d])):
+            code = int(ln["up4"][d] >> np.uint64(16 * c)) & 0xFFFF
+            if code == 0x7FFF:
+                continue
+            if code & 0x8000:
+                e = code & 0x7FFF
+                if e >= ne:
+                    src = loc["lx_src"][loc["lx_off"][w] + e - ne]
+                    assert src // RS == w and G[d] == G[src] + 4
+                    n_loc += 1
+                continue
+            u = w * RS + code
+            assert G[d] == G[u] + 1
+            assert (u % RS % 192) // 64 == (d % RS % 192) // 64     # same wave
+            n_unit += 1
+    assert n_loc == info["n_local"] > 0 and n_unit > 0

@@ -43,6 +43,7 @@ mcr::PlanParams to_params(const mc_plan_params* pp) {
         if (pp->tile) p.tile = pp->tile;
         if (pp->ext_cap) p.ext_cap = pp->ext_cap;
         if (pp->chain) p.chain = pp->chain;
+        p.sync = pp->sync;
     }
     return p;
 }
@@ -63,7 +64,7 @@ void fill_info(const mcr::Plan& P, mc_plan_info* info) {
     info->n_ext = (int64_t)P.ext_src.size();
     info->n_pairs = P.n_pairs;
     info->chain = P.p.chain;
-    info->reserved = 0;
+    info->n_local = (int32_t)P.n_local;
 }
 
 void check_topology_args(int64_t n, const int64_t* endnodes, const int64_t* indegree,
@@ -100,7 +101,8 @@ struct Net {
     hipStream_t stream = nullptr;
 
     // static schedule
-    DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, xid;
+    DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, xid, lx_off, lx_src;
+    DBuf<int16_t> lx;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
     DBuf<int64_t> slot_reach, pos;
@@ -338,6 +340,10 @@ struct Net {
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
         xid.upload(plan.xid.data(), plan.xid.size(), stream);
+        lx.upload(plan.lx.data(), plan.lx.size(), stream);
+        lx_off.upload(plan.lx_off.data(), plan.lx_off.size(), stream);
+        lx_src.upload(plan.lx_src.data(), plan.lx_src.size(), stream);
+        lx_src.reserve(1);
         in_off.upload(plan.in_off.data(), plan.in_off.size(), stream);
         in_list.upload(plan.in_list.data(), plan.in_list.size(), stream);
         in_list.reserve(1);
@@ -472,13 +478,13 @@ struct Net {
         if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
         const size_t xg = plan.ext_src.size() * (size_t)T * 16;
-        lds = mcr::flow_lds_bytes(S, Kc, (int)T, plan.max_ext_wg);
-        bool ok = mcr::flow_shape_ok(S, Kc) &&
-                  plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
+        lds = mcr::flow_lds_bytes(S, Kc, (int)T, plan.max_xe_wg);
+        bool ok = mcr::flow_shape_ok(S, Kc, plan.p.sync != 0) &&
+                  plan.p.tile >= mcr::kFlowMinSlack && plan.max_xe_wg <= mcr::kFlowMaxExt &&
                   T <= mcr::kFlowMaxT && xg < (size_t(1) << 31) && lds <= 160 * 1024;
         if (ok) {
             int bpc = 0;
-            HIPC(mcr::flow_occupancy(S, Kc, dense, lds, &bpc));
+            HIPC(mcr::flow_occupancy(S, Kc, dense, plan.p.sync != 0, lds, &bpc));
             ok = (int64_t)bpc * cu_count >= plan.nwg;
         }
         if (mode == 2 && !ok)
@@ -596,15 +602,15 @@ struct Net {
         if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
         const size_t xg = plan.ext_src.size() * (size_t)E * 16;
-        lds = mcr::flow_lds_bytes(S, Kc, 0, plan.max_ext_wg);
-        bool ok = mcr::flow_shape_ok(S, Kc) &&
-                  plan.p.tile >= mcr::kFlowMinSlack && plan.max_ext_wg <= mcr::kFlowMaxExt &&
+        lds = mcr::flow_lds_bytes(S, Kc, 0, plan.max_xe_wg);
+        bool ok = mcr::flow_shape_ok(S, Kc, plan.p.sync != 0) &&
+                  plan.p.tile >= mcr::kFlowMinSlack && plan.max_xe_wg <= mcr::kFlowMaxExt &&
                   E < (1 << 24) && xg < (size_t(1) << 31) && lds <= 160 * 1024 &&
                   // member-major cells are addressed by 32-bit buffer offsets (flow.hip MEMB)
                   (member_skew() || plan.nslots * E * 16 < (1ll << 31));
         if (ok) {
             int bpc = 0;
-            HIPC(mcr::flow_members_occupancy(S, Kc, lds, &bpc));
+            HIPC(mcr::flow_members_occupancy(S, Kc, plan.p.sync != 0, lds, &bpc));
             ok = (int64_t)bpc * cu_count >= plan.nwg;
         }
         return ok;
@@ -1070,6 +1076,9 @@ struct Net {
         a.up4 = up4.p;
         a.ext_off = ext_off.p;
         a.xid = xid.p;
+        a.lx = lx.p;
+        a.lx_off = plan.p.sync ? lx_off.p : nullptr;
+        a.lx_src = lx_src.p;
         a.XS = XS.p;
         a.ext_g = ext_g.p;
         a.alpha = alpha.p;
@@ -1090,7 +1099,7 @@ struct Net {
         a.n_rows = (int32_t)rows;
         a.T = (int32_t)T;
         a.tile = plan.p.tile;
-        a.ext_cap = plan.max_ext_wg;
+        a.ext_cap = plan.max_xe_wg;
         a.mF = rows * plan.nslots;
         a.mO = cur->Otot;
         a.mX = (int64_t)plan.ext_src.size() * T;
@@ -1146,7 +1155,7 @@ struct Net {
                 }
                 if (timing) HIPC(hipEventRecord(events[0], stream));
                 HIPC(mcr::launch_flow_members(a, plan.nwg, plan.p.slots, plan.p.chain, flds,
-                                              stream));
+                                              plan.p.sync != 0, stream));
                 if (timing) HIPC(hipEventRecord(events[1], stream));
                 HIPC(mcr::launch_member_unpack(IOp, mw, st_o.p, st_i.p, plan.nslots, E, stream));
                 mark_state();
@@ -1191,7 +1200,7 @@ struct Net {
                 a.st_i_out = st_i2.p;
                 if (timing) HIPC(hipEventRecord(events[0], stream));
                 HIPC(mcr::launch_flow(a, plan.nwg, plan.p.slots, plan.p.chain, flds, dense,
-                                      stream));
+                                      plan.p.sync != 0, stream));
                 if (timing) HIPC(hipEventRecord(events[1], stream));
                 st_o.swap(st_o2);
                 st_i.swap(st_i2);
@@ -1621,6 +1630,17 @@ int mc_plan_export_links(const void* plan, uint8_t* flags, uint8_t* up_cnt, uint
         cp(ext_off, P.ext_off);
         cp(ext_src, P.ext_src);
         cp(ext_g, P.ext_g);
+    });
+}
+
+int mc_plan_export_local(const void* plan, int32_t* lx_off, int32_t* lx_src) {
+    return guarded([&] {
+        REQUIRE(plan, "null plan");
+        const mcr::Plan& P = *static_cast<const mcr::Plan*>(plan);
+        if (lx_off && !P.lx_off.empty())
+            std::memcpy(lx_off, P.lx_off.data(), P.lx_off.size() * sizeof(int32_t));
+        if (lx_src && !P.lx_src.empty())
+            std::memcpy(lx_src, P.lx_src.data(), P.lx_src.size() * sizeof(int32_t));
     });
 }
 

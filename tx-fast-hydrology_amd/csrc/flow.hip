@@ -160,10 +160,18 @@ struct Helper {
 // choice so that the tick computes one kind of cell address without branches.
 // Register budget: two waves per SIMD (256 VGPRs) up to 3 positions per lane; lanes of 4
 // positions need more (one wave per SIMD, so at most 3 compute waves + the helper).
-template <int SLOTS, int K, bool DENSE, bool MEMB, bool SKEW = false>
+// SYNC (chunk-synchronous plans, plan.hpp): 0 = one workgroup barrier per tick (classic
+// plans); kWaveSlack = one per kWaveSlack ticks: a unit-slack edge stays inside one wave (its
+// LDS accesses are processed in order, so the wave needs no barrier), an edge between two waves
+// of the workgroup has slack kWaveSlack and its producer writes the value straight into the
+// consumer's external column for tick k + kWaveSlack, which the consumer reads after the next
+// barrier.  The helper copies the tick planes of one barrier period during the next one.
+template <int SLOTS, int K, bool DENSE, bool MEMB, bool SKEW = false, int SYNC = 0>
 __global__ __launch_bounds__(SLOTS + kHelperLanes)
 __attribute__((amdgpu_waves_per_eu(K >= 4 ? 1 : 2, K >= 4 ? 1 : 2)))
 void wavefront_flow(WaveArgs a) {
+    static_assert(SYNC == 0 || (SYNC == kWaveSlack && kChunk == 2 * kWaveSlack),
+                  "sync kernels: two barrier periods of kWaveSlack ticks per chunk");
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int RS = K * SLOTS;
     constexpr unsigned PL = flow_plane_bytes(RS);
@@ -224,6 +232,36 @@ void wavefront_flow(WaveArgs a) {
         __syncthreads();                     // EG staged (LDS) before the helper reads it
         for (int b = 0; b < nb; ++b) h.fetch_now(b, kb, (unsigned)((kb >> 3) & 1));
         __syncthreads();                     // prologue barrier (matches the compute waves)
+        if constexpr (SYNC != 0) {
+            // two barrier periods per chunk: the planes of the period that just ended are
+            // copied during the next one (the compute waves overwrite them a period later)
+            int kc = kb;
+            for (; kc < wend; kc += kChunk) {
+                const int kn = kc + kChunk;
+                const bool pre = kn < wend && nb > 0;
+                const unsigned slot = (unsigned)((kn >> 3) & 1);
+                u32x4 g[kBatch], g1[kBatch];
+                if (pre) h.issue(0, kn, g);
+                if (pre && nb > 1) h.issue(1, kn, g1);
+#pragma unroll
+                for (int q = SYNC; q > 0; --q) copy_row(kc - q);
+                __syncthreads();   // ticks kc .. kc + SYNC - 1
+                if (pre) {
+                    const int bad = h.consume(0, kn, slot, g);
+                    if (__any(bad >= 0)) h.settle(0, kn, slot, bad);
+                }
+                if (pre && nb > 1) {
+                    const int bad = h.consume(1, kn, slot, g1);
+                    if (__any(bad >= 0)) h.settle(1, kn, slot, bad);
+                }
+#pragma unroll
+                for (int q = 0; q < SYNC; ++q) copy_row(kc + q);
+                __syncthreads();   // ticks kc + SYNC .. kc + kChunk - 1
+            }
+#pragma unroll
+            for (int q = SYNC; q > 0; --q) copy_row(kc - q);
+            return;
+        }
         for (int kc = kb; kc < wend; kc += kChunk) {
             const int kn = kc + kChunk;
             const bool pre = kn < wend && nb > 0;
@@ -278,12 +316,35 @@ void wavefront_flow(WaveArgs a) {
 
     bool any3[K];
     unsigned own[K];
+    // sync plans: the XE column this slot's output feeds kWaveSlack ticks later (local edge)
+    bool lxo[K];
+    unsigned lxc[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         decode_codes<RS>(S[p], up[p], XB, 8u, XE, 8u);
         any3[p] = __any(S[p].cnt > 2);
         own[p] = XB + (unsigned)(p * SLOTS + lid) * 8u;
+        const int l = SYNC ? (int)a.lx[S[p].d] : -1;
+        lxo[p] = l >= 0;
+        lxc[p] = XE + (unsigned)(l < 0 ? 0 : l) * 8u;
     }
+    // end of tick i of a chunk: the workgroup barrier (every tick, or every SYNC ticks); between
+    // the ticks of a period only the compiler is kept from moving LDS accesses across
+    auto tick_end = [&](int i) {
+        if (SYNC == 0 || i % (SYNC ? SYNC : 1) == SYNC - 1) __syncthreads();
+        else __asm__ __volatile__("" ::: "memory");
+    };
+    // local edges: the value of tick kc + i feeds the consumer's tick kc + i + SYNC: chunk tick
+    // (i + SYNC) & 7 (plane (i + SYNC + 7) & 7) of this chunk's ring slot, or of the next one's
+    auto write_local = [&](int i, unsigned sb, const double* ov) {
+        if constexpr (SYNC != 0) {
+            const unsigned rs = i + SYNC < kChunk ? sb : XSLOT - sb;
+            const unsigned pl = (unsigned)((i + SYNC + 7) & 7) * PL;
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+                if (lxo[p]) *reinterpret_cast<double*>(lds + lxc[p] + rs + pl) = ov[p];
+        }
+    };
 
     const unsigned epoch = a.epoch;
     int64_t t_loop = 0, c_loop = 0;
@@ -420,7 +481,8 @@ void wavefront_flow(WaveArgs a) {
                             gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
                     }
                 }
-                __syncthreads();
+                write_local(i, sb, ov);
+                tick_end(i);
             }
         }
     } else {
@@ -560,7 +622,8 @@ void wavefront_flow(WaveArgs a) {
                                 gv, xg, (unsigned)((S[p].xs0 + k) * 16), 0, 16);
                         }
                     }
-                    __syncthreads();
+                    write_local(i, sb, ov);
+                    tick_end(i);
                 }
             };
             using yes = std::true_type;
@@ -609,13 +672,17 @@ void wavefront_flow(WaveArgs a) {
 }
 
 template <bool DENSE, bool MEMB, bool SKEW = false>
-const void* flow_fn(int slots, int chain);
+const void* flow_fn(int slots, int chain, bool sync);
 
 }  // namespace
 
-bool flow_shape_ok(int slots, int chain) {
+bool flow_shape_ok(int slots, int chain, bool sync) {
 #define MCR_CASE(S, K) if (slots == S && chain == K) return true;
-    MCR_FLOW_SHAPES(MCR_CASE)
+    if (sync) {
+        MCR_SYNC_SHAPES(MCR_CASE)
+    } else {
+        MCR_FLOW_SHAPES(MCR_CASE)
+    }
 #undef MCR_CASE
     return false;
 }
@@ -623,12 +690,21 @@ bool flow_shape_ok(int slots, int chain) {
 namespace {
 
 template <bool DENSE, bool MEMB, bool SKEW>
-const void* flow_fn(int slots, int chain) {
+const void* flow_fn(int slots, int chain, bool sync) {
 #define MCR_CASE(S, K)                 \
     if (slots == S && chain == K)      \
         return reinterpret_cast<const void*>(&wavefront_flow<S, K, DENSE, MEMB, SKEW>);
-    MCR_FLOW_SHAPES(MCR_CASE)
+#define MCR_SCASE(S, K)                \
+    if (slots == S && chain == K)      \
+        return reinterpret_cast<const void*>(                                          \
+            &wavefront_flow<S, K, DENSE, MEMB, SKEW, kWaveSlack>);
+    if (sync) {
+        MCR_SYNC_SHAPES(MCR_SCASE)
+    } else {
+        MCR_FLOW_SHAPES(MCR_CASE)
+    }
 #undef MCR_CASE
+#undef MCR_SCASE
     return nullptr;
 }
 
@@ -960,32 +1036,36 @@ __global__ __launch_bounds__(256) void member_unpack_ring(
 
 }  // namespace
 
-hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds, int* blocks_per_cu) {
-    return occupancy_of(dense ? flow_fn<true, false>(slots, chain)
-                              : flow_fn<false, false>(slots, chain),
+hipError_t flow_occupancy(int slots, int chain, bool dense, bool sync, size_t lds,
+                          int* blocks_per_cu) {
+    return occupancy_of(dense ? flow_fn<true, false>(slots, chain, sync)
+                              : flow_fn<false, false>(slots, chain, sync),
                         slots, lds, blocks_per_cu);
 }
 
-hipError_t flow_members_occupancy(int slots, int chain, size_t lds, int* blocks_per_cu) {
+hipError_t flow_members_occupancy(int slots, int chain, bool sync, size_t lds,
+                                  int* blocks_per_cu) {
     int a = 0, b = 0;                        // both staging layouts must be resident
-    hipError_t e = occupancy_of(flow_fn<false, true, false>(slots, chain), slots, lds, &a);
-    if (e == hipSuccess) e = occupancy_of(flow_fn<false, true, true>(slots, chain), slots, lds, &b);
+    hipError_t e = occupancy_of(flow_fn<false, true, false>(slots, chain, sync), slots, lds, &a);
+    if (e == hipSuccess)
+        e = occupancy_of(flow_fn<false, true, true>(slots, chain, sync), slots, lds, &b);
     *blocks_per_cu = std::min(a, b);
     return e;
 }
 
 hipError_t launch_flow(const WaveArgs& a, int grid, int slots, int chain, size_t lds, bool dense,
-                       hipStream_t s) {
-    const void* fn = dense ? flow_fn<true, false>(slots, chain) : flow_fn<false, false>(slots, chain);
+                       bool sync, hipStream_t s) {
+    const void* fn = dense ? flow_fn<true, false>(slots, chain, sync)
+                           : flow_fn<false, false>(slots, chain, sync);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<WaveArgs*>(&a)};
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);
 }
 
 hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain, size_t lds,
-                               hipStream_t s) {
-    const void* fn = a.mskew ? flow_fn<false, true, true>(slots, chain)
-                             : flow_fn<false, true, false>(slots, chain);
+                               bool sync, hipStream_t s) {
+    const void* fn = a.mskew ? flow_fn<false, true, true>(slots, chain, sync)
+                             : flow_fn<false, true, false>(slots, chain, sync);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<WaveArgs*>(&a)};
     return hipLaunchKernel(fn, dim3(grid), dim3(slots + kHelperLanes), args, lds, s);

@@ -127,6 +127,28 @@ void wavefront_det(WaveArgs a) {
             carry = Om[wb + (int64_t)(k0 - 1 - gminw) * RS + p * SLOTS + tid];
         xbp[(p * SLOTS + tid) * 2 + ((k0 - 1) & 1)] = carry;
     }
+    // sync plans (plan.hpp): local inputs, XE columns next .. next + nloc - 1 of this
+    // workgroup, deliver at tick k the producer's output of tick k - kWaveSlack.  The first
+    // kWaveSlack ticks of the launch take them from the previous launch's output window (active
+    // cells only: an inactive producer tick feeds an inactive consumer tick); the producers
+    // write the rest during this launch (tick loop below, one tick barrier apart at least).
+    const int next = a.ext_off[w + 1] - e0;
+    int lx_col[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) lx_col[p] = -1;
+    if (a.lx_off) {
+        const int l0 = a.lx_off[w], nloc = a.lx_off[w + 1] - l0;
+        for (int idx = tid; idx < nloc * kWaveSlack; idx += SLOTS) {
+            const int li = idx / kWaveSlack, q = idx - li * kWaveSlack;
+            const int64_t src = a.lx_src[l0 + li];
+            const int kk = k0 - kWaveSlack + q;
+            const bool act = (unsigned)(kk - a.G[src]) < (unsigned)T;
+            xe[(next + li) * tile + q] =
+                act ? Om[wb + (int64_t)(kk - gminw) * RS + (src - (int64_t)w * RS)] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < K; ++p) lx_col[p] = a.lx[S[p].d];
+    }
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;               // zero slot for unused codes
     // drain every prologue load: otherwise the wait-count pass carries "pending" state into
     // the tick loop and waits for each chunk's stores at every tick
@@ -292,6 +314,11 @@ void wavefront_det(WaveArgs a) {
                         }
                     }
                 }
+                // local edges of sync plans: the consumer's input of tick k + kWaveSlack
+#pragma unroll
+                for (int p = 0; p < K; ++p)
+                    if (lx_col[p] >= 0 && c + i + kWaveSlack < tile)
+                        xe[lx_col[p] * tile + c + i + kWaveSlack] = ov[p];
                 __syncthreads();
             }
         };

@@ -36,6 +36,9 @@ namespace mcr {
 #define MCR_FLOW_SHAPES(X)                                                             \
     X(64, 1) X(64, 2) X(128, 2) X(192, 2) X(256, 2) X(384, 2) X(448, 2) X(64, 3) X(128, 3) X(192, 3) \
     X(256, 3) X(64, 4) X(128, 4) X(192, 4)
+// ... of which these also run chunk-synchronous plans (plan.hpp sync: one workgroup barrier per
+// kWaveSlack ticks)
+#define MCR_SYNC_SHAPES(X) X(64, 1) X(64, 2) X(128, 2) X(192, 2) X(256, 2) X(192, 3)
 
 // Ticks whose lateral inflow is formed in one burst (and whose forcing rows are prefetched
 // together).  Launch lengths (`tile`) are multiples of it.
@@ -64,6 +67,10 @@ struct WaveArgs {
     const uint64_t* up4;          // [nslots]
     const int32_t* ext_off;       // [nwg + 1]
     const int32_t* xid;           // [nslots] external input fed by the slot's reach, -1 if none
+    const int16_t* lx;            // [nslots] sync plans: local external input (XE column of the
+                                  // slot's own workgroup) fed kWaveSlack ticks later, -1 if none
+    const int32_t* lx_off;        // [nwg + 1] sync plans: local inputs of each workgroup (their
+    const int32_t* lx_src;        // XE columns follow its granule inputs) and producer slots
     const int32_t* ext_g;         // G of the consuming reach
     const double* alpha;          // [nslots]
     const double* beta;
@@ -138,10 +145,12 @@ inline size_t flow_lds_bytes(int slots, int chain, int T, int ext_cap) {
 }
 
 // One launch for the whole horizon; grid = every workgroup (all must be co-resident).
+// sync: the plan is chunk-synchronous (plan.hpp; shapes MCR_SYNC_SHAPES)
 hipError_t launch_flow(const WaveArgs& a, int grid, int slots, int chain, size_t lds_bytes,
-                       bool dense, hipStream_t s);
+                       bool dense, bool sync, hipStream_t s);
 // Resident workgroups per CU of the dataflow kernel at this LDS size.
-hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds_bytes, int* blocks_per_cu);
+hipError_t flow_occupancy(int slots, int chain, bool dense, bool sync, size_t lds_bytes,
+                          int* blocks_per_cu);
 
 // Member dataflow (flow.hip): ONE step of E ensemble members as one resident launch.  Member e
 // of node slot d runs at tick G[d] + e (the members take the place of the steps of a horizon;
@@ -149,8 +158,9 @@ hipError_t flow_occupancy(int slots, int chain, bool dense, size_t lds_bytes, in
 // and writing the member's new {o, i} in their place; launch_member_unpack then forms the
 // session state from them.
 hipError_t launch_flow_members(const WaveArgs& a, int grid, int slots, int chain,
-                               size_t lds_bytes, hipStream_t s);
-hipError_t flow_members_occupancy(int slots, int chain, size_t lds_bytes, int* blocks_per_cu);
+                               size_t lds_bytes, bool sync, hipStream_t s);
+hipError_t flow_members_occupancy(int slots, int chain, bool sync, size_t lds_bytes,
+                                  int* blocks_per_cu);
 // Tick-major member windows of a member-dataflow step: workgroup w stages the (slot d, member
 // e) it processes at tick k = G[d] + e in row k - gmin[w] of its window, wbase[w] + row * rs +
 // (d - w rs) (rs = chain * slots node slots per row; rows gmin[w] .. gmax[w] + E - 1), so every
@@ -200,7 +210,7 @@ hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, int chain, s
                             bool dense, int members, hipStream_t s);
 // Is (slots, chain) instantiated for the multi-launch sweep / the dataflow kernels?
 bool wavefront_shape_ok(int slots, int chain);
-bool flow_shape_ok(int slots, int chain);
+bool flow_shape_ok(int slots, int chain, bool sync = false);
 
 // Device coefficients by slot kind (partial sums alpha = 1, unrouted reaches and padding 0;
 // kernels.hip set_slot_coeffs), applied after every coefficient upload

@@ -335,7 +335,16 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // cut for free.
     const int64_t RS = (int64_t)K * C;
     const int64_t scap = span_cap(C);
-    std::vector<int64_t> cl(N, -1);
+    // cl: cluster (sync plans: wave cluster) of every lane node, grp: its group (the cluster
+    // itself in classic plans); edges inside a cluster have unit slack, edges inside a group
+    // between its wave clusters kWaveSlack, all others >= tile
+    std::vector<int64_t> cl(N, -1), grp(N, -1);
+    std::vector<int32_t> G(N, 0);
+    // per workgroup: its lane bins (classic plans: one bin of `slots` lanes; sync plans: one per
+    // wave), each a list of chain tops
+    std::vector<std::vector<std::vector<int64_t>>> wg_bins;
+    const int64_t bin_lanes = params.sync ? kWaveLanes : C;
+    if (!params.sync) {
     std::vector<Cluster> clusters;
     std::vector<int32_t> eh(N, 0);          // critical-path estimate (ticks)
     std::vector<uint8_t> merged(N, 0);      // edge (x -> consumer) is inside a cluster
@@ -418,7 +427,6 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         Cluster& c = clusters[cl[j]];
         c.dmax = std::max(c.dmax, dist[j]);
     }
-    std::vector<int32_t> G(N, 0);
     // live clusters in root order (roots appear in `lnodes` order)
     std::vector<int64_t> live;
     for (int64_t j : lnodes)
@@ -437,13 +445,6 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         if (off > (int64_t)1 << 30) return "schedule overflow (network too deep)";
         c.off = (int32_t)off;
         for (int64_t v : members[id]) G[v] = c.off + c.dmax - dist[v];
-    }
-    for (int64_t x = 0; x < N; ++x) {
-        if (top[x] != x) {
-            G[x] = G[top[x]];
-            cl[x] = cl[top[x]];
-        }
-        P.gmax = std::max(P.gmax, G[x]);
     }
 
     // ---- 7. pack clusters into workgroups --------------------------------------------------
@@ -484,16 +485,326 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         c.wg = w;
     }
     P.nwg = (int32_t)wg_fill.size();
+    wg_bins.assign(P.nwg, std::vector<std::vector<int64_t>>(1));
+    for (int64_t id : live)
+        for (int64_t v : members[id]) wg_bins[clusters[id].wg][0].push_back(v);
+    for (int64_t x = 0; x < N; ++x) grp[x] = cl[x];
+    } else {
+    // ---- 5s. two-level clustering (sync plans) ---------------------------------------------
+    // Same greedy as step 5, one level down: each lane node starts a wave cluster inside a new
+    // group; for each input (deepest first) it tries (a) to absorb the input's wave cluster
+    // (unit slack: one wave's lanes, the group's waves still pack into the workgroup), then
+    // (b) to absorb the input's group over a local edge (slack kWaveSlack), else (c) cuts it
+    // (slack tile, granules).  Inputs a cut would not delay are cut.
+    const int W = (int)(C / kWaveLanes);
+    if (W < 1 || W > 8 || C % kWaveLanes) return "sync plans need slots = 64 .. 512 lanes";
+    const int64_t hardx = std::min<int64_t>(hard, 128);   // kFlowMaxExt (kernels.hpp)
+    struct WaveCl {
+        int64_t cnt[kMaxChain + 1] = {};
+        int64_t grp = -1;
+        std::vector<int64_t> mem;        // lane nodes
+    };
+    struct Group {
+        std::vector<int64_t> waves;
+        int64_t ext = 0, nloc = 0, root = -1, wg = -1;
+        int32_t dmax = 0, off = 0;
+        bool dead = false;
+    };
+    std::vector<WaveCl> wcl;
+    std::vector<Group> grps;
+    std::vector<int32_t> eh(N, 0);
+    std::vector<int8_t> eslack(N, 0);   // slack of the edge x -> consumer inside its group
+    std::vector<int64_t> ups, lanes_tmp;
+    auto wave_lanes = [&](int64_t w) { return lanes_needed(wcl[w].cnt, K); };
+    // first-fit decreasing of wave clusters (lane counts) into W waves of kWaveLanes
+    auto ffd_fits = [&](std::vector<int64_t>& l) {
+        std::sort(l.begin(), l.end(), std::greater<int64_t>());
+        int64_t bins[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int64_t x : l) {
+            int b = 0;
+            while (b < W && bins[b] + x > kWaveLanes) ++b;
+            if (b == W) return false;
+            bins[b] += x;
+        }
+        return true;
+    };
+    for (int64_t j : lnodes) {
+        ups.assign(lin_list.begin() + lin_off[j], lin_list.begin() + lin_off[j + 1]);
+        std::stable_sort(ups.begin(), ups.end(),
+                         [&](int64_t a, int64_t b) { return eh[a] > eh[b]; });
+        const int64_t wj = (int64_t)wcl.size();
+        wcl.emplace_back();
+        wcl[wj].cnt[weight(j)] = 1;
+        wcl[wj].mem.push_back(j);
+        const int64_t gj = (int64_t)grps.size();
+        grps.emplace_back();
+        grps[gj].waves.push_back(wj);
+        grps[gj].root = j;
+        wcl[wj].grp = gj;
+        cl[j] = wj;
+        const int32_t best = ups.empty() ? -1 : eh[ups[0]];
+        int32_t ehj = 0;
+        bool first = true;
+        for (int64_t u : ups) {
+            const int64_t wu = cl[u], gu = wcl[wu].grp;
+            Group& A = grps[gj];
+            Group& Bg = grps[gu];
+            const int64_t xe = A.ext + A.nloc + Bg.ext + Bg.nloc;
+            const bool want = first || (eh[u] + B > best + 1) || (A.ext + A.nloc + 1 > soft);
+            first = false;
+            bool done = false;
+            if (want && xe <= hardx && Bg.dmax + 1 <= scap) {
+                // (a) unit slack: u's wave cluster joins j's
+                int64_t mc[kMaxChain + 1];
+                for (int L = 0; L <= kMaxChain; ++L) mc[L] = wcl[wj].cnt[L] + wcl[wu].cnt[L];
+                const int64_t lw = lanes_needed(mc, K);
+                if (lw <= kWaveLanes) {
+                    lanes_tmp.clear();
+                    lanes_tmp.push_back(lw);
+                    for (int64_t w : A.waves) if (w != wj) lanes_tmp.push_back(wave_lanes(w));
+                    for (int64_t w : Bg.waves) if (w != wu) lanes_tmp.push_back(wave_lanes(w));
+                    if (ffd_fits(lanes_tmp)) {
+                        for (int L = 0; L <= kMaxChain; ++L) wcl[wj].cnt[L] = mc[L];
+                        for (int64_t v : wcl[wu].mem) {
+                            cl[v] = wj;
+                            wcl[wj].mem.push_back(v);
+                        }
+                        std::vector<int64_t>().swap(wcl[wu].mem);
+                        for (int64_t w : Bg.waves)
+                            if (w != wu) {
+                                A.waves.push_back(w);
+                                wcl[w].grp = gj;
+                            }
+                        A.ext += Bg.ext;
+                        A.nloc += Bg.nloc;
+                        A.dmax = std::max(A.dmax, Bg.dmax + 1);
+                        Bg.dead = true;
+                        eslack[u] = 1;
+                        ehj = std::max(ehj, eh[u] + 1);
+                        done = true;
+                    }
+                }
+            }
+            if (!done && want && xe + 1 <= hardx && Bg.dmax + kWaveSlack <= scap &&
+                eh[u] + kWaveSlack < eh[u] + B) {
+                // (b) local edge: u's group joins j's, its wave clusters unchanged
+                lanes_tmp.clear();
+                for (int64_t w : A.waves) lanes_tmp.push_back(wave_lanes(w));
+                for (int64_t w : Bg.waves) lanes_tmp.push_back(wave_lanes(w));
+                if (ffd_fits(lanes_tmp)) {
+                    for (int64_t w : Bg.waves) {
+                        A.waves.push_back(w);
+                        wcl[w].grp = gj;
+                    }
+                    A.ext += Bg.ext;
+                    A.nloc += Bg.nloc + 1;
+                    A.dmax = std::max(A.dmax, Bg.dmax + kWaveSlack);
+                    Bg.dead = true;
+                    eslack[u] = kWaveSlack;
+                    ehj = std::max(ehj, eh[u] + kWaveSlack);
+                    done = true;
+                }
+            }
+            if (!done) {
+                grps[gj].ext += 1;
+                ehj = std::max(ehj, eh[u] + B);
+            }
+        }
+        if (grps[gj].ext + grps[gj].nloc > hardx) {
+            std::ostringstream m;
+            m << "node " << j << " needs " << grps[gj].ext + grps[gj].nloc
+              << " external inputs (cap " << hardx << ")";
+            return m.str();
+        }
+        eh[j] = ehj;
+    }
+    // ---- 6s. schedule: distances inside groups (unit / kWaveSlack edges), group offsets -----
+    std::vector<int32_t> dist(N, 0);
+    for (auto it = lnodes.rbegin(); it != lnodes.rend(); ++it) {
+        const int64_t j = *it;
+        const int64_t e = lcons(j);
+        dist[j] = (e >= 0 && eslack[j]) ? dist[e] + eslack[j] : 0;
+        grp[j] = wcl[cl[j]].grp;
+    }
+    std::vector<int64_t> live;                   // live groups in root order
+    for (int64_t j : lnodes)
+        if (grps[grp[j]].root == j) live.push_back(grp[j]);
+    P.n_clusters = (int64_t)live.size();
+    for (int64_t id : live) {
+        Group& g = grps[id];
+        g.dmax = 0;
+        for (int64_t w : g.waves)
+            for (int64_t v : wcl[w].mem) g.dmax = std::max(g.dmax, dist[v]);
+        int64_t off = 0;
+        for (int64_t w : g.waves)
+            for (int64_t v : wcl[w].mem) {
+                const int32_t s = g.dmax - dist[v];
+                for (int64_t k = lin_off[v]; k < lin_off[v + 1]; ++k) {
+                    const int64_t u = lin_list[k];
+                    if (grp[u] != id) off = std::max<int64_t>(off, (int64_t)G[u] + B - s);
+                }
+            }
+        if (off > (int64_t)1 << 30) return "schedule overflow (network too deep)";
+        g.off = (int32_t)off;
+        for (int64_t w : g.waves)
+            for (int64_t v : wcl[w].mem) G[v] = g.off + g.dmax - dist[v];
+    }
+    // ---- 7s. pack groups into workgroups: first fit by offset; a group's wave clusters go to
+    // the workgroup's W waves first-fit decreasing (a wave may hold several wave clusters)
+    std::vector<int64_t> by_off(live);
+    std::stable_sort(by_off.begin(), by_off.end(),
+                     [&](int64_t a, int64_t b) { return grps[a].off < grps[b].off; });
+    struct Bin { int64_t cnt[kMaxChain + 1] = {}; };
+    struct Wg {
+        std::vector<Bin> bins;
+        int64_t xe = 0, lo = 0, hi = 0;
+        std::vector<int64_t> groups;
+        bool dead = false;
+    };
+    std::vector<Wg> wgs;
+    std::vector<std::vector<int>> gat(grps.size());       // wave of each of a group's waves
+    auto sorted_waves = [&](int64_t id) {
+        std::vector<int64_t> ws(grps[id].waves);
+        std::stable_sort(ws.begin(), ws.end(), [&](int64_t a, int64_t b) {
+            return wave_lanes(a) > wave_lanes(b);
+        });
+        grps[id].waves = ws;
+    };
+    // place group id into workgroup b (best fit of its wave clusters on b's waves); returns the
+    // lanes b then uses, or -1 when it does not fit.  commit = false only tests.
+    auto place_group = [&](int64_t id, int64_t b, bool commit) -> int64_t {
+        const Group& g = grps[id];
+        Wg& x = wgs[b];
+        if (x.dead) return -1;
+        const int64_t lo = g.off, hi = (int64_t)g.off + g.dmax;
+        if (x.xe + g.ext + g.nloc > std::max<int64_t>(soft, g.ext + g.nloc)) return -1;
+        if (!x.groups.empty() && std::max(x.hi, hi) - std::min(x.lo, lo) > scap) return -1;
+        std::vector<Bin> tmp(x.bins);
+        std::vector<int> at(g.waves.size(), -1);
+        for (size_t q = 0; q < g.waves.size(); ++q) {
+            int64_t bestl = -1;                          // best fit: the fullest wave it fits
+            for (int v = 0; v < W; ++v) {
+                int64_t c2[kMaxChain + 1];
+                for (int L = 0; L <= kMaxChain; ++L) c2[L] = tmp[v].cnt[L] + wcl[g.waves[q]].cnt[L];
+                const int64_t l2 = lanes_needed(c2, K);
+                if (l2 <= kWaveLanes && l2 > bestl) {
+                    bestl = l2;
+                    at[q] = v;
+                }
+            }
+            if (at[q] < 0) return -1;
+            for (int L = 0; L <= kMaxChain; ++L) tmp[at[q]].cnt[L] += wcl[g.waves[q]].cnt[L];
+        }
+        int64_t used = 0;
+        for (int v = 0; v < W; ++v) used += lanes_needed(tmp[v].cnt, K);
+        if (commit) {
+            x.lo = x.groups.empty() ? lo : std::min(x.lo, lo);
+            x.hi = x.groups.empty() ? hi : std::max(x.hi, hi);
+            x.bins = tmp;
+            x.xe += g.ext + g.nloc;
+            x.groups.push_back(id);
+            gat[id] = at;
+            grps[id].wg = b;
+        }
+        return used;
+    };
+    const int kProbe = 64;   // bounded first fit over the most recent workgroups keeps it O(n)
+    for (int64_t id : by_off) {
+        sorted_waves(id);
+        int64_t w = -1, wfill = -1;
+        const int64_t nb = (int64_t)wgs.size();
+        for (int64_t b = std::max<int64_t>(0, nb - kProbe); b < nb; ++b) {
+            const int64_t f = place_group(id, b, false);
+            if (f > wfill) {                           // best fit over the probed workgroups
+                w = b;
+                wfill = f;
+            }
+        }
+        if (w < 0) {
+            w = nb;
+            wgs.emplace_back();
+            wgs[w].bins.assign(W, Bin());
+        }
+        if (place_group(id, w, true) < 0) return "internal: group does not fit a workgroup";
+    }
+    // repair: dissolve the emptiest workgroups into the others where every group of one finds
+    // room (fragmentation at wave granularity costs ~2 % of the lanes; the dataflow kernel needs
+    // every workgroup resident)
+    {
+        std::vector<int64_t> order(wgs.size());
+        std::iota(order.begin(), order.end(), 0);
+        auto lanes_of = [&](const Wg& x) {
+            int64_t u = 0;
+            for (const Bin& bn : x.bins) u += lanes_needed(bn.cnt, K);
+            return u;
+        };
+        std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+            return lanes_of(wgs[a]) < lanes_of(wgs[b]);
+        });
+        for (int64_t w : order) {
+            if (wgs[w].dead || wgs[w].groups.empty()) continue;
+            const std::vector<Wg> save(wgs);
+            const std::vector<std::vector<int>> save_at(gat);
+            std::vector<int64_t> gs(wgs[w].groups);
+            std::vector<int64_t> gwg(gs.size());
+            for (size_t q = 0; q < gs.size(); ++q) gwg[q] = grps[gs[q]].wg;
+            wgs[w].dead = true;
+            bool ok = true;
+            for (int64_t id : gs) {
+                int64_t bestb = -1, bf = -1;
+                for (int64_t b = 0; b < (int64_t)wgs.size(); ++b) {
+                    const int64_t f = place_group(id, b, false);
+                    if (f > bf) {
+                        bf = f;
+                        bestb = b;
+                    }
+                }
+                if (bestb < 0) {
+                    ok = false;
+                    break;
+                }
+                place_group(id, bestb, true);
+            }
+            if (!ok) {
+                wgs = save;
+                gat = save_at;
+                for (size_t q = 0; q < gs.size(); ++q) grps[gs[q]].wg = gwg[q];
+                for (int64_t b = 0; b < (int64_t)wgs.size(); ++b)
+                    for (int64_t id : wgs[b].groups) grps[id].wg = b;
+            }
+        }
+    }
+    // compact: live workgroups in creation order
+    std::vector<int64_t> wid(wgs.size(), -1);
+    int32_t nw = 0;
+    for (size_t b = 0; b < wgs.size(); ++b)
+        if (!wgs[b].dead && !wgs[b].groups.empty()) wid[b] = nw++;
+    P.nwg = nw;
+    wg_bins.assign(P.nwg, std::vector<std::vector<int64_t>>(W));
+    for (size_t b = 0; b < wgs.size(); ++b) {
+        if (wid[b] < 0) continue;
+        for (int64_t id : wgs[b].groups)
+            for (size_t q = 0; q < grps[id].waves.size(); ++q)
+                for (int64_t v : wcl[grps[id].waves[q]].mem)
+                    wg_bins[wid[b]][gat[id][q]].push_back(v);
+    }
+    }
     P.nslots = (int64_t)P.nwg * RS;
+    for (int64_t x = 0; x < N; ++x) {
+        if (top[x] != x) {
+            G[x] = G[top[x]];
+            cl[x] = cl[top[x]];
+            grp[x] = grp[top[x]];
+        }
+        P.gmax = std::max(P.gmax, G[x]);
+    }
 
     // ---- 8. slot assignment ----------------------------------------------------------------
-    // node slot of a workgroup: position * slots + lane.  The workgroup's chains are packed
-    // into lanes first-fit decreasing (longest first, best fit on the free positions: the
-    // packing lanes_needed counts), a chain on consecutive positions bottom first; lanes are
-    // then ordered by their earliest G, so a wave holds nodes that are active at the same ticks.
-    std::vector<std::vector<int64_t>> wg_chains(P.nwg);
-    for (int64_t id : live)
-        for (int64_t v : members[id]) wg_chains[clusters[id].wg].push_back(v);
+    // node slot of a workgroup: position * slots + lane.  The chains of each lane bin (the
+    // workgroup, or one wave of it in sync plans) are packed into lanes first-fit decreasing
+    // (longest first, best fit on the free positions: the packing lanes_needed counts), a chain
+    // on consecutive positions bottom first; lanes are then ordered by their earliest G, so a
+    // wave holds nodes that are active at the same ticks.
     P.slot_reach.assign(P.nslots, -1);
     P.G.assign(P.nslots, 0);
     P.flags.assign(P.nslots, kSlotPad);
@@ -518,7 +829,8 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     std::vector<int64_t> open[kMaxChain];            // lanes with f free positions
     std::vector<int64_t> lane_order;
     for (int32_t w = 0; w < P.nwg; ++w) {
-        auto& ch = wg_chains[w];
+      for (size_t bi = 0; bi < wg_bins[w].size(); ++bi) {
+        auto& ch = wg_bins[w][bi];
         std::stable_sort(ch.begin(), ch.end(), [&](int64_t a, int64_t b) {
             return weight(a) != weight(b) ? weight(a) > weight(b) : G[a] < G[b];
         });
@@ -542,7 +854,7 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             const int f = K - (int)lanes[ln].size();
             if (f > 0) open[f].push_back(ln);
         }
-        if ((int64_t)lanes.size() > C) return "internal: workgroup overfull";
+        if ((int64_t)lanes.size() > bin_lanes) return "internal: workgroup overfull";
         lane_order.resize(lanes.size());
         std::vector<int32_t> lane_g(lanes.size(), INT32_MAX);
         for (size_t l = 0; l < lanes.size(); ++l) {
@@ -551,12 +863,14 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
         }
         std::stable_sort(lane_order.begin(), lane_order.end(),
                          [&](int64_t a, int64_t b) { return lane_g[a] < lane_g[b]; });
-        const int64_t base = (int64_t)w * RS;
+        const int64_t base = (int64_t)w * RS + (int64_t)bi * bin_lanes;
         for (size_t l = 0; l < lane_order.size(); ++l) {
             const auto& nodes_l = lanes[lane_order[l]];
             for (size_t p = 0; p < nodes_l.size(); ++p)
                 place(nodes_l[p], base + (int64_t)p * C + (int64_t)l);
         }
+      }
+        const int64_t base = (int64_t)w * RS;
         int32_t lo = INT32_MAX, hi = INT32_MIN;
         for (int64_t d = base; d < base + RS; ++d)
             if (P.flags[d] != kSlotPad) {
@@ -571,6 +885,9 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // input codes and external lists
     P.ext_off.assign(P.nwg + 1, 0);
     std::vector<std::vector<std::pair<int64_t, int32_t>>> ext(P.nwg);  // (src node, consumer G)
+    std::vector<std::vector<int64_t>> loc(P.nwg);                       // local edges' sources
+    struct LocRef { int64_t d; int k; int32_t li; };
+    std::vector<LocRef> loc_ref;
     std::vector<int64_t> node_at(P.nslots, -1);
     for (int64_t x = 0; x < N; ++x) node_at[npos[x]] = x;
     for (int64_t d = 0; d < P.nslots; ++d) {
@@ -591,6 +908,16 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
             } else if (cl[u] == cl[j]) {
                 if (G[j] != G[u] + 1) return "internal: in-cluster edge without unit slack";
                 code = (uint16_t)(npos[u] - (int64_t)w * RS);
+                if (P.p.sync && (npos[u] % RS) % C / kWaveLanes != (d % RS) % C / kWaveLanes)
+                    return "internal: unit-slack edge across waves";
+            } else if (grp[u] == grp[j]) {
+                // local edge of a sync plan: column (granule inputs of w) + index, patched below
+                if (G[j] != G[u] + kWaveSlack) return "internal: local edge without its slack";
+                if (npos[u] / RS != w) return "internal: local edge across workgroups";
+                loc[w].push_back(u);
+                loc_ref.push_back({d, (int)(k - k0), (int32_t)(loc[w].size() - 1)});
+                code = 0;
+                P.n_local++;
             } else {
                 if (G[j] < G[u] + B) return "internal: cross-cluster edge without tile slack";
                 const size_t e = ext[w].size();
@@ -606,7 +933,25 @@ std::string build_plan(int64_t n, const int64_t* endnodes, const int64_t* indegr
     // each node has one consumer, so it feeds at most one external input; ext_src names the
     // source's row of the output arrays: the reach, or n + slot for a partial-sum node
     P.xid.assign(P.nslots, -1);
+    P.lx.assign(P.nslots, -1);
+    P.lx_off.assign(P.nwg + 1, 0);
+    for (const LocRef& r : loc_ref) {
+        const int32_t w = (int32_t)(r.d / RS);
+        const int64_t e = (int64_t)ext[w].size() + r.li;
+        if (e >= 0x7fff) return "internal: local input index";
+        P.up4[r.d] |= (uint64_t)(kExtBit | (uint16_t)e) << (16 * r.k);
+    }
     for (int32_t w = 0; w < P.nwg; ++w) {
+        P.lx_off[w + 1] = P.lx_off[w] + (int32_t)loc[w].size();
+        const int64_t xe = (int64_t)ext[w].size() + (int64_t)loc[w].size();
+        if (xe > hard) return "internal: external-input cap exceeded";
+        P.max_xe_wg = std::max(P.max_xe_wg, (int32_t)xe);
+        for (size_t li = 0; li < loc[w].size(); ++li) {
+            const int64_t src = npos[loc[w][li]];
+            if (P.lx[src] != -1 || P.xid[src] != -1) return "internal: node feeds two inputs";
+            P.lx[src] = (int16_t)(ext[w].size() + li);
+            P.lx_src.push_back((int32_t)src);
+        }
         P.ext_off[w + 1] = P.ext_off[w] + (int32_t)ext[w].size();
         P.max_ext_wg = std::max(P.max_ext_wg, (int32_t)ext[w].size());
         for (auto& pr : ext[w]) {

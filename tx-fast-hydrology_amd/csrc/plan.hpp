@@ -31,7 +31,22 @@ struct PlanParams {
     int32_t tile = 32;         // ticks per launch; also the slack of a cross-cluster edge
     int32_t ext_cap = 64;      // preferred max cross-cluster inputs per workgroup (soft)
     int32_t chain = 2;         // node slots per lane (positions 0 .. chain-1, see "lane chains")
+    int32_t sync = 0;          // 1: chunk-synchronous plan ("wave clusters" below)
 };
+
+// Chunk-synchronous plans (sync = 1, the dataflow kernel's default for one member): the kernel
+// joins its waves with ONE workgroup barrier per chunk of kChunk ticks instead of one per tick.
+// A unit-slack edge (value of tick k read at tick k + 1) must then stay inside one wave (LDS
+// accesses of one wave are processed in order), so the clustering is two-level:
+//   * a WAVE CLUSTER is a connected sub-tree that fits one wave's lanes; inside it
+//     G[u] = G[down] - 1 (or a chained edge);
+//   * a GROUP is a connected tree of wave clusters placed in one workgroup; an edge between two
+//     of its wave clusters has slack exactly kWaveSlack = kChunk: the producer writes its tick-k
+//     output straight into the consumer's external-input column for tick k + kChunk (the next
+//     chunk's ring slot, kernels read it after the chunk barrier) -- a "local" external input;
+//   * edges between groups are cross-workgroup (slack >= tile, granules), as before.
+constexpr int kWaveSlack = 4;
+constexpr int kWaveLanes = 64;
 
 // Lane chains: a lane owns `chain` node slots (positions), computed in order within one tick;
 // a node at position p >= 1 may take the output of position p - 1 of the SAME tick (a chained
@@ -88,10 +103,18 @@ struct Plan {
     std::vector<uint8_t> up_cnt;
     std::vector<uint64_t> up4;         // first kUpInline codes, 16 bits each
     std::vector<int32_t> xid;          // external input this slot feeds (index into ext_*), -1
+    // sync plans: the workgroup-local external input (XE column of the slot's own workgroup,
+    // after its ext_off range of granule inputs) this slot's output feeds kWaveSlack ticks
+    // later, -1 if none
+    std::vector<int16_t> lx;
+    int64_t n_local = 0;               // sync plans: local (slack kWaveSlack) edges
+    int32_t max_xe_wg = 0;             // external columns of a workgroup: granule + local
 
     // per workgroup
     std::vector<int32_t> wg_gmin, wg_gmax;  // G range of the workgroup's real reaches
-    std::vector<int32_t> ext_off;           // [nwg + 1]
+    std::vector<int32_t> ext_off;           // [nwg + 1] granule (cross-workgroup) inputs
+    std::vector<int32_t> lx_off;            // [nwg + 1] local inputs (sync plans)
+    std::vector<int32_t> lx_src;            // producer slot of each local input
     std::vector<int64_t> ext_src;           // source row: reach index, or n + slot (partial sum)
     std::vector<int32_t> ext_g;             // G of the consuming reach
 

@@ -38,7 +38,8 @@ class TopologyError(RoutingError, ValueError):
 
 class PlanParams(ctypes.Structure):
     _fields_ = [("slots", ctypes.c_int32), ("tile", ctypes.c_int32),
-                ("ext_cap", ctypes.c_int32), ("chain", ctypes.c_int32)]
+                ("ext_cap", ctypes.c_int32), ("chain", ctypes.c_int32),
+                ("sync", ctypes.c_int32)]
 
 
 class PlanInfo(ctypes.Structure):
@@ -49,7 +50,7 @@ class PlanInfo(ctypes.Structure):
                 ("max_height", ctypes.c_int32), ("max_ext_wg", ctypes.c_int32),
                 ("n_partial", ctypes.c_int64), ("n_ext", ctypes.c_int64),
                 ("n_pairs", ctypes.c_int64), ("chain", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("n_local", ctypes.c_int32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -67,6 +68,7 @@ SIGNATURES = {
     "mc_plan_get_info": (_i32, [_vp, ctypes.POINTER(PlanInfo)]),
     "mc_plan_export": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "mc_plan_export_links": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mc_plan_export_local": (_i32, [_vp, _vp, _vp]),
     "mc_plan_schedule": (_i32, [_vp, _i64, ctypes.POINTER(ctypes.c_int64),
                                 ctypes.POINTER(ctypes.c_int64), _vp, _vp]),
     "mc_plan_paths": (_i32, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
@@ -168,7 +170,11 @@ def lib():
     except OSError as exc:
         raise NativeUnavailable(f"cannot load {path}: {exc}") from exc
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None and "MCROUTE_LIB" in os.environ:
+            continue            # an explicitly chosen (older) build for an A/B run
+        if fn is None:
+            raise NativeUnavailable(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     _lib = L

@@ -16,8 +16,8 @@ from . import _native as nat
 from ._native import f64, i64, ptr
 
 
-def _params(slots=0, tile=0, ext_cap=0, chain=0):
-    return nat.PlanParams(int(slots), int(tile), int(ext_cap), int(chain))
+def _params(slots=0, tile=0, ext_cap=0, chain=0, sync=0):
+    return nat.PlanParams(int(slots), int(tile), int(ext_cap), int(chain), int(sync))
 
 
 # Resident shapes of a single-member session (lanes, slots per lane, ns per tick): one compute
@@ -30,15 +30,38 @@ _DET_SHAPE_MAX_N = 50_000
 _DET_SHAPE_T = 288            # nominal horizon for the estimate: (schedule + T) ticks
 
 
+# (lanes, chain) shapes of the dataflow kernel that run chunk-synchronous plans
+# (kernels.hpp MCR_SYNC_SHAPES)
+SYNC_SHAPES = {(64, 1), (64, 2), (128, 2), (192, 2), (256, 2), (192, 3)}
+
+_det_shape_cache: dict = {}
+
+
 def _det_shape(end, deg, heads, chain):
     """(lanes, chain) of a single-member session's default plan: the shape whose schedule of a
-    nominal horizon ticks least long (host plans of both, small networks only)."""
+    nominal horizon ticks least long (host plans of both, small networks only).  The decision
+    is cached by topology, so the sub-basin DAG's many sessions plan each network once here.
+    The shape is fixed for the session's lifetime (set_members keeps the plan)."""
     if chain or end.size == 0 or end.size > _DET_SHAPE_MAX_N:
         return 192, chain
+    import hashlib
+    key = hashlib.sha1(b"".join(np.ascontiguousarray(a).tobytes()
+                                for a in (end, deg, heads))).hexdigest()
+    hit = _det_shape_cache.get(key)
+    if hit is not None:
+        return hit
+    if len(_det_shape_cache) > 4096:
+        _det_shape_cache.clear()
+    _det_shape_cache[key] = shape = _det_shape_plan(end, deg, heads, chain)
+    return shape
+
+
+def _det_shape_plan(end, deg, heads, chain):
     best = None
     for lanes, k, ns_tick in _DET_SHAPES:
         try:
-            p = Plan(end, deg, heads, slots=lanes, tile=16, chain=k)
+            p = Plan(end, deg, heads, slots=lanes, tile=16, chain=k,
+                     sync=1 if (lanes, k) in SYNC_SHAPES else 0)
         except Exception:       # (a shape the plan cannot build: keep the other)
             continue
         est = (p.info["gmax"] + _DET_SHAPE_T) * ns_tick
@@ -51,7 +74,8 @@ def _det_shape(end, deg, heads, chain):
 class Plan:
     """Compiled schedule of a network (no device memory)."""
 
-    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, chain=0):
+    def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, chain=0,
+                 sync=0):
         L = nat.lib()
         self._end = i64(endnodes)
         self._deg = i64(indegree)
@@ -60,7 +84,7 @@ class Plan:
         if self._deg.size != self.n:
             raise ValueError("indegree and endnodes must have the same length")
         h = ctypes.c_void_p()
-        p = _params(slots, tile, ext_cap, chain)
+        p = _params(slots, tile, ext_cap, chain, sync)
         nat.check(L.mc_plan_create(self.n, ptr(self._end), ptr(self._deg), ptr(self._heads),
                                    self._heads.size, ctypes.byref(p), ctypes.byref(h)))
         self._h = h
@@ -91,6 +115,16 @@ class Plan:
         nat.check(nat.lib().mc_plan_export_links(
             self._h, *(ptr(out[k]) for k in ("flags", "up_cnt", "up4", "ext_off", "ext_src",
                                              "ext_g"))))
+        return out
+
+    def export_local(self) -> dict:
+        """Local edges of a chunk-synchronous plan: lx_off [nwg + 1], lx_src [n_local]."""
+        info = self.info
+        out = dict(lx_off=np.zeros(info["nwg"] + 1, np.int32),
+                   lx_src=np.empty(max(info["n_local"], 1), np.int32))
+        nat.check(nat.lib().mc_plan_export_local(self._h, ptr(out["lx_off"]),
+                                                 ptr(out["lx_src"])))
+        out["lx_src"] = out["lx_src"][: info["n_local"]]
         return out
 
     def schedule(self, T: int):
@@ -175,7 +209,7 @@ class RoutingNet:
     """
 
     def __init__(self, endnodes, indegree, headwaters, slots=0, tile=0, ext_cap=0, members=1,
-                 chain=0):
+                 chain=0, sync=None):
         L = nat.lib()
         end = i64(endnodes)
         deg = i64(indegree)
@@ -192,7 +226,10 @@ class RoutingNet:
             # two chunks (0.605 -> 0.594 ms)
             slots, chain = _det_shape(end, deg, heads, chain)
             tile = tile or 16
-        p = _params(slots, tile, ext_cap, chain)
+            if sync is None:
+                # chunk-synchronous plan (plan.hpp): one workgroup barrier per 4 ticks
+                sync = 1 if (slots, chain or 2) in SYNC_SHAPES else 0
+        p = _params(slots, tile, ext_cap, chain, sync or 0)
         nat.check(L.mc_net_create(self.n, ptr(end), ptr(deg), ptr(heads), heads.size,
                                   ctypes.byref(p), ctypes.byref(h)))
         self._h = h

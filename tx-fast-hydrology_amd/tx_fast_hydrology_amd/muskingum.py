@@ -164,6 +164,10 @@ class _InflowBlock:
 
     def fetch(self):
         if self.rows is None:
+            if getattr(self.net, "_h", 1) is None:
+                # Muskingum.close() settles its rows first; a block kept past that is an error
+                raise RuntimeError("inflow rows were requested after their device session "
+                                   "was closed")
             if self.net.runs != self.run_id:
                 # the model settles its lazy rows before anything reruns its session
                 raise RuntimeError("inflow rows of an earlier run were requested after the "
@@ -342,6 +346,11 @@ class Muskingum:
         return state
 
     def __setstate__(self, state):
+        # a model pickled before the inflows became lazy properties stores them under their
+        # public names, which the properties would shadow
+        for key in ("i_t_next", "i_t_prev"):
+            if key in state:
+                state["_" + key] = state.pop(key)
         self.__dict__.update(state)
         self._device = _DeviceRouting()
         self._own_coefs()
@@ -375,7 +384,10 @@ class Muskingum:
                 setattr(self, name, a)
 
     def close(self):
-        """Release the device session (it is recreated by the next routing call)."""
+        """Release the device session (it is recreated by the next routing call).  Inflow rows a
+        fused horizon left on the session are copied to the host first, so the state stays
+        readable (and a held simulate() generator can still settle)."""
+        self._settle_inflows()
         self._device.close()
 
     # -- properties ----------------------------------------------------------------------------
