@@ -101,7 +101,7 @@ def parse(argv=None, world=None):
     ap.add_argument("--huc8", action="store_true",
                     help="BASELINE configs[0]: one HUC-8 sub-basin (1000 reaches, one outlet, "
                          "deepest path ~100 reaches), deterministic")
-    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow", "paths"],
+    ap.add_argument("--mode", default="auto", choices=["auto", "launches", "dataflow"],
                     help="execution path (mcroute.h mc_set_mode)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -281,7 +281,7 @@ def build_workload(args, rank=0, world=1):
         # launches: the multi-launch ensemble shape), the state handed over on the device
         fnet = engine.RoutingNet(end, indeg, heads, slots=getattr(args, "fslots", 256),
                                  tile=getattr(args, "ftile", 64), members=E)
-        # (the one-step modes "dataflow" / "paths" select the analysis plan's member-step path;
+        # (the one-step mode "dataflow" selects the analysis plan's member-step path;
         # the forecast is a multi-step ensemble horizon: launches)
         fnet.set_mode("launches" if getattr(args, "mode", "auto") == "launches" else "auto")
         fnet.set_coeffs(alpha, beta, chi, gamma)
@@ -320,36 +320,108 @@ def compulsory_bytes(n, E, T, rows):
     return 8.0 * n * (E * T + E * rows + 4 + 4 * E)
 
 
+def run_horizon(net, wl):
+    """One bench step: a 24-h horizon of the workload, with the EnKF cycle where configured --
+    one-step member runs each followed by the (member-sharded) analysis while observations
+    exist (da.py:56-61), then the forecast on its own plan with the state handed over on the
+    device (tests/test_gpu_enkf_horizon.py checks exactly this sequence)."""
+    x = wl.x
+    if wl.enkf is None:
+        net.run(x)
+        return
+    from tx_fast_hydrology_amd import ensemble
+    ek = wl.enkf
+    for k in range(ek.n_an):       # analysis at every model step while obs exist
+        net.run(x[k:k + 1])
+        ensemble.distributed_analysis(net, ek.gauges, ek.Y[k], ek.R)
+    if getattr(ek, "fnet", None) is None:
+        net.run(x[ek.n_an:])
+        return
+    ek.fnet.copy_state_from(net)
+    ek.fnet.run(x[ek.n_an:])
+    net.copy_state_from(ek.fnet)
+
+
+def run_emulated_horizon(nets, wls, stream, stage_ms=None, rec=None):
+    """The configs[3] horizon as N = len(nets) member shards on one GPU (all sessions on the
+    torch stream `stream`): each shard's one-step member run, the analysis through
+    ensemble.emulated_analysis (the N-rank stage program, collectives as device copies), then
+    each shard's forecast with the device hand-over.  rec(r, part, fn) wraps each shard's parts
+    (timing); stage_ms collects the analysis stages' device times."""
+    import torch
+
+    from tx_fast_hydrology_amd import ensemble
+    rec = rec or (lambda r, part, fn: fn())
+    N = len(nets)
+    ek0 = wls[0].enkf
+    x = wls[0].x
+    for k in range(ek0.n_an):
+        for r in range(N):
+            rec(r, "member_steps", lambda r=r: nets[r].run(x[k:k + 1]))
+        with torch.cuda.stream(stream):
+            ensemble.emulated_analysis(nets, ek0.gauges, [wls[r].enkf.Y[k] for r in range(N)],
+                                       ek0.R, stage_ms=stage_ms)
+    for r in range(N):
+        f = wls[r].enkf.fnet
+
+        def fc(r=r, f=f):
+            f.copy_state_from(nets[r])
+            f.run(x[ek0.n_an:])
+            nets[r].copy_state_from(f)
+        rec(r, "forecast", fc)
+
+
+def enkf_restatement(wl, orc, o, i, fp, Y, cores, x_out=None):
+    """Host restatement of the EnKF horizon (test infrastructure and the CPU baseline): the
+    members through the C member loop (OpenMP), at each analysis step the observation-space
+    analysis of da.py:112-126 with the ensemble sample covariance, A HA^T (HA HA^T / (E - 1) +
+    R)^-1 (Y - HX) / (E - 1), applied by the C _apply_gain (nutils.py:116-134), then the forecast.
+    Y: per analysis step [m][E].  Returns the final (o, i) [n][E] and, for steps listed in x_out,
+    the forecast outputs {t: (o_t, i_t)}."""
+    ek = wl.enkf
+    E = o.shape[1]
+    g = ek.gauges
+    coef = (wl.alpha, wl.beta, wl.chi, wl.gamma)
+    heads = wl.start[wl.indeg == 0]
+    x = wl.x
+    o, i = np.ascontiguousarray(o), np.ascontiguousarray(i)
+    for k in range(ek.n_an):
+        o, i = orc.simulate_members(wl.start, wl.end, wl.indeg, *coef, o, i, x[k:k + 1],
+                                    wl.xp, fp, threads=cores)
+        A = o - o.mean(1, keepdims=True)
+        HA = A[g]
+        W = np.linalg.solve(HA @ HA.T / (E - 1) + ek.R, Y[k] - o[g])
+        G = A @ (HA.T @ W) / (E - 1)
+        for e in range(E):
+            ig, og = orc.apply_gain(heads, wl.end, np.ascontiguousarray(G[:, e]), wl.indeg)
+            o[:, e] += og
+            i[:, e] += ig
+        o, i = np.ascontiguousarray(o), np.ascontiguousarray(i)
+    outs = {}
+    t0 = ek.n_an
+    targets = sorted(set(x_out or []))
+    for t1 in targets + [x.size]:
+        if t1 > t0:
+            o, i = orc.simulate_members(wl.start, wl.end, wl.indeg, *coef, o, i, x[t0:t1],
+                                        wl.xp, fp, threads=cores)
+            t0 = t1
+        if t1 in targets:
+            outs[t1 - 1] = (o.copy(), i.copy())
+    return o, i, outs
+
+
 def cpu_enkf_baseline(args, wl, orc):
     """Host baseline of the EnKF horizon on a bounded sample: min(E, cores) members through the C
     member loop (OpenMP) with a NumPy ensemble analysis at the analysis steps."""
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     ek = wl.enkf
     ms = min(wl.E, cores)
-    o = np.ascontiguousarray(wl.o0[:, :ms])
-    i = np.ascontiguousarray(wl.i0[:, :ms])
     fp = np.ascontiguousarray(wl.fp[:, :, :ms])
-    x = wl.x
-    g = ek.gauges
-    coef = (wl.alpha, wl.beta, wl.chi, wl.gamma)
-    heads = wl.start[wl.indeg == 0]
+    Y = [y[:, :ms] for y in ek.Y]
     reps, t = 0, 0.0
     while t < args.cpu_seconds or reps == 0:
         c0 = time.perf_counter()
-        for k in range(ek.n_an):
-            o, i = orc.simulate_members(wl.start, wl.end, wl.indeg, *coef, o, i, x[k:k + 1],
-                                        wl.xp, fp, threads=cores)
-            A = o - o.mean(1, keepdims=True)
-            HA = A[g]
-            W = np.linalg.solve(HA @ HA.T / (ms - 1) + ek.R, ek.Y[k][:, :ms] - o[g])
-            G = A @ (HA.T @ W) / (ms - 1)
-            for e in range(ms):
-                ig, og = orc.apply_gain(heads, wl.end, np.ascontiguousarray(G[:, e]), wl.indeg)
-                o[:, e] += og
-                i[:, e] += ig
-            o, i = np.ascontiguousarray(o), np.ascontiguousarray(i)
-        o, i = orc.simulate_members(wl.start, wl.end, wl.indeg, *coef, o, i, x[ek.n_an:], wl.xp,
-                                    fp, threads=cores)
+        enkf_restatement(wl, orc, wl.o0[:, :ms], wl.i0[:, :ms], fp, Y, cores)
         t += time.perf_counter() - c0
         reps += 1
     return {"value": float(wl.n) * ms * args.T * reps / t, "unit": "reach·member·timesteps/s",
@@ -466,21 +538,7 @@ def emulated_shards(args, t1_ms):
         spans.append((r, part, a, b))
 
     def horizon(stage_ms):
-        for k in range(ek0.n_an):
-            for r in range(N):
-                rec(r, "member_steps", lambda r=r: nets[r].run(x[k:k + 1]))
-            with torch.cuda.stream(stream):
-                ensemble.emulated_analysis(nets, ek0.gauges,
-                                           [wls[r].enkf.Y[k] for r in range(N)], ek0.R,
-                                           stage_ms=stage_ms)
-        for r in range(N):
-            f = wls[r].enkf.fnet
-
-            def fc(r=r, f=f):
-                f.copy_state_from(nets[r])
-                f.run(x[ek0.n_an:])
-                nets[r].copy_state_from(f)
-            rec(r, "forecast", fc)
+        run_emulated_horizon(nets, wls, stream, stage_ms, rec)
 
     with torch.cuda.stream(stream):
         horizon({})                                     # warm-up (plans, buffers)
@@ -589,19 +647,7 @@ def main():
 
     def horizon():
         """One bench step: a 24-h horizon (with the analysis steps of the EnKF workload)."""
-        if wl.enkf is None:
-            net.run(x)
-            return
-        ek = wl.enkf
-        for k in range(ek.n_an):       # analysis at every model step while obs exist
-            net.run(x[k:k + 1])
-            ensemble.distributed_analysis(net, ek.gauges, ek.Y[k], ek.R)
-        if getattr(ek, "fnet", None) is None:
-            net.run(x[ek.n_an:])
-            return
-        ek.fnet.copy_state_from(net)
-        ek.fnet.run(x[ek.n_an:])
-        net.copy_state_from(ek.fnet)
+        run_horizon(net, wl)
     info = net.info
     setup_s = time.time() - t_setup
 

@@ -109,11 +109,6 @@ int mc_plan_export_local(const void* plan, int32_t* lx_off, int32_t* lx_src);
  * (*n_launch, *n_list); then with arrays of at least n_launch+1 / n_list entries. */
 int mc_plan_schedule(const void* plan, int64_t T, int64_t* n_launch, int64_t* n_list,
                      int64_t* off, int32_t* list);
-/* Member-path plan of the network (the one-step ensemble sweep, paths.hpp; host only, for tests
- * and diagnostics): call with the arrays NULL for the sizes (*n_tasks, *n_ovf), then with
- * task_off [n_tasks + 1], seq_reach [n], rec [n * 16] (node records) and ovf [n_ovf]. */
-int mc_plan_paths(const void* plan, int64_t* n_tasks, int64_t* n_ovf, int32_t* task_off,
-                  int64_t* seq_reach, int32_t* rec, int32_t* ovf);
 int mc_plan_destroy(void* plan);
 
 /* ---- stateless mirror of nutils._ax_bu (nutils.py:64-89) -------------------------------- */
@@ -279,9 +274,8 @@ int mc_reset_timing(void* net);
 /* Execution path of mc_run / mc_step.  mode 0 (default): one resident dataflow launch for the
  * whole horizon when the network fits the device at once, else launches of `tile` ticks;
  * 1: always launches of `tile` ticks; 2: dataflow only (MC_E_STATE when it does not fit; a
- * one-step ensemble run is a member-dataflow launch); 3: auto, with every one-step ensemble run
- * swept along the member paths instead (paths.hpp; opt-in: modes 0-2 never take them).
- * last_path: 1 launches, 2 dataflow, 3 member paths (0 before any run). */
+ * one-step ensemble run is a member-dataflow launch).
+ * last_path: 1 launches, 2 dataflow (0 before any run). */
 int mc_set_mode(void* net, int mode);
 int mc_get_mode(void* net, int* mode, int* last_path);
 

@@ -19,13 +19,13 @@ from tx_fast_hydrology_amd import engine, synthetic
 pytestmark = pytest.mark.gpu
 
 
-def _net(end, members=1, slots=0):
+def _net(end, members=1, slots=0, **kw):
     n = end.size
     start = np.arange(n)
     indeg = orc.compute_indegree(start, end)
     K, X, _ = synthetic.model_arrays(n, seed=n)
     coef = orc.muskingum_coeffs(K, X, 300.0)
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=members)
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, members=members, **kw)
     net.set_coeffs(*coef)
     return net, start, indeg
 
@@ -288,14 +288,14 @@ def test_enkf256_large_mean_and_zero_spread_reaches():
     np.testing.assert_allclose(o[rest] - X[rest], G[rest], rtol=0, atol=1e-10 * np.abs(G).max())
 
 
-@pytest.mark.parametrize("E,mode", [(32, "auto"), (256, "auto"), (32, "paths"),
-                                    (100, "paths")])
-def test_lazy_gain_folded_into_member_step(E, mode):
+@pytest.mark.parametrize("E,mode,sync", [(32, "auto", 0), (256, "auto", 0), (32, "auto", 1),
+                                         (256, "auto", 1), (100, "launches", 1)])
+def test_lazy_gain_folded_into_member_step(E, mode, sync):
     """The analysis increments are applied lazily: the next one-step member run applies them
-    while it stages its inputs (launch_member_inputs / path_prep with the pending gain) instead
-    of a separate apply_gain pass.  An EnKF cycle run that way is bit-identical to the same cycle
-    with the gain settled right after every analysis (get_state forces it), outputs included --
-    on both one-step paths (auto: the member-dataflow launch; the member paths opt-in)."""
+    while it stages its inputs (launch_member_inputs with the pending gain) instead of a separate
+    apply_gain pass.  An EnKF cycle run that way is bit-identical to the same cycle with the gain
+    settled right after every analysis (get_state forces it), outputs included -- on the
+    member-dataflow launch of classic and chunk-synchronous plans and on launches."""
     end = synthetic.river_network(5000, 5, 150, np.random.default_rng(4))
     n = end.size
     m = 25
@@ -309,7 +309,7 @@ def test_lazy_gain_folded_into_member_step(E, mode):
     Ys = [X[s].mean(1, keepdims=True) + 0.2 + rng.normal(0, 0.1, (m, E)) for _ in range(3)]
     res = []
     for settle in (False, True):
-        net, start, indeg = _net(end, members=E, slots=192)
+        net, start, indeg = _net(end, members=E, slots=192, tile=16, sync=sync)
         net.set_mode(mode)
         net.set_state(X, I0)
         net.load_forcing(xp, fp)

@@ -210,13 +210,14 @@ def _edge_net():
     return start, end, indeg, start[indeg == 0], coef
 
 
-@pytest.mark.parametrize("mode", ["launches", "auto", "dataflow", "paths"])
-def test_non_finite_ensemble_matches_reference(mode):
+@pytest.mark.parametrize("mode,sync", [("launches", 0), ("auto", 0), ("dataflow", 0),
+                                       ("dataflow", 1), ("launches", 1)])
+def test_non_finite_ensemble_matches_reference(mode, sync):
     """The same contract for an ensemble session: member e is an independent reference run
     (SURVEY a5).  Member 0 carries the non-finite forcing and state of the single-member test,
     member 1 is finite, member 2 overflows inside reach 5's partial sums from finite inputs.
-    A horizon (multi-launch) and one-step runs (member dataflow, or member paths in mode
-    "paths") give every cell of every member exactly as the oracle does."""
+    A horizon (multi-launch) and one-step runs (member dataflow; classic and chunk-synchronous
+    plans) give every cell of every member exactly as the oracle does."""
     start, end, indeg, heads, coef = _edge_net()
     n, E = end.size, 3
     o0 = np.stack([np.linspace(1.0, 2.0, n)] * E, axis=1)
@@ -235,7 +236,7 @@ def test_non_finite_ensemble_matches_reference(mode):
     c = np.ascontiguousarray
     want = [orc.simulate(start, end, indeg, *coef, c(o0[:, e]), c(i0[:, e]), x, xp, c(fp[:, :, e]))
             for e in range(E)]
-    net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16, members=E)
+    net = engine.RoutingNet(end, indeg, heads, slots=64, tile=16, members=E, sync=sync)
     net.set_coeffs(*coef)
     if mode != "dataflow":                           # dataflow mode routes one step only
         net.set_mode(mode)
@@ -258,7 +259,7 @@ def test_non_finite_ensemble_matches_reference(mode):
         for e in range(E):
             assert _same(got_o[0, :, e], want[e][0][t]), (t, e)
             assert _same(got_i[0, :, e], want[e][1][t]), (t, e)
-    path = {"launches": "launches", "auto": "dataflow", "dataflow": "dataflow", "paths": "paths"}
+    path = {"launches": "launches", "auto": "dataflow", "dataflow": "dataflow"}
     assert net.mode()[1] == path[mode]
     # mc_step: the forcing row is q itself
     net.set_state(o0, i0)

@@ -120,19 +120,25 @@ def test_ensemble_rejects_dataflow_and_bad_shapes():
     (3000, 33, 256, 0, "dataflow"), (1200, 2, 128, 0, "dataflow"), (4000, 256, 384, 0, "dataflow"),
     (2500, 137, 192, 0, "dataflow"), (190_000, 32, 384, 0, "dataflow"),
     (190_000, 32, 192, 16, "dataflow"),
-    (3000, 33, 256, 0, "paths"), (1200, 2, 128, 0, "paths"), (4000, 256, 384, 0, "paths"),
-    (2500, 137, 192, 0, "paths"), (2500, 64, 192, 16, "paths"), (190_000, 32, 192, 16, "paths")])
+    (3000, 33, 256, 16, "sync"), (1200, 2, 128, 16, "sync"), (4000, 256, 192, 16, "sync"),
+    (2500, 137, 192, 16, "sync"), (2500, 64, 192, 16, "sync"), (190_000, 32, 192, 16, "sync"),
+    (190_000, 256, 192, 16, "sync")])
 def test_member_dataflow_single_steps(n, E, slots, tile, mode):
-    """One-step runs of an ensemble (the analysis cycle of the EnKF) on both one-step paths: the
-    member-dataflow launch (member e of slot d at tick G[d] + e) and the member paths (paths.hip:
-    heavy paths swept by waves, members on the lanes, several member groups beyond 64).  Several
+    """One-step runs of an ensemble (the analysis cycle of the EnKF) as member-dataflow launches
+    (member e of slot d at tick G[d] + e), on classic plans and on chunk-synchronous ones
+    ("sync": one workgroup barrier per 4 ticks, 4-tick local edges between waves).  Several
     consecutive one-step runs (interpolated between forcing rows) then a multi-step run must
     equal every member's serial run."""
     depth = 1500 if n > 100_000 else 120
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(n, 4 if n < 100_000 else 300, depth,
                                                       n + E, E)
     n = end.size
-    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile, members=E)
+    sync = mode == "sync"
+    mode = "dataflow" if sync else mode
+    net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=slots, tile=tile, members=E,
+                            sync=int(sync))
+    if sync:
+        assert net.info["n_local"] > 0 or n < 3000
     net.set_mode(mode)
     net.set_coeffs(*coef)
     net.set_state(o0, i0)
@@ -165,8 +171,9 @@ def test_member_dataflow_matches_launches_path():
     end, start, indeg, coef, xp, fpe, o0, i0 = _case(2000, 3, 80, 99, E)
     x = xp[0] + 300e9 * np.arange(1, 4)
     res = []
-    for mode in ("dataflow", "launches", "paths"):
-        net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=256, members=E)
+    for mode, sync in (("dataflow", 0), ("launches", 0), ("dataflow", 1), ("launches", 1)):
+        net = engine.RoutingNet(end, indeg, start[indeg == 0], slots=256, tile=16, members=E,
+                                sync=sync)
         net.set_mode(mode)
         net.set_coeffs(*coef)
         net.set_state(o0, i0)

@@ -27,7 +27,6 @@
 #include "capi_common.hpp"
 #include "digest.hpp"
 #include "kernels.hpp"
-#include "paths.hpp"
 #include "plan.hpp"
 
 #pragma clang fp contract(off)
@@ -212,24 +211,7 @@ struct Net {
 
     // outputs of the last run are the {o, i} pairs of a member-dataflow step (IOb, member windows)
     bool out_io = false;
-    // outputs of the last run (a one-step member-paths run) are the session state itself; a call
-    // that changes the state first copies them aside (keep_outputs: out_saved, outS)
-    bool out_state = false, out_saved = false;
-    DBuf<double> outS;
 
-    // ---- member paths (paths.hip): one-step ensemble runs swept along heavy paths, members on
-    // the lanes; the path plan is built from the schedule plan on first use
-    std::unique_ptr<mcr::PathPlan> pplan;
-    int pplan_state = 0;                 // 1 built, -1 not available for this network
-    DBuf<int32_t> prec, povf, ptask, pseq, pqueue;
-    DBuf<double> Pbuf;
-    DBuf<uint32_t> GRb;
-    size_t gr_words = 0;
-    uint32_t pepoch = 0;
-    bool palpha_stale = true;            // records carry alpha: refreshed after set_coeffs
-    // the member paths are opt-in (mode 3): on the bench networks the member-dataflow launch is
-    // faster at every E measured (Texas E=32 0.70 vs 0.38 ms per step;
-    // the single-wave node chain costs ~270 ns a node against the dataflow's shared tick)
 
     // tick-major member windows of the member-dataflow step (kernels.hpp MemberWin), for E
     DBuf<int64_t> mwbase;
@@ -493,111 +475,6 @@ struct Net {
         return ok;
     }
 
-    // the step outputs of a member-paths run are the state: copy them aside before the state
-    // changes (settle_gain, set_state, apply_gain, a state hand-over into this session)
-    void keep_outputs() {
-        if (!out_state) return;
-        const size_t cells = (size_t)(plan.nslots * E);
-        outS.reserve(2 * cells);
-        HIPC(hipMemcpyAsync(outS.p, st_o.p, cells * sizeof(double), hipMemcpyDeviceToDevice,
-                            stream));
-        HIPC(hipMemcpyAsync(outS.p + cells, st_i.p, cells * sizeof(double),
-                            hipMemcpyDeviceToDevice, stream));
-        out_state = false;
-        out_saved = true;
-    }
-    // member-major [E][nslots] source of the step outputs (outflow c = 0, inflow c = 1)
-    const double* state_outputs(int c) const {
-        if (out_saved) return outS.p + (size_t)c * (size_t)(plan.nslots * E);
-        return c == 0 ? st_o.p : st_i.p;
-    }
-
-    bool paths_ready() {
-        if (pplan_state != 0) return pplan_state > 0;
-        pplan_state = -1;
-        auto pp = std::make_unique<mcr::PathPlan>();
-        if (!mcr::build_path_plan(plan, *pp).empty()) return false;
-        std::vector<int32_t> sq((size_t)std::max<int64_t>(plan.nslots, 1), -1);
-        for (int64_t q = 0; q < pp->n; ++q) sq[plan.pos[pp->seq_reach[q]]] = (int32_t)q;
-        prec.upload(pp->rec.data(), pp->rec.size(), stream);
-        povf.upload(pp->ovf.data(), pp->ovf.size(), stream);
-        ptask.upload(pp->task_off.data(), pp->task_off.size(), stream);
-        pseq.upload(sq.data(), sq.size(), stream);
-        sync();                          // (host staging vectors)
-        pplan = std::move(pp);
-        palpha_stale = true;
-        pplan_state = 1;
-        return true;
-    }
-    bool use_paths() {
-        if (E < 2 || mode != 3 || force_mode == 1) return false;
-        return plan.n > 0 && plan.n < (1ll << 30) && paths_ready();
-    }
-    // one step of all E members (T = 1) along the path plan; the pending analysis increments are
-    // applied in the prep pass; the new state is written in place and IS the step's output
-    void run_paths(const double* Fsrc, int64_t rows, int4 ent) {
-        const mcr::PathPlan& pp = *pplan;
-        const int64_t n = pp.n, groups = (E + mcr::kPathLanes - 1) / mcr::kPathLanes;
-        if (palpha_stale) {
-            HIPC(mcr::launch_path_alpha(prec.p, alpha.p, n, stream));
-            palpha_stale = false;
-        }
-        Pbuf.reserve((size_t)(groups * n * 192));
-        const size_t words = (size_t)pp.n_tasks * (size_t)groups * mcr::kPathLanes * 4;
-        REQUIRE(words * 4 < ((size_t)1 << 31), "network too large for the member paths");
-        if (words > gr_words || pepoch == 0xffffffffu) {
-            GRb.reserve(std::max<size_t>(words, 4));
-            HIPC(hipMemsetAsync(GRb.p, 0, std::max<size_t>(words, 4) * 4, stream));
-            gr_words = std::max(gr_words, words);
-            pepoch = 0;
-        }
-        ++pepoch;
-        pqueue.reserve(1);
-        HIPC(hipMemsetAsync(pqueue.p, 0, sizeof(int32_t), stream));
-        HIPC(mcr::launch_path_prep(Fsrc, rows * plan.nslots, (int)rows, ent, st_o.p, st_i.p,
-                                   beta.p, chi.p, gamma.p, flags.p, pseq.p,
-                                   gain_pending ? Gn.p : nullptr, sup_off.p, sup.p, Pbuf.p,
-                                   plan.nslots, n, E, stream));
-        gain_pending = false;
-        mcr::PathArgs a{};
-        a.rec = prec.p;
-        a.ovf = povf.p;
-        a.task_off = ptask.p;
-        a.P = Pbuf.p;
-        a.st_o = st_o.p;
-        a.st_i = st_i.p;
-        a.GR = GRb.p;
-        a.queue = pqueue.p;
-        a.status = status.p;
-        a.patience = patience;
-        a.ns = plan.nslots;
-        a.n = n;
-        a.n_tasks = pp.n_tasks;
-        a.groups = (int32_t)groups;
-        a.E = (int32_t)E;
-        a.gr_bytes = (uint32_t)(std::max<size_t>(words, 4) * 4);
-        a.epoch = pepoch;
-        if (timing) {
-            ensure_events(2);
-            HIPC(hipEventRecord(events[0], stream));
-        }
-        HIPC(mcr::launch_member_paths(a, std::max(cu_count, 1) * 2, stream));
-        mark_state();
-        if (timing) {
-            HIPC(hipEventRecord(events[1], stream));
-            HIPC(hipEventSynchronize(events[1]));
-            float ms = 0.f;
-            HIPC(hipEventElapsedTime(&ms, events[0], events[1]));
-            kernel_ms += ms;
-            run_ms += ms;
-            launches += 1;
-        }
-        ++flow_runs;                     // a wait that gave up is reported at the next sync
-        last_flow.valid = false;         // (never re-routed: the state was updated in place)
-        out_state = true;
-        last_path = 3;
-    }
-
     bool members_fit(size_t& lds) {
         if (mode == 1 || force_mode == 1) return false;
         const int S = plan.p.slots, Kc = plan.p.chain;
@@ -670,7 +547,6 @@ struct Net {
     bool gain_pending = false;
     void settle_gain() {
         if (!gain_pending) return;
-        keep_outputs();
         gain_pending = false;
         HIPC(mcr::launch_apply_gain(Gn.p, st_o.p, st_i.p, flags.p, sup_off.p, sup.p, plan.nslots,
                                     E, stream));
@@ -682,7 +558,6 @@ struct Net {
         if (plan.n == 0) return;
         settle_state();
         settle_gain();
-        keep_outputs();
         const size_t ns = (size_t)plan.nslots;
         Gn.reserve(ns * E);
         to_slots(gain, Gn, E);
@@ -946,7 +821,6 @@ struct Net {
         to_slots(b, beta);
         to_slots(c, chi);
         to_slots(g, gamma);
-        palpha_stale = true;
         // partial sums pass their fold through, unrouted reaches and padding output 0
         HIPC(mcr::launch_set_slot_coeffs(flags.p, alpha.p, beta.p, chi.p, gamma.p, plan.nslots,
                                          stream));
@@ -958,7 +832,6 @@ struct Net {
         REQUIRE(plan.n == 0 || (o && i), "state arrays must not be NULL");
         settle_state();
         gain_pending = false;            // replaced
-        keep_outputs();
         to_slots(o, st_o, E);
         to_slots(i, st_i, E, &stage2);   // its own staging (stream-ordered reuse, no sync)
         const size_t cells = (size_t)(plan.n * E);
@@ -1055,14 +928,6 @@ struct Net {
         }
         last_path = 0;
         out_io = false;
-        out_state = out_saved = false;
-        if (E > 1 && T == 1 && use_paths()) {
-            // ---- one step of all members along the path plan (paths.hip)
-            settle_state();
-            run_paths(Fsrc, rows, tabh[0]);
-            T_out = T;
-            return;
-        }
         ensure_schedule(T);
         const int64_t nl = (int64_t)cur->off.size() - 1;
         if (timing) ensure_events(2 * (size_t)nl + 2);
@@ -1338,10 +1203,7 @@ struct Net {
         for (int c = 0; c < 2; ++c) {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
-            if (out_state || out_saved)    // T = 1: the state after the step
-                HIPC(mcr::launch_gather_from_slots(state_outputs(c), outT.p, pos.p, n, plan.nslots,
-                                                   E, stream));
-            else if (out_io)               // T = 1: t0 = 0, t1 = 1
+            if (out_io)                    // T = 1: t0 = 0, t1 = 1
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, outT.p, n, E,
                                            stream));
             else {
@@ -1409,10 +1271,7 @@ struct Net {
             uint64_t* dg = c == 0 ? dgo : dgi;
             if (!dst && !dg) continue;
             double* buf = c == 0 ? aO[r].p : aI[r].p;
-            if (out_state || out_saved)
-                HIPC(mcr::launch_gather_from_slots(state_outputs(c), buf, pos.p, n, plan.nslots, E,
-                                                   stream));
-            else if (out_io)
+            if (out_io)
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, buf, n, E, stream));
             else {
                 const OutView ov = out_view();
@@ -1473,10 +1332,7 @@ struct Net {
         for (int k = 0; k < 2; ++k) {
             double* dst = k == 0 ? oo : io;
             if (!dst) continue;
-            if (out_state || out_saved)    // T = 1: [j][0][e] is the step layout
-                HIPC(mcr::launch_gather_from_slots(state_outputs(k), outT.p, pos.p, n, plan.nslots,
-                                                   E, stream));
-            else if (out_io)               // T = 1: [j][0][e] is the step layout
+            if (out_io)                    // T = 1: [j][0][e] is the step layout
                 HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, k == 1, outT.p, n, E,
                                            stream));
             else {
@@ -1641,25 +1497,6 @@ int mc_plan_export_local(const void* plan, int32_t* lx_off, int32_t* lx_src) {
             std::memcpy(lx_off, P.lx_off.data(), P.lx_off.size() * sizeof(int32_t));
         if (lx_src && !P.lx_src.empty())
             std::memcpy(lx_src, P.lx_src.data(), P.lx_src.size() * sizeof(int32_t));
-    });
-}
-
-int mc_plan_paths(const void* plan, int64_t* n_tasks, int64_t* n_ovf, int32_t* task_off,
-                  int64_t* seq_reach, int32_t* rec, int32_t* ovf) {
-    return guarded([&] {
-        REQUIRE(plan && n_tasks && n_ovf, "null argument");
-        mcr::PathPlan pp;
-        const std::string err = mcr::build_path_plan(*static_cast<const mcr::Plan*>(plan), pp);
-        if (!err.empty()) throw Fail(MC_E_TOPOLOGY, err);
-        *n_tasks = pp.n_tasks;
-        *n_ovf = (int64_t)pp.ovf.size();
-        auto cp = [](auto* dst, const auto& v) {
-            if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
-        };
-        cp(task_off, pp.task_off);
-        cp(seq_reach, pp.seq_reach);
-        cp(rec, pp.rec);
-        cp(ovf, pp.ovf);
     });
 }
 
@@ -1872,7 +1709,6 @@ int mc_net_copy_state(void* dst_net, const void* src_net) {
         S->settle_gain();
         D->settle_state();
         D->gain_pending = false;         // its state is replaced
-        D->keep_outputs();
         // order: after the source's pending work, on the destination's stream; the source waits
         // for the copy before it may overwrite its state again
         hipEvent_t ev;
@@ -1909,7 +1745,7 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         REQUIRE(D->E == 1 && S->E == 1, "lateral corrections route single-member sessions");
         REQUIRE(0 <= dst_reach && dst_reach < D->plan.n && 0 <= src_reach && src_reach < S->plan.n,
                 "reach index out of range");
-        REQUIRE(S->T_out > 0 && S->cur && !S->out_io && !S->out_state && !S->out_saved,
+        REQUIRE(S->T_out > 0 && S->cur && !S->out_io,
                 "the source session has no horizon outputs");
         REQUIRE(D->n_rows == S->T_out,
                 "the destination's forcing rows must be the source horizon's steps (one input "
@@ -2047,10 +1883,9 @@ int mc_reset_timing(void* net) {
 
 int mc_set_mode(void* net, int mode) {
     return guarded([&] {
-        REQUIRE(mode >= 0 && mode <= 3,
-                "mode must be 0 (auto), 1 (multi-launch), 2 (dataflow; one-step ensemble runs "
-                "as member-dataflow launches) or 3 (auto with one-step ensemble runs always "
-                "along the member paths)");
+        REQUIRE(mode >= 0 && mode <= 2,
+                "mode must be 0 (auto), 1 (multi-launch) or 2 (dataflow; one-step ensemble runs "
+                "as member-dataflow launches)");
         as_net(net)->mode = mode;
     });
 }

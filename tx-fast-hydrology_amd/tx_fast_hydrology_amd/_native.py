@@ -71,8 +71,6 @@ SIGNATURES = {
     "mc_plan_export_local": (_i32, [_vp, _vp, _vp]),
     "mc_plan_schedule": (_i32, [_vp, _i64, ctypes.POINTER(ctypes.c_int64),
                                 ctypes.POINTER(ctypes.c_int64), _vp, _vp]),
-    "mc_plan_paths": (_i32, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
-                             _vp, _vp, _vp, _vp]),
     "mc_plan_destroy": (_i32, [_vp]),
     "mc_ax_bu_f64": (_i32, [_i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                             _vp]),

@@ -140,21 +140,6 @@ class Plan:
                                      ptr(off), ptr(lst)))
         return off, lst[: nls.value]
 
-    def paths(self) -> dict:
-        """The member-path plan of the network (paths.hpp): tasks in ticket order, the node
-        sequence (caller reaches) and the node records (meta, slot, alpha, input codes)."""
-        L = nat.lib()
-        nt, no = ctypes.c_int64(), ctypes.c_int64()
-        nat.check(L.mc_plan_paths(self._h, ctypes.byref(nt), ctypes.byref(no), None, None, None,
-                                  None))
-        task_off = np.empty(nt.value + 1, np.int32)
-        seq = np.empty(self.n, np.int64)
-        rec = np.empty((self.n, 16), np.int32)
-        ovf = np.empty(max(no.value, 1), np.int32)
-        nat.check(L.mc_plan_paths(self._h, ctypes.byref(nt), ctypes.byref(no), ptr(task_off),
-                                  ptr(seq), ptr(rec), ptr(ovf)))
-        return dict(task_off=task_off, seq_reach=seq, rec=rec, ovf=ovf[: no.value])
-
     def close(self):
         if getattr(self, "_h", None):
             nat.lib().mc_plan_destroy(self._h)
@@ -488,10 +473,10 @@ class RoutingNet:
                                           ctypes.byref(r)))
         return dict(kernel_ms=k.value, launches=n.value, run_ms=r.value)
 
-    MODES = {"auto": 0, "launches": 1, "dataflow": 2, "paths": 3}
+    MODES = {"auto": 0, "launches": 1, "dataflow": 2}
 
     def set_mode(self, mode: str):
-        """Execution path: "auto" (default), "launches", "dataflow" or "paths" (mcroute.h
+        """Execution path: "auto" (default), "launches" or "dataflow" (mcroute.h
         mc_set_mode)."""
         nat.check(nat.lib().mc_set_mode(self._h, self.MODES[mode]))
 
@@ -501,12 +486,12 @@ class RoutingNet:
         nat.check(nat.lib().mc_set_flow_patience(self._h, int(wall_ticks)))
 
     def mode(self) -> tuple:
-        """(requested mode, path of the last run: "launches" / "dataflow" / "paths" / None)."""
+        """(requested mode, path of the last run: "launches" / "dataflow" / None)."""
         m = ctypes.c_int()
         p = ctypes.c_int()
         nat.check(nat.lib().mc_get_mode(self._h, ctypes.byref(m), ctypes.byref(p)))
         names = {v: k for k, v in self.MODES.items()}
-        return names[m.value], {1: "launches", 2: "dataflow", 3: "paths"}.get(p.value)
+        return names[m.value], {1: "launches", 2: "dataflow"}.get(p.value)
 
     def set_trace(self, enable: bool):
         nat.check(nat.lib().mc_set_trace(self._h, 1 if enable else 0))
