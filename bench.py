@@ -270,8 +270,12 @@ def build_workload(args, rank=0, world=1):
     # loads (Texas ens64 14.1 -> 13.1 ms per horizon); the dataflow workloads at a 16-tick
     # cross-cluster slack (two chunks, the minimum): Texas det 0.605 -> 0.594 ms
     tile = args.tile or (64 if E > 1 and enkf is None else 16)
+    # the deterministic horizon runs a chunk-synchronous plan (the session's default); the EnKF
+    # member steps keep the classic plan (same box: 397 vs 388 us per EnKF32 member step -- the
+    # member tick waits on its staged cells, not on the barrier)
+    sync = getattr(args, "sync", None)
     net = engine.RoutingNet(end, indeg, heads, slots=slots, tile=tile, members=E,
-                            chain=args.chain, sync=getattr(args, "sync", None))
+                            chain=args.chain, sync=sync)
     net.set_mode(getattr(args, "mode", "auto"))
     net.set_coeffs(alpha, beta, chi, gamma)
     net.set_state(o0, i0)
@@ -470,6 +474,33 @@ def cpu_baseline(args, wl, orc, E, x):
             "cores": 1, "kind": "port",
             "sample": f"{reps} x full 24 h horizon (T={args.T}) on the same {n}-reach "
                       f"network, serial C (-O3 -ffp-contract=off), {t_cpu:.1f} s"}
+
+
+def reach_order_timing(net, n, T, reps=5):
+    """Device time to produce both series of the last horizon in the reference's layout
+    (outflows and inflows, reach order, step-major [T][n]: mc_gather_outputs into device
+    buffers), HIP events on the session stream, and the bytes that must move: the outflow rows
+    read once, both series written."""
+    import torch
+    stream = torch.cuda.Stream()
+    net.set_stream(stream.cuda_stream)
+    o = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    i = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    with torch.cuda.stream(stream):
+        net.gather_outputs(0, T, o, i)                 # warm-up
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            net.gather_outputs(0, T, o, i)
+        b.record(stream)
+    b.synchronize()
+    net.set_stream(None)
+    ms = a.elapsed_time(b) / reps
+    moved = 3.0 * 8 * n * T
+    return {"ms": round(ms, 4), "bytes": moved,
+            "gbs": round(moved / (ms * 1e-3) / 1e9, 1),
+            "frac": round(moved / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+            "counts": "outflow rows read once + outflow and inflow series written (f64)"}
 
 
 def api_timing(wl, runs=2):
@@ -766,6 +797,12 @@ def main():
             nt.close()
         shards = emulated_shards(args, elapsed / args.steps * 1e3)
 
+    # ---- the reference layout on the device (det, N = 1): both [T][n] series in reach order,
+    # what _ax_bu returns every step (nutils.py:64-89), from the last horizon's outputs --------
+    reach_order = None
+    if world == 1 and E == 1 and wl.enkf is None:
+        reach_order = reach_order_timing(net, n, args.T)
+
     # ---- the drop-in API over the same horizon (det, N = 1) ---------------------------------
     api_ms = None
     if world == 1 and E == 1 and wl.enkf is None and not args.no_api and wl.n < 1_000_000:
@@ -826,6 +863,9 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu"] = value / cpu["value"]
+        if reach_order is not None:
+            line["reach_order_ms"] = reach_order["ms"]
+            line["reach_order"] = reach_order
         if api_ms is not None:
             line["api_ms_per_horizon"] = round(api_ms, 3)
             line["api_path"] = ("Muskingum.simulate over the same 24 h horizon, every step "

@@ -238,6 +238,13 @@ int mc_load_forcing_series(void* net, int64_t n_rows, const double* xp, const do
 int mc_run(void* net, int64_t T, const double* x);
 /* Copy steps [t0, t1) of the last mc_run to the host, step-major: out_o[t - t0][j]. */
 int mc_fetch_outputs(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i);
+/* Device-side form of mc_fetch_outputs: the outflows / inflows of steps [t0, t1) of the last
+ * run in the reference's layout (reach order, step-major: what _ax_bu returns at every step,
+ * nutils.py:64-89, and simulate_iter yields, muskingum.py:527-533) written into caller-owned
+ * DEVICE buffers dev_o / dev_i ([t1 - t0][n](E) float64; either may be NULL), enqueued on the
+ * session stream and returning at once (stream-ordered: a consumer on that stream, or after
+ * mc_synchronize, sees them).  Nothing crosses PCIe. */
+int mc_gather_outputs(void* net, int64_t t0, int64_t t1, double* dev_o, double* dev_i);
 /* Asynchronous form of mc_fetch_outputs for the drop-in API's fused horizons (muskingum.py
  * simulate_iter, :499-536, yields every step's fresh arrays): queues the copy of steps [t0, t1)
  * into out_o / out_i (host, [t1 - t0][n]; pinned memory makes the copy asynchronous and full

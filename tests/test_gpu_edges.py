@@ -210,16 +210,17 @@ def _edge_net():
     return start, end, indeg, start[indeg == 0], coef
 
 
-@pytest.mark.parametrize("mode,sync", [("launches", 0), ("auto", 0), ("dataflow", 0),
-                                       ("dataflow", 1), ("launches", 1)])
-def test_non_finite_ensemble_matches_reference(mode, sync):
+@pytest.mark.parametrize("mode,sync,E", [("launches", 0, 3), ("auto", 0, 3), ("dataflow", 0, 3),
+                                         ("dataflow", 1, 3), ("launches", 1, 3),
+                                         ("launches", 0, 4), ("auto", 0, 4)])
+def test_non_finite_ensemble_matches_reference(mode, sync, E):
     """The same contract for an ensemble session: member e is an independent reference run
     (SURVEY a5).  Member 0 carries the non-finite forcing and state of the single-member test,
     member 1 is finite, member 2 overflows inside reach 5's partial sums from finite inputs.
     A horizon (multi-launch) and one-step runs (member dataflow; classic and chunk-synchronous
     plans) give every cell of every member exactly as the oracle does."""
     start, end, indeg, heads, coef = _edge_net()
-    n, E = end.size, 3
+    n = end.size                 # E = 4: member 3 finite; even E runs two members per instance
     o0 = np.stack([np.linspace(1.0, 2.0, n)] * E, axis=1)
     o0[2, 0] = np.nan                                # unrouted reach: state never read
     i0 = np.stack([orc.init_inflows(start, end, np.nan_to_num(o0[:, e])) for e in range(E)], 1)

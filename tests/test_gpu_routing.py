@@ -553,3 +553,35 @@ def test_load_forcing_series_layout():
     got_o, got_i = net.fetch_outputs()
     assert np.array_equal(got_o, want_o) and np.array_equal(got_i, want_i)
     net.close()
+
+
+@pytest.mark.parametrize("sync", [1, 0])
+def test_device_gather_reference_layout(exec_mode, sync):
+    """mc_gather_outputs: both series of a Texas horizon in the reference's layout (reach order,
+    step-major) on the device -- from the dataflow horizon's slot rows (auto) or the multi-launch
+    windows (launches) -- equal the host fetch and the serial oracle bit for bit, whole and by
+    blocks."""
+    import torch
+    end = synthetic.texas(seed=0)
+    n = end.size
+    K, X, o0 = synthetic.model_arrays(n, seed=0)
+    indeg, heads, coef, _, i0 = _model(end, K, X, 300.0, o0=o0)
+    xp, fp = synthetic.forcing(n, rows=25, seed=1)
+    xp = xp.astype(float)
+    x = xp[0] + 300e9 * np.arange(1, 289)
+    want_o, want_i, _, _ = orc.simulate(np.arange(n), end, indeg, *coef, o0, i0, x, xp, fp)
+    net = _net(end, indeg, heads, coef, o0, i0, slots=192, tile=16, sync=sync)
+    net.load_forcing(xp, fp)
+    net.run(x)
+    T = x.size
+    o = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    i = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    net.gather_outputs(0, T, o, i)
+    net.synchronize()
+    assert np.array_equal(o.cpu().numpy(), want_o) and np.array_equal(i.cpu().numpy(), want_i)
+    ob = torch.empty((37, n), dtype=torch.float64, device="cuda")
+    net.gather_outputs(100, 137, ob, None)
+    net.synchronize()
+    assert np.array_equal(ob.cpu().numpy(), want_o[100:137])
+    got_o, got_i = net.fetch_outputs(5, 29)
+    assert np.array_equal(got_o, want_o[5:29]) and np.array_equal(got_i, want_i[5:29])

@@ -101,6 +101,9 @@ struct Net {
 
     // static schedule
     DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, xid, lx_off, lx_src;
+    // upstream window bases of every inflow-list entry (ujb[k] = jbase[in_list[k]], per
+    // schedule) for the reach-order gathers
+
     DBuf<int16_t> lx;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
@@ -125,6 +128,7 @@ struct Net {
         std::vector<int32_t> list;
         DBuf<int32_t> active;
         DBuf<int64_t> wbase, jbase;    // window base per workgroup, step-0 cell per reach
+        DBuf<int64_t> ujb;             // jbase of every inflow-list entry (in_list order)
         int64_t Otot = 0;              // output cells of one member
         uint64_t used = 0;
     };
@@ -206,6 +210,9 @@ struct Net {
     } last_flow;
     std::vector<int4> stab_host;     // step table last uploaded to stab
     int force_mode = -1;             // >= 0: mode override during a re-run
+    // members per instance of the ensemble sweep (members.hip): 0 = default (2), 1 = the
+    // one-member kernel (MCR_MEMBERS_MB for A/B runs)
+    int members_mb = getenv("MCR_MEMBERS_MB") ? atoi(getenv("MCR_MEMBERS_MB")) : 0;
     int64_t patience = mcr::kFlowPatience;   // dataflow waits (mc_set_flow_patience)
     int64_t reroutes = 0;            // horizons re-routed after a give-up (mc_net_reroutes)
 
@@ -322,6 +329,7 @@ struct Net {
         ext_g.upload(plan.ext_g.data(), plan.ext_g.size(), stream);
         pos.upload(plan.pos.data(), plan.pos.size(), stream);
         xid.upload(plan.xid.data(), plan.xid.size(), stream);
+
         lx.upload(plan.lx.data(), plan.lx.size(), stream);
         lx_off.upload(plan.lx_off.data(), plan.lx_off.size(), stream);
         lx_src.upload(plan.lx_src.data(), plan.lx_src.size(), stream);
@@ -874,6 +882,9 @@ struct Net {
             hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
             HIPC(mcr::launch_window_index(pos.p, G.p, flags.p, wg_gmin.p, hit->wbase.p,
                                           row_width(), plan.n, hit->jbase.p, stream));
+            hit->ujb.reserve(std::max<size_t>(plan.in_list.size(), 1));
+            HIPC(mcr::launch_take_index(hit->jbase.p, in_list.p, (int64_t)plan.in_list.size(),
+                                        hit->ujb.p, stream));
             sync();
         }
         hit->used = ++use_clock;
@@ -899,6 +910,30 @@ struct Net {
     };
     OutView out_view() const {
         return {O.p, cur->Otot, cur->jbase.p, (int64_t)row_width()};
+    }
+    // steps [t0, t1) of the last run's outflows / inflows, reach order, step-major, into device
+    // buffers (either may be NULL), on the session stream
+    void gather_block(int64_t t0, int64_t t1, double* o_dst, double* i_dst) {
+        const int64_t n = plan.n;
+        if (out_io) {                      // T = 1: t0 = 0, t1 = 1
+            if (o_dst) HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, false, o_dst, n, E,
+                                                  stream));
+            if (i_dst) HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, true, i_dst, n, E,
+                                                  stream));
+            return;
+        }
+        const OutView ov = out_view();
+        if (E == 1) {                      // both series in one pass, whole rows per step
+            HIPC(mcr::launch_gather_windows(ov.O, ov.jbase, in_off.p, cur->ujb.p, ov.stride,
+                                            o_dst, i_dst, n, t0, t1, stream));
+            return;
+        }
+        for (int c = 0; c < 2; ++c) {
+            double* dst = c == 0 ? o_dst : i_dst;
+            if (dst)
+                HIPC(mcr::launch_gather_steps(ov.O, ov.mO, ov.jbase, in_off.p, in_list.p, c == 1,
+                                              (int)ov.stride, dst, n, t0, t1, E, stream));
+        }
     }
 
     // Run T steps using forcing buffer `Fsrc` with `rows` rows and the host step table.
@@ -1079,8 +1114,14 @@ struct Net {
                 last_path = 2;
             }
             a.table_cap = (int32_t)mcr::table_entries(plan.p.slots, plan.p.tile);
-            const size_t lds = mcr::wavefront_lds_bytes(plan.p.slots, plan.p.chain, a.table_cap,
-                                                        a.ext_cap, a.tile);
+            // ensembles: two members per workgroup instance (members.hip) where it applies
+            const int mb = members_mb > 0 ? members_mb : 2;
+            const bool memb2 = E >= 2 && E % mb == 0 && mb > 1 && !dense && !plan.p.sync &&
+                               mcr::members_shape_ok(plan.p.slots, plan.p.chain, mb);
+            const size_t lds = memb2 ? mcr::members_lds_bytes(plan.p.slots, plan.p.chain,
+                                                              a.table_cap, a.ext_cap, mb)
+                                     : mcr::wavefront_lds_bytes(plan.p.slots, plan.p.chain,
+                                                                a.table_cap, a.ext_cap, a.tile);
             if (launched == 0 && trace) {
                 trace_buf.reserve(mcr::kTraceWords * (size_t)std::max<int64_t>(cur->off[nl], 1));
                 trace_wg = cur->list;
@@ -1095,8 +1136,12 @@ struct Net {
                 }
                 a.kappa0 = (int32_t)(k * plan.p.tile);
                 if (timing) HIPC(hipEventRecord(events[2 * launched], stream));
-                HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, plan.p.chain, lds, dense,
-                                           (int)E, stream));
+                if (memb2)
+                    HIPC(mcr::launch_members(a, (int)grid, plan.p.slots, plan.p.chain, lds,
+                                             (int)E, mb, stream));
+                else
+                    HIPC(mcr::launch_wavefront(a, (int)grid, plan.p.slots, plan.p.chain, lds,
+                                               dense, (int)E, stream));
                 if (timing) HIPC(hipEventRecord(events[2 * launched + 1], stream));
                 ++launched;
                 last_path = 1;
@@ -1203,14 +1248,7 @@ struct Net {
         for (int c = 0; c < 2; ++c) {
             double* dst = c == 0 ? oo : io;
             if (!dst) continue;
-            if (out_io)                    // T = 1: t0 = 0, t1 = 1
-                HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, outT.p, n, E,
-                                           stream));
-            else {
-                const OutView ov = out_view();
-                HIPC(mcr::launch_gather_steps(ov.O, ov.mO, ov.jbase, in_off.p, in_list.p, c == 1,
-                                              (int)ov.stride, outT.p, n, t0, t1, E, stream));
-            }
+            gather_block(t0, t1, c == 0 ? outT.p : nullptr, c == 1 ? outT.p : nullptr);
             HIPC(hipMemcpyAsync(dst, outT.p, n * k * E * sizeof(double), hipMemcpyDeviceToHost,
                                 stream));
             sync();
@@ -1266,20 +1304,16 @@ struct Net {
         aI[r].reserve(cells);
         aDg[r].reserve((size_t)std::max<int64_t>(2 * k, 1));
         bool any = false;
-        for (int c = 0; c < 2 && n > 0 && k > 0; ++c) {
-            double* dst = c == 0 ? oo : io;
-            uint64_t* dg = c == 0 ? dgo : dgi;
-            if (!dst && !dg) continue;
-            double* buf = c == 0 ? aO[r].p : aI[r].p;
-            if (out_io)
-                HIPC(mcr::launch_gather_io(IOb.p, member_win(), pos.p, c == 1, buf, n, E, stream));
-            else {
-                const OutView ov = out_view();
-                HIPC(mcr::launch_gather_steps(ov.O, ov.mO, ov.jbase, in_off.p, in_list.p, c == 1,
-                                              (int)ov.stride, buf, n, t0, t1, E, stream));
-            }
-            if (dg) HIPC(mcr::launch_row_digests(buf, k, n * E, aDg[r].p + c * k, stream));
+        const bool want_o = oo || dgo, want_i = io || dgi;
+        if (n > 0 && k > 0 && (want_o || want_i)) {
+            gather_block(t0, t1, want_o ? aO[r].p : nullptr, want_i ? aI[r].p : nullptr);
             any = true;
+        }
+        for (int c = 0; c < 2 && any; ++c) {
+            uint64_t* dg = c == 0 ? dgo : dgi;
+            if (dg)
+                HIPC(mcr::launch_row_digests(c == 0 ? aO[r].p : aI[r].p, k, n * E,
+                                             aDg[r].p + c * k, stream));
         }
         hipStream_t cs = stream;
         if (ring) {
@@ -1761,7 +1795,8 @@ int mc_net_lateral_correction(void* dst_net, int64_t dst_reach, const void* src_
         } guard{ev};
         HIPC(hipEventRecord(ev, S->stream));
         HIPC(hipStreamWaitEvent(D->stream, ev, 0));
-        HIPC(mcr::launch_lateral_correction(S->O.p, S->cur->jbase.p, src_reach, S->row_width(),
+        const auto ov = S->out_view();
+        HIPC(mcr::launch_lateral_correction(ov.O, ov.jbase, src_reach, (int)ov.stride,
                                             o_start, alpha, beta, gamma, D->F.p, D->plan.nslots,
                                             D->plan.pos[dst_reach], S->T_out, D->stream));
         HIPC(mcr::launch_flag_nonfinite(D->F.p, D->n_rows * D->plan.nslots, D->nf.p + 1,
@@ -1801,6 +1836,17 @@ int mc_run(void* net, int64_t T, const double* x) {
 
 int mc_fetch_outputs(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i) {
     return guarded([&] { as_net(net)->fetch(t0, t1, out_o, out_i); });
+}
+
+int mc_gather_outputs(void* net, int64_t t0, int64_t t1, double* dev_o, double* dev_i) {
+    return guarded([&] {
+        Net* N = as_net(net);
+        N->settle();
+        REQUIRE(N->T_out > 0, "no outputs: call mc_run first");
+        REQUIRE(0 <= t0 && t0 <= t1 && t1 <= N->T_out, "step range out of bounds");
+        if (N->plan.n == 0 || t1 == t0) return;
+        N->gather_block(t0, t1, dev_o, dev_i);
+    });
 }
 
 int mc_fetch_outputs_async(void* net, int64_t t0, int64_t t1, double* out_o, double* out_i,

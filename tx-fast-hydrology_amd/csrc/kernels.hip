@@ -149,6 +149,10 @@ void wavefront_det(WaveArgs a) {
 #pragma unroll
         for (int p = 0; p < K; ++p) lx_col[p] = a.lx[S[p].d];
     }
+    bool lx_any = false;                                // wave-uniform: skip the writes below
+#pragma unroll
+    for (int p = 0; p < K; ++p) lx_any = lx_any || lx_col[p] >= 0;
+    lx_any = __any(lx_any);
     if (tid < 2) xbp[RS * 2 + tid] = 0.0;               // zero slot for unused codes
     // drain every prologue load: otherwise the wait-count pass carries "pending" state into
     // the tick loop and waits for each chunk's stores at every tick
@@ -315,10 +319,12 @@ void wavefront_det(WaveArgs a) {
                     }
                 }
                 // local edges of sync plans: the consumer's input of tick k + kWaveSlack
+                if (lx_any) {
 #pragma unroll
-                for (int p = 0; p < K; ++p)
-                    if (lx_col[p] >= 0 && c + i + kWaveSlack < tile)
-                        xe[lx_col[p] * tile + c + i + kWaveSlack] = ov[p];
+                    for (int p = 0; p < K; ++p)
+                        if (lx_col[p] >= 0 && c + i + kWaveSlack < tile)
+                            xe[lx_col[p] * tile + c + i + kWaveSlack] = ov[p];
+                }
                 __syncthreads();
             }
         };
@@ -477,6 +483,41 @@ __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
         out[x] = inflow ? inflow_at(Oe, jbase, in_off, in_list, j, t0 + t, slots)
                         : (jb < 0 ? 0.0 : Oe[jb + (t0 + t) * slots]);
     }
+}
+
+// Both series of a step block in reach order from the output windows (kernels.hpp
+// launch_gather_windows): grid (reach tiles, steps), one thread per (step, reach): the outflow
+// cell and the upstream cells of its inflow fold in the windows, two coalesced row stores.  No
+// 64-bit division per element; the upstream window bases (ujb) are one load per input instead
+// of in_list -> jbase.  Steps run in order across the grid, so a window line (eight slots of
+// one tick, read at the steps of its slots' schedule offsets) is re-read from the L2 / the
+// Infinity cache rather than HBM.
+__global__ __launch_bounds__(256) void gather_windows(
+        const double* __restrict__ O, const int64_t* __restrict__ jbase,
+        const int64_t* __restrict__ in_off, const int64_t* __restrict__ ujb, int64_t stride,
+        double* __restrict__ out_o, double* __restrict__ out_i, int64_t n, int64_t t0) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const int64_t tt = blockIdx.y;
+    const int64_t toff = (t0 + tt) * stride;
+    const int64_t orow = tt * n + j;
+    if (out_o) {
+        const int64_t jb = jbase[j];
+        out_o[orow] = jb < 0 ? 0.0 : O[jb + toff];
+    }
+    if (out_i) {
+        const int64_t k0 = in_off[j], k1 = in_off[j + 1];
+        double s = 0.0;
+        for (int64_t k = k0; k < k1; ++k) s = s + O[ujb[k] + toff];
+        out_i[orow] = s;
+    }
+}
+
+__global__ void take_index(const int64_t* __restrict__ src, const int64_t* __restrict__ idx,
+                           int64_t m, int64_t* __restrict__ dst) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m;
+         k += (int64_t)gridDim.x * blockDim.x)
+        dst[k] = src[idx[k]];
 }
 
 // out[j][t][e]
@@ -653,6 +694,25 @@ hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase
     if (n <= 0 || t1 <= t0) return hipSuccess;
     hipLaunchKernelGGL(gather_steps, grid_for(n * (t1 - t0) * E, 256), 256, 0, s, O, mO, jbase,
                        in_off, in_list, inflow, slots, out, n, t0, t1, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_windows(const double* O, const int64_t* jbase, const int64_t* in_off,
+                                 const int64_t* ujb, int64_t stride, double* out_o,
+                                 double* out_i, int64_t n, int64_t t0, int64_t t1,
+                                 hipStream_t s) {
+    if (n <= 0 || t1 <= t0 || (!out_o && !out_i)) return hipSuccess;
+    const int64_t tiles = (n + 255) / 256;
+    if (tiles > 0x7fffffff || t1 - t0 > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_windows, dim3((unsigned)tiles, (unsigned)(t1 - t0)), 256, 0, s, O,
+                       jbase, in_off, ujb, stride, out_o, out_i, n, t0);
+    return hipGetLastError();
+}
+
+hipError_t launch_take_index(const int64_t* src, const int64_t* idx, int64_t m, int64_t* dst,
+                             hipStream_t s) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(take_index, grid_for(m, 256), 256, 0, s, src, idx, m, dst);
     return hipGetLastError();
 }
 

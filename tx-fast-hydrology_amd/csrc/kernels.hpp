@@ -208,6 +208,12 @@ hipError_t probe_tick_floor(int slots, int chain, int grid, int ticks, hipStream
 // members: ensemble members (grid y); member strides are in `a`.
 hipError_t launch_wavefront(const WaveArgs& a, int grid, int slots, int chain, size_t lds_bytes,
                             bool dense, int members, hipStream_t s);
+// Ensemble sweep with mb members per workgroup instance (members.hip): the multi-launch
+// protocol of launch_wavefront for classic plans, non-dense step tables and E % mb == 0.
+size_t members_lds_bytes(int slots, int chain, int table_cap, int ext_cap, int mb);
+bool members_shape_ok(int slots, int chain, int mb);
+hipError_t launch_members(const WaveArgs& a, int grid, int slots, int chain, size_t lds_bytes,
+                          int members, int mb, hipStream_t s);
 // Is (slots, chain) instantiated for the multi-launch sweep / the dataflow kernels?
 bool wavefront_shape_ok(int slots, int chain);
 bool flow_shape_ok(int slots, int chain, bool sync = false);
@@ -254,6 +260,18 @@ __device__ inline uint64_t digest_term_dev(uint64_t bits, uint64_t j) {
 // out[r] = digest of row r of rows [nrows][n] (row stride n)
 hipError_t launch_row_digests(const double* rows, int64_t nrows, int64_t n, uint64_t* out,
                               hipStream_t s);
+
+// Both series of steps [t0, t1) in reach order, step-major, from the output windows (E = 1):
+// out_o[t - t0][j] = O[jbase[j] + t stride] (0 for jbase[j] < 0: a never-processed reach,
+// nutils.py:68), out_i[t - t0][j] = ((0 + O[ujb[k0] + t stride]) + ...) over j's inflow list
+// (in_off, rank order; ujb[k] = the window base of in_list[k]).  Either output may be NULL.
+hipError_t launch_gather_windows(const double* O, const int64_t* jbase, const int64_t* in_off,
+                                 const int64_t* ujb, int64_t stride, double* out_o,
+                                 double* out_i, int64_t n, int64_t t0, int64_t t1,
+                                 hipStream_t s);
+// dst[k] = src[idx[k]]
+hipError_t launch_take_index(const int64_t* src, const int64_t* idx, int64_t m, int64_t* dst,
+                             hipStream_t s);
 
 hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbase,
                                 const int64_t* in_off, const int64_t* in_list, bool inflow,

@@ -103,6 +103,7 @@ SIGNATURES = {
     "mc_ens_pack": (_i32, [_vp, _i64, _vp]),
     "mc_ens_slice_update": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
     "mc_load_forcing_series": (_i32, [_vp, _i64, _vp, _vp]),
+    "mc_gather_outputs": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "mc_fetch_outputs_async": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp,
                                       ctypes.POINTER(ctypes.c_int64)]),
     "mc_fetch_wait": (_i32, [_vp, _i64]),

@@ -438,6 +438,18 @@ class RoutingNet:
         self._fetching[ticket.value] = (out_o, out_i, digest_o, digest_i)
         return ticket.value
 
+    def gather_outputs(self, t0, t1, dev_o=None, dev_i=None):
+        """Steps [t0, t1) of the last run's outflows / inflows in reach order, step-major, into
+        device tensors (anything with .data_ptr(), float64 [t1 - t0, n(, E)]) on the session
+        stream (mcroute.h mc_gather_outputs); nothing is copied to the host."""
+        for t in (dev_o, dev_i):
+            if t is not None and t.numel() != (t1 - t0) * self.n * self.E:
+                raise ValueError("device buffers must hold [t1 - t0, n(, E)] values")
+        nat.check(nat.lib().mc_gather_outputs(
+            self._h, int(t0), int(t1),
+            ctypes.c_void_p(dev_o.data_ptr() if dev_o is not None else 0),
+            ctypes.c_void_p(dev_i.data_ptr() if dev_i is not None else 0)))
+
     def fetch_wait(self, ticket: int):
         nat.check(nat.lib().mc_fetch_wait(self._h, int(ticket)))
         self._fetching.pop(int(ticket), None)
