@@ -135,5 +135,17 @@ __device__ __forceinline__ double fold_values(const double* v, bool chained, boo
     return I;
 }
 
+// The reference update o = 0 + (((a I + b Ip) + c Op) + g q) (nutils.py:80-83), evaluated as
+// ((a I + b Ip) + c Op) + (0 + g q).  Bit-identical for every input: a round-to-nearest sum is
+// -0.0 only when both addends are -0.0, so the leading 0 + only ever turns a -0.0 into +0.0,
+// and it does the same when applied to the last addend first (NaN and +-Inf propagate the same
+// way through either order).  gq0 = 0 + g q does not depend on the inflow I, so the
+// canonicalising add leaves the tick's dependent chain: alpha I, + b Ip, + c Op, + gq0.
+__device__ __forceinline__ double gq_term(double g, double q) { return 0.0 + g * q; }
+__device__ __forceinline__ double muskingum_update(double a, double I, double b, double ip,
+                                                   double c, double op, double gq0) {
+    return ((a * I + b * ip) + c * op) + gq0;
+}
+
 }  // namespace dev
 }  // namespace mcr

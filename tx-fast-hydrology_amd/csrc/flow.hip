@@ -322,7 +322,10 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         decode_codes<RS>(S[p], up[p], XB, 8u, XE, 8u);
-        any3[p] = __any(S[p].cnt > 2);
+        // every slot folds four inputs (codes beyond its count read the zero slot: adding +0.0
+        // to a published value is exact): no wave-uniform test and no selects of the 2- and
+        // 4-input sums (same box: det 0.467 -> 0.462 ms, EnKF32 21.9 -> 21.6 ms per horizon)
+        any3[p] = true;
         own[p] = XB + (unsigned)(p * SLOTS + lid) * 8u;
         const int l = SYNC ? (int)a.lx[S[p].d] : -1;
         lxo[p] = l >= 0;
@@ -436,8 +439,9 @@ void wavefront_flow(WaveArgs a) {
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                    const double rr = 0.0 + (((S[p].al * I + S[p].be * rIO[p][r].y) +
-                                              S[p].ch * rIO[p][r].x) + S[p].ga * rQ[p][r]);
+                    const double rr = dev::muskingum_update(S[p].al, I, S[p].be, rIO[p][r].y,
+                                                            S[p].ch, rIO[p][r].x,
+                                                            dev::gq_term(S[p].ga, rQ[p][r]));
                     const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
                     ov[p] = o;
                     Iv[p] = I;
@@ -597,8 +601,9 @@ void wavefront_flow(WaveArgs a) {
                         bool act = (unsigned)(k - S[p].G) < (unsigned)T;
                         if constexpr (PSUM) act = act && !S[p].psum;   // zero state (Slot::psum)
                         const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                        const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
-                                                  S[p].ch * S[p].op) + S[p].ga * qv[p]);
+                        const double rr = dev::muskingum_update(S[p].al, I, S[p].be, S[p].ip,
+                                                                S[p].ch, S[p].op,
+                                                                dev::gq_term(S[p].ga, qv[p]));
                         const double o = rr;   // psum / unrouted / pad: set_slot_coeffs
                         S[p].op = act ? o : S[p].op;
                         S[p].ip = act ? I : S[p].ip;
@@ -1212,7 +1217,8 @@ void tick_floor(int ticks, double* __restrict__ out) {
             for (int p = 0; p < K; ++p) {
                 double I = v[p][0] + v[p][1];
                 if (p > 0) I = I + prev;
-                const double o = 0.0 + (((al * I + be * ip[p]) + ch * op[p]) + ga * q);
+                const double o = dev::muskingum_update(al, I, be, ip[p], ch, op[p],
+                                                       dev::gq_term(ga, q));
                 op[p] = o;
                 ip[p] = I;
                 prev = o;

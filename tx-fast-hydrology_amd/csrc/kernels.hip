@@ -290,8 +290,9 @@ void wavefront_det(WaveArgs a) {
                     bool upd = act[p];
                     if constexpr (PSUM) upd = upd && !S[p].psum;   // partial sums: zero state
                     const double I = fold_values(vin[p], S[p].chained, any3[p], prev, p == 0);
-                    const double rr = 0.0 + (((S[p].al * I + S[p].be * S[p].ip) +
-                                              S[p].ch * S[p].op) + S[p].ga * qv[p]);
+                    const double rr = dev::muskingum_update(S[p].al, I, S[p].be, S[p].ip,
+                                                            S[p].ch, S[p].op,
+                                                            dev::gq_term(S[p].ga, qv[p]));
                     const double o = rr;   // psum / unrouted / pad: coefficients set_slot_coeffs
                     S[p].op = upd ? o : S[p].op;
                     S[p].ip = upd ? I : S[p].ip;
@@ -486,30 +487,49 @@ __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
 }
 
 // Both series of a step block in reach order from the output windows (kernels.hpp
-// launch_gather_windows): grid (reach tiles, steps), one thread per (step, reach): the outflow
-// cell and the upstream cells of its inflow fold in the windows, two coalesced row stores.  No
+// launch_gather_windows): grid (reach tiles, step blocks), one thread per (reach, block of
+// kGatherSteps steps): the outflow cells and the upstream cells of its inflow folds in the
+// windows, coalesced row stores.  No
 // 64-bit division per element; the upstream window bases (ujb) are one load per input instead
 // of in_list -> jbase.  Steps run in order across the grid, so a window line (eight slots of
 // one tick, read at the steps of its slots' schedule offsets) is re-read from the L2 / the
 // Infinity cache rather than HBM.
+constexpr int kGatherSteps = 8;       // steps per thread of gather_windows
 __global__ __launch_bounds__(256) void gather_windows(
         const double* __restrict__ O, const int64_t* __restrict__ jbase,
         const int64_t* __restrict__ in_off, const int64_t* __restrict__ ujb, int64_t stride,
-        double* __restrict__ out_o, double* __restrict__ out_i, int64_t n, int64_t t0) {
+        double* __restrict__ out_o, double* __restrict__ out_i, int64_t n, int64_t t0,
+        int64_t t1) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
-    const int64_t tt = blockIdx.y;
-    const int64_t toff = (t0 + tt) * stride;
-    const int64_t orow = tt * n + j;
+    // kGatherSteps consecutive steps per thread: the index loads are made once and the cell
+    // loads of the steps are independent (in flight together)
+    const int64_t tb = t0 + (int64_t)blockIdx.y * kGatherSteps;
+    const int nt = (int)(t1 - tb < kGatherSteps ? t1 - tb : kGatherSteps);
     if (out_o) {
         const int64_t jb = jbase[j];
-        out_o[orow] = jb < 0 ? 0.0 : O[jb + toff];
+        double v[kGatherSteps];
+#pragma unroll
+        for (int q = 0; q < kGatherSteps; ++q)
+            v[q] = (jb < 0 || q >= nt) ? 0.0 : O[jb + (tb + q) * stride];
+#pragma unroll
+        for (int q = 0; q < kGatherSteps; ++q)
+            if (q < nt) out_o[(tb + q - t0) * n + j] = v[q];
     }
     if (out_i) {
         const int64_t k0 = in_off[j], k1 = in_off[j + 1];
-        double s = 0.0;
-        for (int64_t k = k0; k < k1; ++k) s = s + O[ujb[k] + toff];
-        out_i[orow] = s;
+        double s[kGatherSteps];
+#pragma unroll
+        for (int q = 0; q < kGatherSteps; ++q) s[q] = 0.0;
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t ub = ujb[k];
+#pragma unroll
+            for (int q = 0; q < kGatherSteps; ++q)
+                if (q < nt) s[q] = s[q] + O[ub + (tb + q) * stride];
+        }
+#pragma unroll
+        for (int q = 0; q < kGatherSteps; ++q)
+            if (q < nt) out_i[(tb + q - t0) * n + j] = s[q];
     }
 }
 
@@ -704,8 +724,9 @@ hipError_t launch_gather_windows(const double* O, const int64_t* jbase, const in
     if (n <= 0 || t1 <= t0 || (!out_o && !out_i)) return hipSuccess;
     const int64_t tiles = (n + 255) / 256;
     if (tiles > 0x7fffffff || t1 - t0 > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gather_windows, dim3((unsigned)tiles, (unsigned)(t1 - t0)), 256, 0, s, O,
-                       jbase, in_off, ujb, stride, out_o, out_i, n, t0);
+    const int64_t blocks = (t1 - t0 + kGatherSteps - 1) / kGatherSteps;
+    hipLaunchKernelGGL(gather_windows, dim3((unsigned)tiles, (unsigned)blocks), 256, 0, s, O,
+                       jbase, in_off, ujb, stride, out_o, out_i, n, t0, t1);
     return hipGetLastError();
 }
 

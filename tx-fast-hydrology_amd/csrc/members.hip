@@ -308,8 +308,9 @@ void wavefront_members(WaveArgs a) {
                             I = I + vin[p][3].v[m];
                         }
                         if (p > 0) I = I + (S[p].chained ? prev[m] : 0.0);
-                        const double o = 0.0 + (((S[p].al * I + S[p].be * ip[p][m]) +
-                                                 S[p].ch * op[p][m]) + S[p].ga * qv[p][m]);
+                        const double o = dev::muskingum_update(
+                            S[p].al, I, S[p].be, ip[p][m], S[p].ch, op[p][m],
+                            dev::gq_term(S[p].ga, qv[p][m]));
                         op[p][m] = upd ? o : op[p][m];
                         ip[p][m] = upd ? I : ip[p][m];
                         ov[p][m] = o;
