@@ -365,7 +365,7 @@ void wavefront_flow(WaveArgs a) {
         const int64_t mwb = skew ? a.wbase[w] : 0;      // member window of this workgroup
         const int rows = wend - gminw;                  // its rows: ticks gmin .. gmax + E - 1
         const int64_t mS = a.mS;
-        constexpr int kRing = 4;
+        constexpr int kRing = 4;          // (8: EnKF32 21.45 vs 21.49 ms per horizon, not kept)
         static_assert(kChunk % kRing == 0, "ring slots must be static in the unrolled chunk");
         // tick-major windows (SKEW): the staging cell of tick k (row clamped, wave-uniform)
         auto cell = [&](int k, int p) -> int64_t {

@@ -487,14 +487,15 @@ __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
 }
 
 // Both series of a step block in reach order from the output windows (kernels.hpp
-// launch_gather_windows): grid (reach tiles, step blocks), one thread per (reach, block of
-// kGatherSteps steps): the outflow cells and the upstream cells of its inflow folds in the
-// windows, coalesced row stores.  No
+// launch_gather_windows): grid (reach tiles, steps), one thread per (reach, step): the outflow
+// cell and the upstream cells of its inflow fold in the windows, coalesced row stores.  No
 // 64-bit division per element; the upstream window bases (ujb) are one load per input instead
 // of in_list -> jbase.  Steps run in order across the grid, so a window line (eight slots of
 // one tick, read at the steps of its slots' schedule offsets) is re-read from the L2 / the
 // Infinity cache rather than HBM.
-constexpr int kGatherSteps = 8;       // steps per thread of gather_windows
+// steps per thread of gather_windows: 1 (Texas o + i horizon 1.63 ms; 8 steps per thread with
+// the index loads shared: 1.91 ms -- fewer threads in flight for the same random cell loads)
+constexpr int kGatherSteps = 1;
 __global__ __launch_bounds__(256) void gather_windows(
         const double* __restrict__ O, const int64_t* __restrict__ jbase,
         const int64_t* __restrict__ in_off, const int64_t* __restrict__ ujb, int64_t stride,
