@@ -716,6 +716,9 @@ def main():
     launch_ms = tm["kernel_ms"] / launches
     path = net.mode()[1]
     kernel = "wavefront_flow" if path == "dataflow" else "wavefront_det"
+    if path == "launches" and E >= 2 and E % 2 == 0 and not getattr(args, "sync", None) and \
+            os.environ.get("MCR_MEMBERS_MB", "2") != "1":
+        kernel = "wavefront_members"      # two members per instance (capi.cpp run: memb2)
     if wl.enkf is not None and len(nets) > 1:
         # member steps on the member-dataflow kernel, the forecast on the multi-launch kernel
         kernel = "wavefront_flow (member steps) + wavefront_det (forecast)"

@@ -251,8 +251,12 @@ void wavefront_members(WaveArgs a) {
 #pragma unroll
             for (int u = 0; u < kUpInline; ++u) m_[p][u] = S[p].ubase[u];
 
-        auto run_chunk = [&](auto mtag, auto ptag) {
+        // ALL: every live slot of this wave runs a step at every tick of the chunk (wave-
+        // uniform; most chunks of an ensemble horizon): no per-tick activity tests and no state
+        // selects -- the output stores keep the slot's liveness in this launch as their mask
+        auto run_chunk = [&](auto mtag, auto ptag, auto atag) {
             constexpr bool MASKQ = decltype(mtag)::value, PSUM = decltype(ptag)::value;
+            constexpr bool ALL = decltype(atag)::value;
 #pragma unroll
             for (int i = 0; i < kChunk; ++i) {
                 const int k = kc + i;
@@ -295,7 +299,7 @@ void wavefront_members(WaveArgs a) {
                 for (int m = 0; m < MB; ++m) prev[m] = 0.0;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    act[p] = (unsigned)(k - S[p].G) < (unsigned)T;
+                    act[p] = ALL ? S[p].G != (1 << 29) : (unsigned)(k - S[p].G) < (unsigned)T;
                     bool upd = act[p];
                     if constexpr (PSUM) upd = upd && !S[p].psum;
 #pragma unroll
@@ -311,8 +315,13 @@ void wavefront_members(WaveArgs a) {
                         const double o = dev::muskingum_update(
                             S[p].al, I, S[p].be, ip[p][m], S[p].ch, op[p][m],
                             dev::gq_term(S[p].ga, qv[p][m]));
-                        op[p][m] = upd ? o : op[p][m];
-                        ip[p][m] = upd ? I : ip[p][m];
+                        if constexpr (ALL && !PSUM) {
+                            op[p][m] = o;        // (a slot that is not live is not written back)
+                            ip[p][m] = I;
+                        } else {
+                            op[p][m] = upd ? o : op[p][m];
+                            ip[p][m] = upd ? I : ip[p][m];
+                        }
                         ov[p][m] = o;
                         prev[m] = o;
                     }
@@ -354,13 +363,20 @@ void wavefront_members(WaveArgs a) {
         };
         using yes = std::true_type;
         using no = std::false_type;
+        bool all = true;
+#pragma unroll
+        for (int p = 0; p < K; ++p)
+            all = all && (S[p].G == (1 << 29) ||
+                          (unsigned)(kc - S[p].G) <= (unsigned)(T - kChunk));
+        all = T >= kChunk && __all(all);
         if (__builtin_expect(!maskq && !anyps, 1)) [[likely]] {
-            run_chunk(no{}, no{});
+            if (all) run_chunk(no{}, no{}, yes{});
+            else run_chunk(no{}, no{}, no{});
         } else if (maskq) {
-            if (anyps) run_chunk(yes{}, yes{});
-            else run_chunk(yes{}, no{});
+            if (anyps) run_chunk(yes{}, yes{}, no{});
+            else run_chunk(yes{}, no{}, no{});
         } else {
-            run_chunk(no{}, yes{});
+            run_chunk(no{}, yes{}, no{});
         }
 #pragma unroll
         for (int p = 0; p < K; ++p) {
