@@ -705,34 +705,44 @@ def main():
         nt.set_timing(True)
     for _ in range(args.timing_runs):
         horizon()
-    tm = {"kernel_ms": 0.0, "launches": 0}
+    per_net = []
     for nt in nets:
         nt.synchronize()
-        t_ = nt.timing()
-        tm["kernel_ms"] += t_["kernel_ms"]
-        tm["launches"] += t_["launches"]
+        per_net.append(nt.timing())
         nt.set_timing(False)
+    T_k = args.T                       # timesteps the roofline kernel routes per horizon
+    tm = per_net[-1] if len(nets) > 1 else per_net[0]
+    members_steps = None
+    if len(nets) > 1:
+        # EnKF: the dominant kernel is the forecast (fnet, T - n_an of the T steps, most of the
+        # device time); the member steps between analyses are reported beside it
+        T_k = args.T - wl.enkf.n_an
+        ms_ = per_net[0]
+        members_steps = {"kernel": "wavefront_flow (member dataflow, one step per launch)",
+                         "launches_per_step": ms_["launches"] / args.timing_runs,
+                         "kernel_ms_per_step": round(ms_["kernel_ms"] / args.timing_runs, 4)}
     launches = max(tm["launches"], 1)
     launch_ms = tm["kernel_ms"] / launches
-    path = net.mode()[1]
+    path = (nets[-1] if len(nets) > 1 else net).mode()[1]
     kernel = "wavefront_flow" if path == "dataflow" else "wavefront_det"
-    if path == "launches" and E >= 2 and E % 2 == 0 and not getattr(args, "sync", None) and \
+    if path == "launches" and E >= 2 and E % 2 == 0 and \
+            (len(nets) > 1 or not getattr(args, "sync", None)) and \
             os.environ.get("MCR_MEMBERS_MB", "2") != "1":
         kernel = "wavefront_members"      # two members per instance (capi.cpp run: memb2)
-    if wl.enkf is not None and len(nets) > 1:
-        # member steps on the member-dataflow kernel, the forecast on the multi-launch kernel
-        kernel = "wavefront_flow (member steps) + wavefront_det (forecast)"
     # 72 B per reach·timestep deterministic, 40 + 32/E per reach·member·timestep
     per_unit = BYTES_PER_UNIT if E == 1 else 40.0 + 32.0 / E
-    bytes_per_launch = per_unit * n * E * args.T * args.timing_runs / launches
+    bytes_per_launch = per_unit * n * E * T_k * args.timing_runs / launches
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
     launches_per_step = tm["launches"] / args.timing_runs
-    comp = compulsory_bytes(n, E, args.T, wl.rows) / launches_per_step
+    comp = compulsory_bytes(n, E, T_k, wl.rows) / launches_per_step
     roofline = {"bound": "latency", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
                 "algorithmic_bytes_per_unit": per_unit, "kernel": kernel,
                 "launches_per_step": launches_per_step, "avg_launch_us": round(launch_ms * 1e3, 3),
                 "kernel_ms_per_step": round(tm["kernel_ms"] / args.timing_runs, 4)}
+    if members_steps is not None:
+        roofline["timesteps_per_step"] = T_k
+        roofline["member_steps"] = members_steps
     # the routing recurrence keeps coefficients and state in registers / LDS: it is bound by its
     # dependency chain (schedule ticks x per-tick latency), not by DRAM bandwidth
     if wl.enkf is None and E == 1 and path == "dataflow" and \
@@ -748,11 +758,11 @@ def main():
                      "chained updates, LDS outputs, barrier; %s per CU, no memory traffic), "
                      "measured now on this device"
                      % ("2 workgroups" if info["slots"] == 192 else "1 workgroup")}
-    elif wl.enkf is None and E > 1:
+    elif E > 1:
         # an ensemble horizon is throughput-bound: its critical path (the schedule's ticks at the
         # bare tick latency) is a small fraction of it, and the bound it is measured against is
         # the HBM roofline of the bytes it must move (compulsory, below)
-        ticks = info["gmax"] + args.T
+        ticks = nets[-1].info["gmax"] + T_k
         ns_tick = engine.probe_tick_floor(192, 2, 8192)
         floor_ms = ticks * ns_tick * 1e-6
         roofline["bound"] = "hbm"

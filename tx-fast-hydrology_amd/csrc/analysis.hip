@@ -165,6 +165,31 @@ __global__ void mean_anomalies(const double* __restrict__ X, double* __restrict_
     }
 }
 
+// The same for few rows of many members (the gauge anomalies HA of the ensemble-space weights:
+// 500 rows x 256 members): a wave per row loads all of the row's members at once into LDS and
+// every lane folds them in member order from there, so the sum is mean_anomalies' left fold
+// and the loads are not serialised behind it (a thread per row walked 256 dependent adds with
+// its loads 8 at a time: 28 us per EnKF256 analysis)
+constexpr int kRowMaxE = 1024;
+__global__ __launch_bounds__(256) void mean_anomalies_rows(const double* __restrict__ X,
+                                                           double* __restrict__ A, int64_t ns,
+                                                           int64_t E) {
+    __shared__ double buf[4][kRowMaxE];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t d = (int64_t)blockIdx.x * 4 + wv;
+    if (d >= ns) return;                                   // wave-uniform
+    double* b = buf[wv];
+    for (int64_t e = lane; e < E; e += 64) b[e] = X[e * ns + d];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double s = 0.0;
+#pragma unroll 8
+    for (int64_t e = 0; e < E; ++e) s += b[e];
+    const double xbar = s / (double)E;
+    for (int64_t e = lane; e < E; e += 64) A[e * ns + d] = b[e] - xbar;
+}
+
 // Increments of a reach slice in one pass, for ensembles of at most MAXE members (the per-GPU
 // shares of the sharded EnKF): per slot d the member mean (mean_anomalies' order), the
 // anomalies A[e] = X[e][d] - mean in registers, and G[e][d] = sum_f A[f] Z[f][e] with Z (Et x Et,
@@ -407,7 +432,11 @@ hipError_t launch_scale_rows(const double* HA, const double* r, double* U, int64
 
 hipError_t launch_mean_anomalies(const double* X, double* A, int64_t ns, int64_t E,
                                  hipStream_t s) {
-    hipLaunchKernelGGL(mean_anomalies, grid_for(ns, 256), 256, 0, s, X, A, ns, E);
+    if (ns <= 8192 && E >= 32 && E <= kRowMaxE)
+        hipLaunchKernelGGL(mean_anomalies_rows, dim3((unsigned)((ns + 3) / 4)), 256, 0, s, X, A,
+                           ns, E);
+    else
+        hipLaunchKernelGGL(mean_anomalies, grid_for(ns, 256), 256, 0, s, X, A, ns, E);
     return hipGetLastError();
 }
 

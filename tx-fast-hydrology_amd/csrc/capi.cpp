@@ -150,7 +150,7 @@ struct Net {
     int64_t E = 1;
 
     // ensemble analysis (analysis.hip): anomalies, gauge operators, dense products, solver
-    DBuf<double> An, HA, Zn, Gn, Yb, HXb, Db, Rd, Rb, Ub, EE, Wk;   // Wk: split-K slices
+    DBuf<double> An, HA, Zn, Gn, GIn, Yb, HXb, Db, Rd, Rb, Ub, EE, Wk;   // Wk: split-K slices
     // SPD solves (dense.hip block LDL^T): padded matrix, unit block factor and its transpose,
     // inverted diagonal blocks, solve scratch, padded right-hand sides
     DBuf<double> Pf, Sd, Rhs;
@@ -1031,7 +1031,10 @@ struct Net {
                 double* IOp = IOb.p;
                 const mcr::MemberWin mw = member_win();
                 mcr::PendingGain pg;
-                if (gain_pending) pg = mcr::PendingGain{Gn.p, sup_off.p, sup.p};
+                if (gain_pending) {
+                    GIn.reserve((size_t)(plan.nslots * E));
+                    pg = mcr::PendingGain{Gn.p, sup_off.p, sup.p, GIn.p};
+                }
                 HIPC(mcr::launch_member_inputs(Fsrc, a.mF, plan.nslots, (int)rows, tabh[0], st_o.p,
                                                st_i.p, IOp, Qm.p, E, mw, stream, pg));
                 gain_pending = false;

@@ -806,6 +806,37 @@ __global__ __launch_bounds__(256) void member_inputs(
     }
 }
 
+// The one-hop inflow increments of a pending gain, GI[e][d] = the left fold from 0 of
+// (0 + G[e][u]) over the routed upstream slots u of d in rank order -- exactly the sum
+// apply_gain adds to the inflow state (analysis.hip).  Thread per slot, kGiRun members per
+// thread: the upstream list is read once, and a wave's upstream reads stay within a few lines
+// of each member row (upstream slots sit mostly one lane position away in the plan's order).
+constexpr int kGiRun = 8;
+__global__ __launch_bounds__(256) void inflow_increments(
+        const double* __restrict__ G, const int32_t* __restrict__ up_off,
+        const int32_t* __restrict__ up, double* __restrict__ GI, int64_t ns, int64_t E) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= ns) return;
+    const int64_t e0 = (int64_t)blockIdx.y * kGiRun;
+    const int ne = (int)(E - e0 < kGiRun ? E - e0 : kGiRun);
+    const int32_t u0 = up_off[d], u1 = up_off[d + 1];
+    int32_t upr[kUpInline];
+#pragma unroll
+    for (int k = 0; k < kUpInline; ++k) upr[k] = u0 + k < u1 ? up[u0 + k] : (int32_t)d;
+#pragma unroll 2
+    for (int k = 0; k < ne; ++k) {
+        const double* Ge = G + (e0 + k) * ns;
+        double gu[kUpInline];
+#pragma unroll
+        for (int q = 0; q < kUpInline; ++q) gu[q] = Ge[upr[q]];      // unconditional (dummy d)
+        double ig = 0.0;
+#pragma unroll
+        for (int q = 0; q < kUpInline; ++q) ig = u0 + q < u1 ? ig + (0.0 + gu[q]) : ig;
+        for (int32_t q = u0 + kUpInline; q < u1; ++q) ig = ig + (0.0 + Ge[up[q]]);
+        GI[(e0 + k) * ns + d] = ig;
+    }
+}
+
 // Member staging of the skewed windows through LDS (E >= kSkewMembers): one wave per group of
 // kStageSlots consecutive slots (one 256-B IO segment of a window row).  The per-lane form above
 // writes cell (d, e) at row G[d] + e, so a wave's store touches a different window line in
@@ -854,12 +885,14 @@ __global__ __launch_bounds__(256) void member_inputs_ring(
     const int64_t rlo = (int64_t)clamp_row(ent.x, n_rows) * ns + d;
     const int64_t rhi = (int64_t)clamp_row(ent.y < 0 ? ent.x : ent.y, n_rows) * ns + d;
     const bool gained = GAIN && (fl == kSlotRouted || fl == kSlotUnrouted);
-    const int32_t u0 = GAIN ? gain.up_off[d] : 0, u1 = GAIN ? gain.up_off[d + 1] : 0;
+    const bool pre = GAIN && gain.gi != nullptr;           // one-hop fold formed beforehand
+    const int32_t u0 = GAIN && !pre ? gain.up_off[d] : 0;
+    const int32_t u1 = GAIN && !pre ? gain.up_off[d + 1] : 0;
     // the first kUpInline upstream slots in registers: their increments are loaded together
     // (independent loads) and folded in rank order; longer lists continue in a loop
     int32_t upr[kUpInline];
 #pragma unroll
-    for (int k = 0; k < kUpInline; ++k) upr[k] = GAIN && u0 + k < u1 ? gain.up[u0 + k] : (int32_t)d;
+    for (int k = 0; k < kUpInline; ++k) upr[k] = u0 + k < u1 ? gain.up[u0 + k] : (int32_t)d;
     auto value = [&](int64_t e, double& o, double& i, double& q) {
         const int64_t idx = e * ns + d;
         const double* Fe = F + e * mF;
@@ -869,14 +902,18 @@ __global__ __launch_bounds__(256) void member_inputs_ring(
         i = st_i[idx];
         if (gained) {
             const double* Ge = gain.G + e * ns;
-            double gu[kUpInline];
-#pragma unroll
-            for (int k = 0; k < kUpInline; ++k) gu[k] = Ge[upr[k]];   // unconditional (dummy d)
             const double og = fl == kSlotRouted ? 0.0 + Ge[d] : 0.0;
             double ig = 0.0;
+            if (pre) {
+                ig = gain.gi[idx];
+            } else {
+                double gu[kUpInline];
 #pragma unroll
-            for (int k = 0; k < kUpInline; ++k) ig = u0 + k < u1 ? ig + (0.0 + gu[k]) : ig;
-            for (int32_t u = u0 + kUpInline; u < u1; ++u) ig = ig + (0.0 + Ge[gain.up[u]]);
+                for (int k = 0; k < kUpInline; ++k) gu[k] = Ge[upr[k]];   // unconditional (dummy d)
+#pragma unroll
+                for (int k = 0; k < kUpInline; ++k) ig = u0 + k < u1 ? ig + (0.0 + gu[k]) : ig;
+                for (int32_t u = u0 + kUpInline; u < u1; ++u) ig = ig + (0.0 + Ge[gain.up[u]]);
+            }
             o = o + og;
             i = i + ig;
         }
@@ -1142,14 +1179,29 @@ hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_r
                                 const PendingGain& gain) {
     if (ns * E == 0) return hipSuccess;
     if ((E + kMemberRun - 1) / kMemberRun > 65535) return hipErrorInvalidValue;
-    if (mw.skew && MCR_STAGE_RING && mw.rs % kStageSlots == 0 && ns % kStageSlots == 0) {
+    const bool ring = mw.skew && MCR_STAGE_RING && mw.rs % kStageSlots == 0 &&
+                      ns % kStageSlots == 0;
+    // the one-hop fold formed first for the LDS-ring staging (EnKF256 115.2 -> 112.8 ms per
+    // horizon, same box); the per-lane runs of small ensembles gather it in place (EnKF32 21.7
+    // vs 22.5 ms with the extra pass)
+    PendingGain g = gain;
+    if (!ring) g.gi = nullptr;
+    if (g.G && g.gi) {
+        if ((E + kGiRun - 1) / kGiRun > 65535) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(inflow_increments,
+                           dim3((unsigned)((ns + 255) / 256), (unsigned)((E + kGiRun - 1) / kGiRun)),
+                           256, 0, s, g.G, g.up_off, g.up, g.gi, ns, E);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (ring) {
         const dim3 grid((unsigned)((ns / kStageSlots + 3) / 4));
         if (gain.G)
             hipLaunchKernelGGL((member_inputs_ring<true>), grid, 256, 0, s, F, mF, ns, n_rows,
-                               ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+                               ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, g);
         else
             hipLaunchKernelGGL((member_inputs_ring<false>), grid, 256, 0, s, F, mF, ns, n_rows,
-                               ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+                               ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm, E, mw, g);
         return hipGetLastError();
     }
     constexpr int kGainRun = 4;
@@ -1159,11 +1211,11 @@ hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t ns, int n_r
                            dim3((unsigned)((ns + 255) / 256),
                                 (unsigned)((E + kGainRun - 1) / kGainRun)),
                            256, 0, s, F, mF, ns, n_rows, ent, st_o, st_i,
-                           reinterpret_cast<double2*>(IO), Qm, E, mw, gain);
+                           reinterpret_cast<double2*>(IO), Qm, E, mw, g);
     } else {
         hipLaunchKernelGGL((member_inputs<false, kMemberRun>), member_grid(ns, E), 256, 0, s, F,
                            mF, ns, n_rows, ent, st_o, st_i, reinterpret_cast<double2*>(IO), Qm,
-                           E, mw, gain);
+                           E, mw, g);
     }
     return hipGetLastError();
 }

@@ -185,6 +185,11 @@ struct PendingGain {
     const double* G = nullptr;       // [E][nslots] increments (NULL: none)
     const int32_t* up_off = nullptr; // routed upstream slots of each slot, rank order (CSR)
     const int32_t* up = nullptr;
+    // scratch [E][nslots] (may be NULL; used by the LDS-ring staging): the one-hop inflow
+    // increments of every (slot, member)
+    // are formed into it first by a slot-parallel pass (coalesced upstream reads), so the
+    // staging kernel reads one value per cell instead of gathering the upstream increments
+    double* gi = nullptr;
 };
 hipError_t launch_member_inputs(const double* F, int64_t mF, int64_t nslots, int n_rows,
                                 int4 ent, const double* st_o, const double* st_i, double* IO,

@@ -35,15 +35,18 @@ struct PlanParams {
 };
 
 // Chunk-synchronous plans (sync = 1, the dataflow kernel's default for one member): the kernel
-// joins its waves with ONE workgroup barrier per chunk of kChunk ticks instead of one per tick.
-// A unit-slack edge (value of tick k read at tick k + 1) must then stay inside one wave (LDS
-// accesses of one wave are processed in order), so the clustering is two-level:
+// joins its waves with ONE workgroup barrier per kWaveSlack ticks (two per chunk of kChunk)
+// instead of one per tick.  A unit-slack edge (value of tick k read at tick k + 1) must then stay
+// inside one wave (LDS accesses of one wave are processed in order), so the clustering is
+// two-level:
 //   * a WAVE CLUSTER is a connected sub-tree that fits one wave's lanes; inside it
 //     G[u] = G[down] - 1 (or a chained edge);
 //   * a GROUP is a connected tree of wave clusters placed in one workgroup; an edge between two
-//     of its wave clusters has slack exactly kWaveSlack = kChunk: the producer writes its tick-k
-//     output straight into the consumer's external-input column for tick k + kChunk (the next
-//     chunk's ring slot, kernels read it after the chunk barrier) -- a "local" external input;
+//     of its wave clusters has slack exactly kWaveSlack: the producer writes its tick-k output
+//     straight into the consumer's external-input column for tick k + kWaveSlack (this chunk's
+//     or the next chunk's ring slot; the consumer reads it after the next barrier) -- a "local"
+//     external input.  (Slack 8 with one barrier per chunk: a 1212-tick Texas schedule against
+//     1168 at slack 4 and 1141 for the classic plan.)
 //   * edges between groups are cross-workgroup (slack >= tile, granules), as before.
 constexpr int kWaveSlack = 4;
 constexpr int kWaveLanes = 64;
