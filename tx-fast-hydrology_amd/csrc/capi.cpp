@@ -101,9 +101,7 @@ struct Net {
 
     // static schedule
     DBuf<int32_t> G, sup_off, sup, ext_off, ext_g, wg_gmin, wg_gmax, xid, lx_off, lx_src;
-    // upstream window bases of every inflow-list entry (ujb[k] = jbase[in_list[k]], per
-    // schedule) for the reach-order gathers
-
+    DBuf<int32_t> pos32, in_off32, upos32;   // reach -> slot, inflow lists in slot space
     DBuf<int16_t> lx;
     DBuf<uint8_t> flags, up_cnt;
     DBuf<uint64_t> up4;
@@ -120,6 +118,7 @@ struct Net {
     // outputs in workgroup windows (kernels.hpp), their per-horizon index (window base of each
     // workgroup, step-0 index of each reach and of each external input) and a scratch for fetches
     DBuf<double> O, outT;
+    DBuf<double> gsc;                  // reach-order gathers: steps of a pass in slot order
     DBuf<int64_t> in_off, in_list;   // inflow lists (plan.hpp), caller order
     // per-horizon schedules (active workgroups per launch, output windows), cached per T
     struct Sched {
@@ -128,7 +127,7 @@ struct Net {
         std::vector<int32_t> list;
         DBuf<int32_t> active;
         DBuf<int64_t> wbase, jbase;    // window base per workgroup, step-0 cell per reach
-        DBuf<int64_t> ujb;             // jbase of every inflow-list entry (in_list order)
+        DBuf<int64_t> sjb;             // window index of step 0 of every node slot
         int64_t Otot = 0;              // output cells of one member
         uint64_t used = 0;
     };
@@ -337,6 +336,18 @@ struct Net {
         in_off.upload(plan.in_off.data(), plan.in_off.size(), stream);
         in_list.upload(plan.in_list.data(), plan.in_list.size(), stream);
         in_list.reserve(1);
+        {   // int32 copies for the reach-order permutation (kernels.hip permute_steps)
+            std::vector<int32_t> rp(plan.n), ro(plan.n + 1), ru(plan.in_list.size());
+            for (int64_t j = 0; j < plan.n; ++j) rp[j] = (int32_t)plan.pos[j];
+            for (int64_t j = 0; j <= plan.n; ++j) ro[j] = (int32_t)plan.in_off[j];
+            for (size_t k = 0; k < plan.in_list.size(); ++k)
+                ru[k] = (int32_t)plan.pos[plan.in_list[k]];
+            pos32.upload(rp.data(), rp.size(), stream);
+            pos32.reserve(1);
+            in_off32.upload(ro.data(), ro.size(), stream);
+            upos32.upload(ru.data(), ru.size(), stream);
+            upos32.reserve(1);
+        }
         {   // inflow lists in slot space (int32) for the gain scatter
             REQUIRE(ns < ((size_t)1 << 31), "network too large (node slots must fit int32)");
             std::vector<int32_t> so(ns + 1, 0), sl;
@@ -882,9 +893,9 @@ struct Net {
             hit->jbase.reserve((size_t)std::max<int64_t>(plan.n, 1));
             HIPC(mcr::launch_window_index(pos.p, G.p, flags.p, wg_gmin.p, hit->wbase.p,
                                           row_width(), plan.n, hit->jbase.p, stream));
-            hit->ujb.reserve(std::max<size_t>(plan.in_list.size(), 1));
-            HIPC(mcr::launch_take_index(hit->jbase.p, in_list.p, (int64_t)plan.in_list.size(),
-                                        hit->ujb.p, stream));
+            hit->sjb.reserve((size_t)std::max<int64_t>(plan.nslots, 1));
+            HIPC(mcr::launch_slot_window_index(G.p, flags.p, wg_gmin.p, hit->wbase.p, row_width(),
+                                               plan.nslots, hit->sjb.p, stream));
             sync();
         }
         hit->used = ++use_clock;
@@ -923,9 +934,14 @@ struct Net {
             return;
         }
         const OutView ov = out_view();
-        if (E == 1) {                      // both series in one pass, whole rows per step
-            HIPC(mcr::launch_gather_windows(ov.O, ov.jbase, in_off.p, cur->ujb.p, ov.stride,
-                                            o_dst, i_dst, n, t0, t1, stream));
+        if (E == 1) {                      // both series, slot order first (kernels.hip)
+            // scratch of at most 512 MB (the whole Texas horizon; CONUS in passes of ~24 steps)
+            const int64_t steps = std::max<int64_t>(
+                1, std::min<int64_t>(t1 - t0, (512ll << 20) / (8 * std::max<int64_t>(plan.nslots, 1))));
+            gsc.reserve((size_t)std::max<int64_t>(steps * plan.nslots, 1));
+            HIPC(mcr::launch_gather_slots(ov.O, cur->sjb.p, ov.stride, pos32.p, in_off32.p,
+                                          upos32.p, o_dst, i_dst, n, plan.nslots, t0, t1,
+                                          gsc.p, steps, stream));
             return;
         }
         for (int c = 0; c < 2; ++c) {

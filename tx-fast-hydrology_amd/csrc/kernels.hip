@@ -486,59 +486,102 @@ __global__ void gather_steps(const double* __restrict__ O, int64_t mO,
     }
 }
 
-// Both series of a step block in reach order from the output windows (kernels.hpp
-// launch_gather_windows): grid (reach tiles, steps), one thread per (reach, step): the outflow
-// cell and the upstream cells of its inflow fold in the windows, coalesced row stores.  No
-// 64-bit division per element; the upstream window bases (ujb) are one load per input instead
-// of in_list -> jbase.  Steps run in order across the grid, so a window line (eight slots of
-// one tick, read at the steps of its slots' schedule offsets) is re-read from the L2 / the
-// Infinity cache rather than HBM.
-// steps per thread of gather_windows: 1 (Texas o + i horizon 1.63 ms; 8 steps per thread with
-// the index loads shared: 1.91 ms -- fewer threads in flight for the same random cell loads)
-constexpr int kGatherSteps = 1;
-__global__ __launch_bounds__(256) void gather_windows(
-        const double* __restrict__ O, const int64_t* __restrict__ jbase,
-        const int64_t* __restrict__ in_off, const int64_t* __restrict__ ujb, int64_t stride,
-        double* __restrict__ out_o, double* __restrict__ out_i, int64_t n, int64_t t0,
-        int64_t t1) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    // kGatherSteps consecutive steps per thread: the index loads are made once and the cell
-    // loads of the steps are independent (in flight together)
-    const int64_t tb = t0 + (int64_t)blockIdx.y * kGatherSteps;
-    const int nt = (int)(t1 - tb < kGatherSteps ? t1 - tb : kGatherSteps);
+// Both series of a step block in reach order from the output windows (E = 1), in two passes
+// (kernels.hpp launch_gather_slots).  Reading the windows in reach order loads one random
+// 8-byte cell per (reach, step) from all over the windows (0.6 GB for Texas, more than the
+// Infinity cache): 1.63 ms per Texas horizon for o + i, ~0.8 TB/s.  Here
+//   1. unskew_windows: thread per slot, kUnskewSteps steps each -> S[t][slot] (slot order).  A
+//      wave's 64 slots read their window column pieces (slots of equal schedule offset share
+//      lines, a line is re-read at the neighbouring slots' steps from L2) and store whole rows;
+//   2. permute_steps: S[t] -> reach order, out_o[t][j] = S[t][pos[j]] and the inflow fold
+//      ((0 + S[t][pos[u1]]) + ...) over j's rank-ordered inflow list.  The random reads stay in
+//      one step's row (nslots doubles, 1.6 MB for Texas): workgroup b runs on XCD b % 8
+//      (round-robin dispatch), so XCD x takes the steps t0 + x, t0 + x + 8, ... one after the
+//      other and each row is read from HBM once, into that XCD's L2.
+// Same values as reading the windows directly (pass 1 copies the cells; never-processed and
+// padding slots read 0).
+constexpr int kUnskewSteps = 16;
+__global__ __launch_bounds__(256) void unskew_windows(const double* __restrict__ O,
+                                                      const int64_t* __restrict__ sjb,
+                                                      int64_t stride, double* __restrict__ S,
+                                                      int64_t ns, int64_t t0, int64_t t1) {
+    const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (d >= ns) return;
+    const int64_t tb = t0 + (int64_t)blockIdx.y * kUnskewSteps;
+    const int nt = (int)(t1 - tb < kUnskewSteps ? t1 - tb : kUnskewSteps);
+    const int64_t jb = sjb[d];
+    double v[kUnskewSteps];
+#pragma unroll
+    for (int q = 0; q < kUnskewSteps; ++q)
+        v[q] = (jb < 0 || q >= nt) ? 0.0 : O[jb + (tb + q) * stride];
+#pragma unroll
+    for (int q = 0; q < kUnskewSteps; ++q)
+        if (q < nt) S[(tb + q - t0) * ns + d] = v[q];
+}
+
+// kPermuteSteps steps per thread (t, t + 8, ...: all on the thread's XCD), so the index loads
+// are shared: 2 measured 1.04 ms for both Texas series, 1 1.07, 4 1.27; non-temporal index loads
+// and series stores 1.26-1.42 (same box)
+constexpr int kPermuteSteps = 2;
+__global__ __launch_bounds__(256) void permute_steps(
+        const double* __restrict__ S, const int32_t* __restrict__ pos,
+        const int32_t* __restrict__ in_off, const int32_t* __restrict__ upos,
+        double* __restrict__ out_o, double* __restrict__ out_i, int64_t n, int64_t ns,
+        int64_t t0, int64_t t1, int ntile) {
+    constexpr int P = kPermuteSteps;
+    const int x = (int)(blockIdx.x & 7);
+    const int64_t q = blockIdx.x >> 3;
+    const int64_t tb = t0 + (q / ntile) * 8 * P + x;     // steps tb, tb + 8, ... (P of them)
+    const int64_t j = (q % ntile) * 256 + threadIdx.x;
+    if (tb >= t1 || j >= n) return;
     if (out_o) {
-        const int64_t jb = jbase[j];
-        double v[kGatherSteps];
+        const int64_t d = pos[j];
+        double v[P];
 #pragma unroll
-        for (int q = 0; q < kGatherSteps; ++q)
-            v[q] = (jb < 0 || q >= nt) ? 0.0 : O[jb + (tb + q) * stride];
-#pragma unroll
-        for (int q = 0; q < kGatherSteps; ++q)
-            if (q < nt) out_o[(tb + q - t0) * n + j] = v[q];
-    }
-    if (out_i) {
-        const int64_t k0 = in_off[j], k1 = in_off[j + 1];
-        double s[kGatherSteps];
-#pragma unroll
-        for (int q = 0; q < kGatherSteps; ++q) s[q] = 0.0;
-        for (int64_t k = k0; k < k1; ++k) {
-            const int64_t ub = ujb[k];
-#pragma unroll
-            for (int q = 0; q < kGatherSteps; ++q)
-                if (q < nt) s[q] = s[q] + O[ub + (tb + q) * stride];
+        for (int h = 0; h < P; ++h) {
+            const int64_t t = tb + 8 * h;
+            v[h] = t < t1 ? S[(t - t0) * ns + d] : 0.0;
         }
 #pragma unroll
-        for (int q = 0; q < kGatherSteps; ++q)
-            if (q < nt) out_i[(tb + q - t0) * n + j] = s[q];
+        for (int h = 0; h < P; ++h) {
+            const int64_t t = tb + 8 * h;
+            if (t < t1) out_o[(t - t0) * n + j] = v[h];
+        }
+    }
+    if (out_i) {
+        const int32_t k0 = in_off[j], k1 = in_off[j + 1];
+        double sm[P];
+#pragma unroll
+        for (int h = 0; h < P; ++h) sm[h] = 0.0;
+        for (int32_t k = k0; k < k1; ++k) {
+            const int64_t u = upos[k];
+#pragma unroll
+            for (int h = 0; h < P; ++h) {
+                const int64_t t = tb + 8 * h;
+                if (t < t1) sm[h] = sm[h] + S[(t - t0) * ns + u];
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < P; ++h) {
+            const int64_t t = tb + 8 * h;
+            if (t < t1) out_i[(t - t0) * n + j] = sm[h];
+        }
     }
 }
 
-__global__ void take_index(const int64_t* __restrict__ src, const int64_t* __restrict__ idx,
-                           int64_t m, int64_t* __restrict__ dst) {
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m;
-         k += (int64_t)gridDim.x * blockDim.x)
-        dst[k] = src[idx[k]];
+// window index of step 0 of every node slot (-1: padding and never-processed slots)
+__global__ void slot_window_index(const int32_t* __restrict__ G, const uint8_t* __restrict__ flags,
+                                  const int32_t* __restrict__ wg_gmin,
+                                  const int64_t* __restrict__ wbase, int slots, int64_t ns,
+                                  int64_t* __restrict__ sjb) {
+    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < ns;
+         d += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t w = d / slots;
+        const uint8_t fl = flags[d];
+        sjb[d] = fl == kSlotUnrouted || fl == kSlotPad
+                     ? -1
+                     : wbase[w] + (int64_t)(G[d] - wg_gmin[w]) * slots + (d - w * slots);
+    }
 }
 
 // out[j][t][e]
@@ -718,24 +761,39 @@ hipError_t launch_gather_steps(const double* O, int64_t mO, const int64_t* jbase
     return hipGetLastError();
 }
 
-hipError_t launch_gather_windows(const double* O, const int64_t* jbase, const int64_t* in_off,
-                                 const int64_t* ujb, int64_t stride, double* out_o,
-                                 double* out_i, int64_t n, int64_t t0, int64_t t1,
-                                 hipStream_t s) {
-    if (n <= 0 || t1 <= t0 || (!out_o && !out_i)) return hipSuccess;
-    const int64_t tiles = (n + 255) / 256;
-    if (tiles > 0x7fffffff || t1 - t0 > 65535) return hipErrorInvalidValue;
-    const int64_t blocks = (t1 - t0 + kGatherSteps - 1) / kGatherSteps;
-    hipLaunchKernelGGL(gather_windows, dim3((unsigned)tiles, (unsigned)blocks), 256, 0, s, O,
-                       jbase, in_off, ujb, stride, out_o, out_i, n, t0, t1);
+hipError_t launch_slot_window_index(const int32_t* G, const uint8_t* flags, const int32_t* wg_gmin,
+                                    const int64_t* wbase, int slots, int64_t ns, int64_t* sjb,
+                                    hipStream_t s) {
+    if (ns > 0)
+        hipLaunchKernelGGL(slot_window_index, grid_for(ns, 256), 256, 0, s, G, flags, wg_gmin,
+                           wbase, slots, ns, sjb);
     return hipGetLastError();
 }
 
-hipError_t launch_take_index(const int64_t* src, const int64_t* idx, int64_t m, int64_t* dst,
-                             hipStream_t s) {
-    if (m <= 0) return hipSuccess;
-    hipLaunchKernelGGL(take_index, grid_for(m, 256), 256, 0, s, src, idx, m, dst);
-    return hipGetLastError();
+hipError_t launch_gather_slots(const double* O, const int64_t* sjb, int64_t stride,
+                               const int32_t* pos, const int32_t* in_off, const int32_t* upos,
+                               double* out_o, double* out_i, int64_t n, int64_t ns, int64_t t0,
+                               int64_t t1, double* scratch, int64_t scratch_steps,
+                               hipStream_t s) {
+    if (n <= 0 || t1 <= t0 || (!out_o && !out_i)) return hipSuccess;
+    if (!scratch || scratch_steps < 1) return hipErrorInvalidValue;
+    const int64_t ntile = (n + 255) / 256;
+    for (int64_t c0 = t0; c0 < t1; c0 += scratch_steps) {
+        const int64_t c1 = std::min(t1, c0 + scratch_steps);
+        const int64_t sb = (c1 - c0 + kUnskewSteps - 1) / kUnskewSteps;
+        constexpr int P = kPermuteSteps;
+        const int64_t blocks = 8 * ntile * ((c1 - c0 + 8 * P - 1) / (8 * P));
+        if ((ns + 255) / 256 > 0x7fffffff || sb > 65535 || blocks > 0x7fffffff)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(unskew_windows, dim3((unsigned)((ns + 255) / 256), (unsigned)sb), 256,
+                           0, s, O, sjb, stride, scratch, ns, c0, c1);
+        hipLaunchKernelGGL(permute_steps, dim3((unsigned)blocks), 256, 0, s, scratch, pos, in_off,
+                           upos, out_o ? out_o + (c0 - t0) * n : nullptr,
+                           out_i ? out_i + (c0 - t0) * n : nullptr, n, ns, c0, c1, (int)ntile);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // one workgroup per row: strided partial sums, then an LDS tree (sums mod 2^64 are exact, so

@@ -267,16 +267,20 @@ hipError_t launch_row_digests(const double* rows, int64_t nrows, int64_t n, uint
                               hipStream_t s);
 
 // Both series of steps [t0, t1) in reach order, step-major, from the output windows (E = 1):
-// out_o[t - t0][j] = O[jbase[j] + t stride] (0 for jbase[j] < 0: a never-processed reach,
-// nutils.py:68), out_i[t - t0][j] = ((0 + O[ujb[k0] + t stride]) + ...) over j's inflow list
-// (in_off, rank order; ujb[k] = the window base of in_list[k]).  Either output may be NULL.
-hipError_t launch_gather_windows(const double* O, const int64_t* jbase, const int64_t* in_off,
-                                 const int64_t* ujb, int64_t stride, double* out_o,
-                                 double* out_i, int64_t n, int64_t t0, int64_t t1,
-                                 hipStream_t s);
-// dst[k] = src[idx[k]]
-hipError_t launch_take_index(const int64_t* src, const int64_t* idx, int64_t m, int64_t* dst,
-                             hipStream_t s);
+// out_o[t - t0][j] = O[sjb[pos[j]] + t stride] (0 for a never-processed reach, nutils.py:68),
+// out_i[t - t0][j] = ((0 + o[t][u1]) + ...) over j's inflow list (in_off, rank order; upos[k] =
+// pos[in_list[k]]).  Either output may be NULL.  Two passes through `scratch` (scratch_steps x
+// ns doubles: the steps of a pass in slot order, kernels.hip unskew_windows / permute_steps).
+// sjb: launch_slot_window_index.
+hipError_t launch_gather_slots(const double* O, const int64_t* sjb, int64_t stride,
+                               const int32_t* pos, const int32_t* in_off, const int32_t* upos,
+                               double* out_o, double* out_i, int64_t n, int64_t ns, int64_t t0,
+                               int64_t t1, double* scratch, int64_t scratch_steps,
+                               hipStream_t s);
+// sjb[d] = window index of step 0 of node slot d (-1: padding / never-processed slots)
+hipError_t launch_slot_window_index(const int32_t* G, const uint8_t* flags, const int32_t* wg_gmin,
+                                    const int64_t* wbase, int slots, int64_t ns, int64_t* sjb,
+                                    hipStream_t s);
 
 hipError_t launch_gather_series(const double* O, int64_t mO, const int64_t* jbase,
                                 const int64_t* in_off, const int64_t* in_list, bool inflow,
