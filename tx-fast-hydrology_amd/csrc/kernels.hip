@@ -520,8 +520,10 @@ __global__ __launch_bounds__(256) void unskew_windows(const double* __restrict__
 }
 
 // kPermuteSteps steps per thread (t, t + 8, ...: all on the thread's XCD), so the index loads
-// are shared: 2 measured 1.04 ms for both Texas series, 1 1.07, 4 1.27; non-temporal index loads
-// and series stores 1.26-1.42 (same box)
+// are shared, and non-temporal series stores (they pass the L2 that holds the steps' rows):
+// 0.97 ms for both Texas series (same box: plain stores 1.04, one step per thread 1.04-1.07,
+// four 1.27, non-temporal index loads too 1.26; non-temporal scratch stores in the first pass
+// within noise)
 constexpr int kPermuteSteps = 2;
 __global__ __launch_bounds__(256) void permute_steps(
         const double* __restrict__ S, const int32_t* __restrict__ pos,
@@ -529,6 +531,7 @@ __global__ __launch_bounds__(256) void permute_steps(
         double* __restrict__ out_o, double* __restrict__ out_i, int64_t n, int64_t ns,
         int64_t t0, int64_t t1, int ntile) {
     constexpr int P = kPermuteSteps;
+    auto st = [](double v, double* p) { __builtin_nontemporal_store(v, p); };
     const int x = (int)(blockIdx.x & 7);
     const int64_t q = blockIdx.x >> 3;
     const int64_t tb = t0 + (q / ntile) * 8 * P + x;     // steps tb, tb + 8, ... (P of them)
@@ -545,7 +548,7 @@ __global__ __launch_bounds__(256) void permute_steps(
 #pragma unroll
         for (int h = 0; h < P; ++h) {
             const int64_t t = tb + 8 * h;
-            if (t < t1) out_o[(t - t0) * n + j] = v[h];
+            if (t < t1) st(v[h], out_o + (t - t0) * n + j);
         }
     }
     if (out_i) {
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(256) void permute_steps(
 #pragma unroll
         for (int h = 0; h < P; ++h) {
             const int64_t t = tb + 8 * h;
-            if (t < t1) out_i[(t - t0) * n + j] = sm[h];
+            if (t < t1) st(sm[h], out_i + (t - t0) * n + j);
         }
     }
 }
